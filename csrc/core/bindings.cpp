@@ -1,0 +1,108 @@
+// pybind11 bindings for the native scheduler core and the HBM arena.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../runtime/arena.h"
+#include "scheduler.h"
+
+namespace py = pybind11;
+
+PYBIND11_MODULE(_dlsched_core, m) {
+  m.doc() = "Native DAG scheduling core + HBM arena (distributed_llm_scheduler_amd)";
+
+  py::class_<dls::Instance>(m, "Instance")
+      .def(py::init<>())
+      .def_readwrite("task_ids", &dls::Instance::task_ids)
+      .def_readwrite("mem", &dls::Instance::mem)
+      .def_readwrite("compute", &dls::Instance::compute)
+      .def_readwrite("deps", &dls::Instance::deps)
+      .def_readwrite("params", &dls::Instance::params)
+      .def_readwrite("param_names", &dls::Instance::param_names)
+      .def_readwrite("param_cost", &dls::Instance::param_cost)
+      .def_readwrite("node_ids", &dls::Instance::node_ids)
+      .def_readwrite("node_mem", &dls::Instance::node_mem)
+      .def_readwrite("node_speed", &dls::Instance::node_speed)
+      .def_readwrite("out_size", &dls::Instance::out_size)
+      .def_readwrite("link_bw", &dls::Instance::link_bw)
+      .def_readwrite("link_lat", &dls::Instance::link_lat)
+      .def_readwrite("load_bw", &dls::Instance::load_bw);
+
+  py::class_<dls::NodeResult>(m, "NodeResult")
+      .def_readonly("available_memory", &dls::NodeResult::available_memory)
+      .def_readonly("cached", &dls::NodeResult::cached)
+      .def_readonly("completed", &dls::NodeResult::completed)
+      .def_readonly("last_used", &dls::NodeResult::last_used);
+
+  py::class_<dls::Result>(m, "Result")
+      .def_readonly("assigned_node", &dls::Result::assigned_node)
+      .def_readonly("completed", &dls::Result::completed)
+      .def_readonly("failed", &dls::Result::failed)
+      .def_readonly("node_first_use_order", &dls::Result::node_first_use_order)
+      .def_readonly("schedule", &dls::Result::schedule)
+      .def_readonly("nodes", &dls::Result::nodes)
+      .def_readonly("rounds", &dls::Result::rounds)
+      .def_readonly("param_usage_count", &dls::Result::param_usage_count)
+      .def_readonly("param_last_used", &dls::Result::param_last_used)
+      .def_readonly("time_step", &dls::Result::time_step)
+      .def_readonly("start_time", &dls::Result::start_time)
+      .def_readonly("finish_time", &dls::Result::finish_time)
+      .def_property_readonly("events", [](const dls::Result& r) {
+        py::list out;
+        for (const auto& e : r.events) out.append(py::make_tuple(e.round, e.action, e.node, e.item));
+        return out;
+      });
+
+  m.def(
+      "run_policy",
+      [](const dls::Instance& inst, int policy) {
+        py::gil_scoped_release nogil;
+        return dls::run_policy(inst, static_cast<dls::Policy>(policy));
+      },
+      py::arg("instance"), py::arg("policy"));
+  m.def(
+      "replay_with_deps",
+      [](const dls::Instance& inst, const std::vector<std::vector<int>>& schedule, bool with_transfers) {
+        std::vector<double> s, f;
+        dls::replay_with_deps(inst, schedule, s, f, with_transfers);
+        return py::make_tuple(s, f);
+      },
+      py::arg("instance"), py::arg("schedule"), py::arg("with_transfers") = true);
+  m.def("depth_from_sources", &dls::depth_from_sources);
+  m.def("bottom_level", &dls::bottom_level);
+
+  m.attr("POLICY_DFS") = static_cast<int>(dls::Policy::DFS);
+  m.attr("POLICY_GREEDY") = static_cast<int>(dls::Policy::GREEDY);
+  m.attr("POLICY_CRITICAL") = static_cast<int>(dls::Policy::CRITICAL);
+  m.attr("POLICY_MRU") = static_cast<int>(dls::Policy::MRU);
+  m.attr("POLICY_EFT") = static_cast<int>(dls::Policy::EFT);
+  m.attr("ACTION_RUN") = static_cast<int>(dls::Action::RUN);
+  m.attr("ACTION_LOAD") = static_cast<int>(dls::Action::LOAD);
+  m.attr("ACTION_EVICT") = static_cast<int>(dls::Action::EVICT);
+  m.attr("ACTION_FAIL") = static_cast<int>(dls::Action::FAIL);
+
+  py::class_<dls::Arena>(m, "Arena")
+      .def(py::init<uint64_t, uint64_t>(), py::arg("capacity"), py::arg("align") = 256)
+      .def("alloc", &dls::Arena::alloc)
+      .def("release", &dls::Arena::release)
+      .def_property_readonly("capacity", &dls::Arena::capacity)
+      .def_property_readonly("used", &dls::Arena::used)
+      .def_property_readonly("peak", &dls::Arena::peak)
+      .def_property_readonly("largest_free", &dls::Arena::largest_free)
+      .def_property_readonly("num_free_blocks", &dls::Arena::num_free_blocks)
+      .def_property_readonly("num_live", &dls::Arena::num_live)
+      .def("reset_peak", &dls::Arena::reset_peak);
+
+  py::class_<dls::ParamCache>(m, "ParamCache")
+      .def(py::init<dls::Arena*>(), py::keep_alive<1, 2>())
+      .def("resident", &dls::ParamCache::resident)
+      .def("offset", &dls::ParamCache::offset)
+      .def("acquire", &dls::ParamCache::acquire, py::arg("param"), py::arg("bytes"), py::arg("allow_evict") = true)
+      .def("evict", &dls::ParamCache::evict)
+      .def("pin", &dls::ParamCache::pin)
+      .def("residents", &dls::ParamCache::residents)
+      .def_property_readonly("hits", &dls::ParamCache::hits)
+      .def_property_readonly("misses", &dls::ParamCache::misses)
+      .def_property_readonly("evictions", &dls::ParamCache::evictions)
+      .def_property_readonly("reloads", &dls::ParamCache::reloads)
+      .def_property_readonly("bytes_filled", &dls::ParamCache::bytes_filled);
+}

@@ -1,0 +1,118 @@
+"""In-tree native build: the C++ scheduling core (g++) and the HIP/CDNA4 kernels (hipcc).
+
+Everything is compiled with explicit compiler command lines (no hipify, no JIT cache
+under ~/.cache) so the produced ``.so`` files live inside the package directory and
+travel with the repository snapshot to the GPU box.
+
+* ``_dlsched_core*.so`` — csrc/core + csrc/runtime, pure C++17 + pybind11.
+* ``_dlsched_ops*.so``  — csrc/kernels/*.hip compiled for ``--offload-arch=gfx950``
+  plus a torch binding translation unit; it links against torch's bundled
+  ``libamdhip64.so.7`` (same soname as /opt/rocm's, resolved to the already-loaded one).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO, "csrc")
+BUILD_DIR = os.path.join(REPO, "build", "native")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("DLS_OFFLOAD_ARCH", "gfx950")
+
+CORE_SO = os.path.join(PKG_DIR, "_dlsched_core" + EXT)
+OPS_SO = os.path.join(PKG_DIR, "_dlsched_ops" + EXT)
+
+
+def _newer(out: str, srcs) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build_core(force: bool = False, verbose: bool = False) -> str:
+    import pybind11
+
+    srcs = sorted(glob.glob(os.path.join(CSRC, "core", "*.cpp")) + glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "core", "*.h")) + glob.glob(os.path.join(CSRC, "runtime", "*.h")))
+    if not force and not _newer(CORE_SO, srcs + hdrs):
+        return CORE_SO
+    cmd = [
+        os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
+        "-Wall", "-Wno-sign-compare",
+        f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+        *srcs, "-o", CORE_SO + ".tmp",
+    ]
+    _run(cmd, verbose)
+    os.replace(CORE_SO + ".tmp", CORE_SO)
+    return CORE_SO
+
+
+def _torch_flags():
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    inc = [f"-I{p}" for p in ce.include_paths()] + [f"-I{sysconfig.get_paths()['include']}"]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    defs = [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_dlsched_ops",
+            "-DTORCH_API_INCLUDE_EXTENSION_H", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1"]
+    libdir = ce.library_paths()[0]
+    libs = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+            "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+    return inc, defs, libs
+
+
+def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
+    """Compile every csrc/kernels/*.hip for gfx950 and link the torch op library."""
+    kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    binding = os.path.join(CSRC, "kernels", "ops_binding.cpp")
+    if not force and not _newer(OPS_SO, kern + hdrs + [binding]):
+        return OPS_SO
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    inc, defs, libs = _torch_flags()
+    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+              f"-I{os.path.join(CSRC, 'kernels')}"]
+
+    def compile_kernel(src):
+        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        if force or _newer(obj, [src] + hdrs):
+            _run([hipcc, *common, "-c", src, "-o", obj], verbose)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(compile_kernel, kern))
+    bobj = os.path.join(BUILD_DIR, "ops_binding.o")
+    if force or _newer(bobj, [binding] + hdrs):
+        _run([hipcc, "-O2", "-std=c++17", "-fPIC", *inc, *defs, f"-I{os.path.join(CSRC, 'kernels')}",
+              "-x", "c++", "-c", binding, "-o", bobj], verbose)
+    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, bobj, *libs, "-o", OPS_SO + ".tmp"], verbose)
+    os.replace(OPS_SO + ".tmp", OPS_SO)
+    return OPS_SO
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_core(force=force, verbose=verbose)
+    if glob.glob(os.path.join(CSRC, "kernels", "*.hip")):
+        build_ops(force=force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, verbose=True)
