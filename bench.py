@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: GPT-2 operator DAG placed by the scheduler onto N MI355X GPUs and
+executed by the native executor (HIP kernels, RCCL p2p for cross-GPU edges).
+
+Metric (BASELINE.json): "DAG makespan (ms) + tasks completed under mem cap, GPT-2 DAG at
+1/2/4/8 MI355X". One step = executing the whole placed DAG once: N request replicas of
+the reference's GPT-2-small DAG (99 tasks each, batch 1 x 512 tokens — test_gpt2.py:53),
+random-init bf16 weights, synthetic token ids. Weak scaling: one 512-token request per GPU.
+``value`` is the step makespan in ms (max over ranks); lower is better.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_llm_scheduler_amd.parallel import runtime  # noqa: E402
+
+METRIC = "DAG makespan (ms) + tasks completed under mem cap, GPT-2 DAG at 1/2/4/8 MI355X"
+# Reference GPT-2 DAG makespan, N=1 at 100% memory, all four policies: 3.330 (abstract)
+# seconds (the reference simulates, it never executes).
+REF_MAKESPAN_MS = 3330.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--scheduler", default="EFT")
+    ap.add_argument("--replicas-per-gpu", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--cap-gb", type=float, default=288.0, help="per-GPU HBM budget for parameters")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-fuse", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="also print a measured per-kernel timeline")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    gpu = torch.cuda.is_available()
+    device = torch.device(f"cuda:{local}") if gpu else torch.device("cpu")
+    if gpu:
+        torch.cuda.set_device(device)
+    pg = None
+    if world > 1:
+        dist.init_process_group("nccl" if gpu else "gloo", rank=rank, world_size=world,
+                                **({"device_id": device} if gpu else {}))
+        pg = dist.group.WORLD
+
+    replicas = world * args.replicas_per_gpu
+    t0 = time.time()
+    plan = runtime.plan(args.model, world=world, scheduler=args.scheduler, cap_gb=args.cap_gb, replicas=replicas,
+                        batch=args.batch, seq=args.seq, cost_model="bytes", fuse=not args.no_fuse)
+    log(f"[bench] rank {rank}: planned {plan.stats['tasks_completed']}/{plan.stats['tasks_total']} tasks in "
+        f"{(time.time() - t0) * 1e3:.1f} ms; {plan.stats}")
+    ex = runtime.make_executor(plan, rank, device, pg=pg, use_graph=not args.no_graph)
+
+    def sync():
+        if gpu:
+            torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        ex.step()
+    sync()
+    captured = ex.capture() if not args.no_graph else False
+    if captured:
+        ex.step()
+    sync()
+    log(f"[bench] rank {rank}: warmup done ({args.warmup} steps, hipGraph={captured})")
+
+    sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        ex.step()
+    sync()
+    elapsed = time.perf_counter() - t_start
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device if world > 1 and gpu else "cpu")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+
+    timeline = None
+    if args.profile:
+        st = ex.step(profile=True)
+        timeline = [(tid, round(a, 4), round(b, 4)) for tid, a, b in st.timeline]
+
+    if rank == 0:
+        tokens = replicas * args.batch * args.seq
+        out = {
+            "metric": METRIC,
+            "value": round(ms_per_step, 5),
+            "unit": "ms",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": round(ms_per_step / REF_MAKESPAN_MS, 7),
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {"model": {"gpt2": "gpt2-small"}.get(args.model, args.model), "global_batch": replicas * args.batch, "seq_len": args.seq,
+                       "parallelism": f"dag-placement x{world} ({plan.scheduler_name}, {replicas} request DAGs)"},
+            "tasks_completed": plan.stats["tasks_completed"],
+            "tasks_total": plan.stats["tasks_total"],
+            "mem_cap_gb_per_gpu": args.cap_gb,
+            "scheduler": plan.scheduler_name,
+            "tokens_per_s": round(tokens / (ms_per_step / 1e3), 1),
+            "kernels_per_rank": plan.stats["kernels_per_rank"],
+            "cross_gpu_edges": plan.stats["cross_gpu_edges"],
+            "hip_graph": bool(captured),
+            "weights": "random-init",
+            "baseline_note": "vs_baseline = measured ms / reference simulated makespan 3330 (abstract s x1e3) "
+                             "for the same GPT-2 DAG at 100% memory (BASELINE.md §2.3)",
+        }
+        if timeline is not None:
+            out["timeline_ms"] = timeline
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

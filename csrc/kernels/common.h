@@ -1,0 +1,82 @@
+// Shared CDNA4 (gfx950) helpers for the hand-written kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave64: lane = threadIdx.x & 63, wave = threadIdx.x >> 6; block sizes are
+//    multiples of 64.
+//  * bf16 storage as clang's native __bf16; math in fp32. Conversions use plain casts,
+//    which hipcc lowers to v_cvt_pk_bf16_f32 (NaN-preserving, RNE).
+//  * global memory is touched in 16-byte vectors (8 x bf16) wherever the layout allows
+//    (cdna_hip_programming.md Guideline 13: scalar bf16 loads cost 2-2.5x).
+//  * MFMA: __builtin_amdgcn_mfma_f32_16x16x32_bf16. Operand maps (lane l):
+//      A[row l&15][k 8*(l>>4)+j], B[k 8*(l>>4)+j][col l&15], j = 0..7
+//      C/D[row 4*(l>>4)+i][col l&15], i = 0..3
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define DLS_WAVE 64
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+__device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reductions inside aligned groups of 16 lanes (one MFMA 16x16 column group)
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  // 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))) == x * sigmoid(2u)
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return x / (1.0f + __expf(-2.0f * u));
+}
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// consecutive logical tiles land on the same XCD (blocks b, b+8, ... share one), so
+// neighbouring output tiles that share operand panels hit the same private L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  if (nwg <= 8) return orig;
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8, idx = orig / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+enum DlsAct : int { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_SILU = 2, ACT_RELU = 3 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case ACT_GELU_TANH: return gelu_tanh(v);
+    case ACT_SILU: return silu(v);
+    case ACT_RELU: return fmaxf(v, 0.f);
+    default: return v;
+  }
+}

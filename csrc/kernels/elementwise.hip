@@ -1,0 +1,128 @@
+// Memory-bound element-wise kernels: GELU(tanh), residual add, SwiGLU, token+position
+// embedding gather, rotary embedding. All move 16-byte (8 x bf16) vectors per lane and
+// grid-stride over at most 256 CUs x 8 blocks (cdna_hip_programming.md Guideline 11,13).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+inline int grid_for(int64_t n_vec) {
+  int64_t g = (n_vec + 255) / 256;
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
+__global__ __launch_bounds__(256) void gelu_kernel(const bf16x8* __restrict__ x, bf16x8* __restrict__ y,
+                                                   int64_t nvec) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const bf16x8 a = x[i];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_tanh(bf2f(a[e])));
+    y[i] = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void add_kernel(const bf16x8* __restrict__ a, const bf16x8* __restrict__ b,
+                                                  bf16x8* __restrict__ y, int64_t nvec) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const bf16x8 u = a[i], v = b[i];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(u[e]) + bf2f(v[e]));
+    y[i] = o;
+  }
+}
+
+// gu [M][2F] = [gate | up] -> y [M][F] = silu(gate) * up
+__global__ __launch_bounds__(256) void swiglu_kernel(const bf16* __restrict__ gu, bf16* __restrict__ y, int M,
+                                                     int F) {
+  const int fv = F / 8;
+  const int64_t nvec = (int64_t)M * fv;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / fv, c = i % fv;
+    const bf16x8 g = reinterpret_cast<const bf16x8*>(gu + m * 2 * F)[c];
+    const bf16x8 u = reinterpret_cast<const bf16x8*>(gu + m * 2 * F + F)[c];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(bf2f(g[e])) * bf2f(u[e]));
+    reinterpret_cast<bf16x8*>(y + m * F)[c] = o;
+  }
+}
+
+// y[m] = wte[tok[m]] + wpe[m % S] (wpe may be null: token embedding only)
+__global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restrict__ tok,
+                                                        const bf16* __restrict__ wte,
+                                                        const bf16* __restrict__ wpe, bf16* __restrict__ y, int M,
+                                                        int S, int H) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int t = tok[row];
+  const bf16x8* er = reinterpret_cast<const bf16x8*>(wte + (size_t)t * H);
+  const bf16x8* pr = wpe ? reinterpret_cast<const bf16x8*>(wpe + (size_t)(row % S) * H) : nullptr;
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * H);
+  for (int c = lane; c < H / 8; c += 64) {
+    bf16x8 a = er[c];
+    if (pr) {
+      const bf16x8 p = pr[c];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] = f2bf(bf2f(a[e]) + bf2f(p[e]));
+    }
+    yr[c] = a;
+  }
+}
+
+// Rotary embedding (rotate-half convention), in place on the q heads (columns
+// [0, n_head*D)) and k heads (columns [k_col, k_col + n_kv*D)) of each token row.
+// cos/sin tables [S][D/2] fp32 are precomputed on the host (no on-device trig).
+__global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, int ld, int M, int S, int n_head,
+                                                   int n_kv, int D, int k_col, const float* __restrict__ cos_t,
+                                                   const float* __restrict__ sin_t) {
+  const int half = D / 2;
+  const int heads = n_head + n_kv;
+  const int64_t total = (int64_t)M * heads * half;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int j = (int)(i % half);
+    const int64_t t = i / half;
+    const int hh = (int)(t % heads);
+    const int m = (int)(t / heads);
+    const int pos = m % S;
+    const int col = hh < n_head ? hh * D : k_col + (hh - n_head) * D;
+    bf16* base = qkv + (size_t)m * ld + col;
+    const float c = cos_t[pos * half + j], s = sin_t[pos * half + j];
+    const float x1 = bf2f(base[j]), x2 = bf2f(base[j + half]);
+    base[j] = f2bf(x1 * c - x2 * s);
+    base[j + half] = f2bf(x2 * c + x1 * s);
+  }
+}
+
+}  // namespace
+
+void launch_gelu(const void* x, void* y, int64_t n, hipStream_t s) {
+  const int64_t nv = n / 8;
+  hipLaunchKernelGGL(gelu_kernel, dim3(grid_for(nv)), dim3(256), 0, s, (const bf16x8*)x, (bf16x8*)y, nv);
+}
+
+void launch_add(const void* a, const void* b, void* y, int64_t n, hipStream_t s) {
+  const int64_t nv = n / 8;
+  hipLaunchKernelGGL(add_kernel, dim3(grid_for(nv)), dim3(256), 0, s, (const bf16x8*)a, (const bf16x8*)b,
+                     (bf16x8*)y, nv);
+}
+
+void launch_swiglu(const void* gu, void* y, int M, int F, hipStream_t s) {
+  hipLaunchKernelGGL(swiglu_kernel, dim3(grid_for((int64_t)M * F / 8)), dim3(256), 0, s, (const bf16*)gu,
+                     (bf16*)y, M, F);
+}
+
+void launch_embedding(const int32_t* tokens, const void* wte, const void* wpe, void* y, int M, int S, int H,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(embedding_kernel, dim3((M + 3) / 4), dim3(256), 0, s, tokens, (const bf16*)wte,
+                     (const bf16*)wpe, (bf16*)y, M, S, H);
+}
+
+void launch_rope(void* qkv, int ld, int M, int S, int n_head, int n_kv_head, int D, int k_col, const float* cos_t,
+                 const float* sin_t, hipStream_t s) {
+  const int64_t total = (int64_t)M * (n_head + n_kv_head) * (D / 2);
+  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(total / 8 + 1)), dim3(256), 0, s, (bf16*)qkv, ld, M, S, n_head,
+                     n_kv_head, D, k_col, cos_t, sin_t);
+}

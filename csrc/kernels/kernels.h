@@ -1,0 +1,63 @@
+// Host-side launchers for the HIP/CDNA4 kernels (raw pointers + hipStream_t, so the
+// torch binding translation unit does not need the device compiler's headers).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+struct GemmArgs {
+  const void* A;  // bf16 [M][lda]
+  int lda;
+  const void* W;  // bf16 [N][ldw]
+  int ldw;
+  void* C;        // bf16 [M][ldc]
+  int ldc;
+  const void* bias;  // bf16 [N] or nullptr
+  const void* R;     // bf16 [M][ldr] residual or nullptr
+  int ldr;
+  int M, N, K;
+  int act;       // DlsAct
+  float alpha;
+  int config;    // -1 = auto
+};
+
+int gemm_pick_config(int M, int N, int K);
+void launch_gemm_bf16(const GemmArgs& a, hipStream_t s);
+
+struct AttnArgs {
+  const void* q; int ldq;   // bf16, row = token (b*S + s), head h at column h*D
+  const void* k; int ldk;   // kv head g at column g*D
+  const void* v; int ldv;
+  void* o; int ldo;         // bf16 output, head h at column h*D
+  int B, S, n_head, n_kv_head, D;
+  float scale;
+  int causal;
+};
+void launch_attention_fwd(const AttnArgs& a, hipStream_t s);
+
+// y = LN(x [+ r]) * w + b ; if r != nullptr and sum_out != nullptr, sum_out = x + r
+void launch_layernorm(const void* x, const void* r, void* sum_out, const void* w, const void* b, void* y, int M,
+                      int H, float eps, hipStream_t s);
+void launch_rmsnorm(const void* x, const void* r, void* sum_out, const void* w, void* y, int M, int H, float eps,
+                    hipStream_t s);
+
+void launch_gelu(const void* x, void* y, int64_t n, hipStream_t s);
+void launch_add(const void* a, const void* b, void* y, int64_t n, hipStream_t s);
+void launch_swiglu(const void* gu, void* y, int M, int F, hipStream_t s);  // gu [M][2F] (gate|up)
+void launch_embedding(const int32_t* tokens, const void* wte, const void* wpe, void* y, int M, int S, int H,
+                      hipStream_t s);
+// in-place rotary embedding on the q and k head slices of a packed qkv row buffer
+void launch_rope(void* qkv, int ld, int M, int S, int n_head, int n_kv_head, int D, int k_col, const float* cos_t,
+                 const float* sin_t, hipStream_t s);
+
+// MoE
+void launch_moe_router(const void* logits, int M, int E, int topk, int32_t* topk_idx, float* topk_w,
+                       hipStream_t s);
+void launch_moe_align(const int32_t* topk_idx, int M, int topk, int E, int32_t* src_rows, int32_t* slot_of,
+                      int32_t* offsets, hipStream_t s);
+void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int rows, int H, hipStream_t s);
+void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
+                        int topk, int H, hipStream_t s);
+// X [rows][K] sorted by expert, offsets [E+1], W [E][N][K] -> Y [rows][N]
+void launch_grouped_gemm(const void* X, const int32_t* offsets, const void* W, void* Y, int E, int N, int K,
+                         int max_rows, int act, hipStream_t s);

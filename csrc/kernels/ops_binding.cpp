@@ -1,0 +1,275 @@
+// torch bindings for the hand-written HIP/CDNA4 kernels (module _dlsched_ops).
+//
+// Every op validates device / dtype / layout on the host before launching (a kernel
+// that indexes past its operands can take the whole node down), launches on torch's
+// current HIP stream (so the executor's stream and hipGraph capture apply), and
+// allocates outputs through torch's caching allocator unless the caller passes `out`
+// (the executor passes views into its HBM arena).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_bf16(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+
+// 2-D view [rows][cols] with unit column stride and 16-B aligned rows
+void check_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have contiguous rows");
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+at::Tensor as2d(const at::Tensor& t) { return t.dim() == 2 ? t : t.reshape({-1, t.size(-1)}); }
+
+at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                const c10::optional<at::Tensor>& residual, int64_t act, double alpha,
+                const c10::optional<at::Tensor>& out, int64_t config) {
+  check_bf16(a_in, "A");
+  check_bf16(w, "W");
+  at::Tensor a = as2d(a_in);
+  check_rows(a, "A");
+  check_rows(w, "W");
+  const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K, "W must be [N][K] with K = ", K, ", got ", w.sizes());
+  TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8");
+  at::Tensor c;
+  if (out.has_value()) {
+    c = as2d(*out);
+    check_bf16(c, "out");
+    TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1, "out must be [M][N]");
+  } else {
+    c = at::empty({M, N}, a.options());
+  }
+  const void* bptr = nullptr;
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N, "bias must be contiguous [N]");
+    bptr = bias->data_ptr();
+  }
+  const void* rptr = nullptr;
+  int ldr = 0;
+  if (residual.has_value()) {
+    at::Tensor r = as2d(*residual);
+    check_bf16(r, "residual");
+    TORCH_CHECK(r.size(0) == M && r.size(1) == N && r.stride(1) == 1, "residual must be [M][N]");
+    rptr = r.data_ptr();
+    ldr = (int)r.stride(0);
+  }
+  if (M == 0 || N == 0) return c;
+  GemmArgs g{a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0), c.data_ptr(), (int)c.stride(0),
+             bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, (int)config};
+  launch_gemm_bf16(g, cur_stream());
+  return c;
+}
+
+at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
+                     int64_t n_head, int64_t n_kv_head, int64_t head_dim, bool causal, double scale,
+                     const c10::optional<at::Tensor>& out) {
+  for (auto* p : {&q, &k, &v}) {
+    check_bf16(*p, "qkv");
+    check_rows(*p, "qkv");
+    TORCH_CHECK(p->size(0) == B * S, "q/k/v must have B*S rows");
+  }
+  TORCH_CHECK(head_dim == 64 || head_dim == 128, "head_dim must be 64 or 128");
+  TORCH_CHECK(n_head % n_kv_head == 0, "n_head must be a multiple of n_kv_head");
+  TORCH_CHECK(q.size(1) >= n_head * head_dim && k.size(1) >= n_kv_head * head_dim &&
+                  v.size(1) >= n_kv_head * head_dim,
+              "q/k/v column extent too small for the head layout");
+  at::Tensor o = out.has_value() ? as2d(*out) : at::empty({B * S, n_head * head_dim}, q.options());
+  check_rows(o, "out");
+  AttnArgs a{q.data_ptr(), (int)q.stride(0), k.data_ptr(), (int)k.stride(0), v.data_ptr(), (int)v.stride(0),
+             o.data_ptr(), (int)o.stride(0), (int)B, (int)S, (int)n_head, (int)n_kv_head, (int)head_dim,
+             (float)scale, causal ? 1 : 0};
+  launch_attention_fwd(a, cur_stream());
+  return o;
+}
+
+std::vector<at::Tensor> norm(const at::Tensor& x_in, const at::Tensor& w, const c10::optional<at::Tensor>& b,
+                             double eps, const c10::optional<at::Tensor>& residual, bool rms,
+                             const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& sum_out) {
+  check_bf16(x_in, "x");
+  at::Tensor x = as2d(x_in).contiguous();
+  const int64_t M = x.size(0), H = x.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "hidden size must be a multiple of 8 and <= 8192");
+  check_bf16(w, "weight");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == H, "weight must be contiguous [H]");
+  if (b.has_value()) {
+    check_bf16(*b, "bias");
+    TORCH_CHECK(b->is_contiguous() && b->numel() == H, "bias must be contiguous [H]");
+  }
+  at::Tensor y = out.has_value() ? as2d(*out) : at::empty({M, H}, x.options());
+  TORCH_CHECK(y.is_contiguous(), "out must be contiguous");
+  at::Tensor r, s;
+  if (residual.has_value()) {
+    r = as2d(*residual).contiguous();
+    check_bf16(r, "residual");
+    TORCH_CHECK(r.sizes() == x.sizes(), "residual must match x");
+    s = sum_out.has_value() ? as2d(*sum_out) : at::empty({M, H}, x.options());
+    TORCH_CHECK(s.is_contiguous(), "sum_out must be contiguous");
+  }
+  if (M == 0) return {y, s};
+  if (rms)
+    launch_rmsnorm(x.data_ptr(), r.defined() ? r.data_ptr() : nullptr, s.defined() ? s.data_ptr() : nullptr,
+                   w.data_ptr(), y.data_ptr(), (int)M, (int)H, (float)eps, cur_stream());
+  else
+    launch_layernorm(x.data_ptr(), r.defined() ? r.data_ptr() : nullptr, s.defined() ? s.data_ptr() : nullptr,
+                     w.data_ptr(), b.has_value() ? b->data_ptr() : nullptr, y.data_ptr(), (int)M, (int)H,
+                     (float)eps, cur_stream());
+  return {y, s};
+}
+
+at::Tensor gelu(const at::Tensor& x, const c10::optional<at::Tensor>& out) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "x must be contiguous with numel % 8 == 0");
+  at::Tensor y = out.has_value() ? *out : at::empty_like(x);
+  TORCH_CHECK(y.is_contiguous() && y.numel() == x.numel(), "out mismatch");
+  launch_gelu(x.data_ptr(), y.data_ptr(), x.numel(), cur_stream());
+  return y;
+}
+
+at::Tensor add(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& out) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && a.numel() == b.numel() && a.numel() % 8 == 0,
+              "add operands must be contiguous, equal-sized, numel % 8 == 0");
+  at::Tensor y = out.has_value() ? *out : at::empty_like(a);
+  TORCH_CHECK(y.is_contiguous() && y.numel() == a.numel(), "out mismatch");
+  launch_add(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream());
+  return y;
+}
+
+at::Tensor swiglu(const at::Tensor& gu_in, const c10::optional<at::Tensor>& out) {
+  check_bf16(gu_in, "gate_up");
+  at::Tensor gu = as2d(gu_in).contiguous();
+  const int64_t M = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(gu.size(1) % 16 == 0, "gate_up width must be 2F with F % 8 == 0");
+  at::Tensor y = out.has_value() ? as2d(*out) : at::empty({M, F}, gu.options());
+  TORCH_CHECK(y.is_contiguous() && y.size(0) == M && y.size(1) == F, "out mismatch");
+  launch_swiglu(gu.data_ptr(), y.data_ptr(), (int)M, (int)F, cur_stream());
+  return y;
+}
+
+at::Tensor embedding(const at::Tensor& tokens, const at::Tensor& wte, const c10::optional<at::Tensor>& wpe, int64_t S,
+                     const c10::optional<at::Tensor>& out) {
+  TORCH_CHECK(tokens.is_cuda() && tokens.scalar_type() == at::kInt && tokens.is_contiguous(),
+              "tokens must be contiguous int32 on the GPU");
+  check_bf16(wte, "wte");
+  TORCH_CHECK(wte.is_contiguous(), "wte must be contiguous");
+  const int64_t M = tokens.numel(), H = wte.size(1);
+  TORCH_CHECK(H % 8 == 0, "hidden size must be a multiple of 8");
+  if (wpe.has_value()) {
+    check_bf16(*wpe, "wpe");
+    TORCH_CHECK(wpe->is_contiguous() && wpe->size(1) == H && wpe->size(0) >= S, "wpe must be [>=S][H]");
+  }
+  at::Tensor y = out.has_value() ? as2d(*out) : at::empty({M, H}, wte.options());
+  TORCH_CHECK(y.is_contiguous() && y.size(0) == M && y.size(1) == H, "out mismatch");
+  launch_embedding(tokens.data_ptr<int32_t>(), wte.data_ptr(), wpe.has_value() ? wpe->data_ptr() : nullptr,
+                   y.data_ptr(), (int)M, (int)S, (int)H, cur_stream());
+  return y;
+}
+
+void rope_(at::Tensor& qkv, int64_t S, int64_t n_head, int64_t n_kv_head, int64_t head_dim, int64_t k_col,
+           const at::Tensor& cos_t, const at::Tensor& sin_t) {
+  check_bf16(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be a 2-D row buffer");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.numel() >= S * head_dim / 2,
+              "cos/sin tables must be contiguous fp32 [S][D/2]");
+  TORCH_CHECK(k_col + n_kv_head * head_dim <= qkv.size(1) && n_head * head_dim <= qkv.size(1), "head layout");
+  launch_rope(qkv.data_ptr(), (int)qkv.stride(0), (int)qkv.size(0), (int)S, (int)n_head, (int)n_kv_head,
+              (int)head_dim, (int)k_col, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), cur_stream());
+}
+
+std::vector<at::Tensor> moe_router(const at::Tensor& logits, int64_t topk) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits must be contiguous [M][E]");
+  const int64_t M = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(E <= 64 && topk >= 1 && topk <= 8 && topk <= E, "router supports E <= 64, 1 <= topk <= min(8, E)");
+  auto idx = at::empty({M, topk}, logits.options().dtype(at::kInt));
+  auto w = at::empty({M, topk}, logits.options().dtype(at::kFloat));
+  launch_moe_router(logits.data_ptr(), (int)M, (int)E, (int)topk, idx.data_ptr<int32_t>(), w.data_ptr<float>(),
+                    cur_stream());
+  return {idx, w};
+}
+
+std::vector<at::Tensor> moe_align(const at::Tensor& idx, int64_t E) {
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kInt && idx.dim() == 2 && idx.is_contiguous(),
+              "topk_idx must be contiguous int32 [M][k]");
+  const int64_t M = idx.size(0), k = idx.size(1);
+  auto opt = idx.options();
+  auto src = at::empty({M * k}, opt), slot = at::empty({M * k}, opt), off = at::empty({E + 1}, opt);
+  launch_moe_align(idx.data_ptr<int32_t>(), (int)M, (int)k, (int)E, src.data_ptr<int32_t>(),
+                   slot.data_ptr<int32_t>(), off.data_ptr<int32_t>(), cur_stream());
+  return {src, slot, off};
+}
+
+at::Tensor moe_permute(const at::Tensor& x, const at::Tensor& src_rows) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "x must be contiguous [M][H]");
+  TORCH_CHECK(src_rows.scalar_type() == at::kInt && src_rows.is_contiguous(), "src_rows must be int32");
+  auto out = at::empty({src_rows.numel(), x.size(1)}, x.options());
+  launch_moe_permute(x.data_ptr(), src_rows.data_ptr<int32_t>(), out.data_ptr(), (int)src_rows.numel(),
+                     (int)x.size(1), cur_stream());
+  return out;
+}
+
+at::Tensor moe_combine(const at::Tensor& eo, const at::Tensor& slot_of, const at::Tensor& w) {
+  check_bf16(eo, "expert_out");
+  TORCH_CHECK(eo.dim() == 2 && eo.is_contiguous() && eo.size(1) % 8 == 0, "expert_out must be contiguous [R][H]");
+  TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kFloat && w.is_contiguous(), "weights must be fp32 [M][k]");
+  TORCH_CHECK(slot_of.numel() == w.numel() && slot_of.scalar_type() == at::kInt, "slot_of mismatch");
+  const int64_t M = w.size(0), k = w.size(1), H = eo.size(1);
+  auto y = at::empty({M, H}, eo.options());
+  launch_moe_combine(eo.data_ptr(), slot_of.data_ptr<int32_t>(), w.data_ptr<float>(), y.data_ptr(), (int)M, (int)k,
+                     (int)H, cur_stream());
+  return y;
+}
+
+at::Tensor grouped_gemm(const at::Tensor& X, const at::Tensor& offsets, const at::Tensor& W, int64_t act) {
+  check_bf16(X, "X");
+  check_bf16(W, "W");
+  TORCH_CHECK(X.dim() == 2 && X.is_contiguous(), "X must be contiguous [rows][K]");
+  TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W must be contiguous [E][N][K]");
+  TORCH_CHECK(offsets.scalar_type() == at::kInt && offsets.numel() == W.size(0) + 1, "offsets must be int32 [E+1]");
+  const int64_t rows = X.size(0), K = X.size(1), E = W.size(0), N = W.size(1);
+  TORCH_CHECK(W.size(2) == K && K % 8 == 0, "W must be [E][N][K]");
+  auto Y = at::empty({rows, N}, X.options());
+  if (rows == 0) return Y;
+  launch_grouped_gemm(X.data_ptr(), offsets.data_ptr<int32_t>(), W.data_ptr(), Y.data_ptr(), (int)E, (int)N, (int)K,
+                      (int)rows, (int)act, cur_stream());
+  return Y;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "Hand-written HIP/CDNA4 (gfx950) kernels for distributed_llm_scheduler_amd";
+  m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),
+        py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1);
+  m.def("gemm_pick_config", &gemm_pick_config);
+  m.def("attention", &attention, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"),
+        py::arg("n_head"), py::arg("n_kv_head"), py::arg("head_dim"), py::arg("causal") = true,
+        py::arg("scale") = 0.125, py::arg("out") = py::none());
+  m.def("norm", &norm, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5,
+        py::arg("residual") = py::none(), py::arg("rms") = false, py::arg("out") = py::none(),
+        py::arg("sum_out") = py::none());
+  m.def("gelu", &gelu, py::arg("x"), py::arg("out") = py::none());
+  m.def("add", &add, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
+  m.def("swiglu", &swiglu, py::arg("gate_up"), py::arg("out") = py::none());
+  m.def("embedding", &embedding, py::arg("tokens"), py::arg("wte"), py::arg("wpe") = py::none(), py::arg("S") = 1,
+        py::arg("out") = py::none());
+  m.def("rope_", &rope_);
+  m.def("moe_router", &moe_router);
+  m.def("moe_align", &moe_align);
+  m.def("moe_permute", &moe_permute);
+  m.def("moe_combine", &moe_combine);
+  m.def("grouped_gemm", &grouped_gemm, py::arg("X"), py::arg("offsets"), py::arg("W"), py::arg("act") = 0);
+}

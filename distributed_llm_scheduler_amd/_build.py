@@ -101,7 +101,7 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
         objs = list(ex.map(compile_kernel, kern))
     bobj = os.path.join(BUILD_DIR, "ops_binding.o")
     if force or _newer(bobj, [binding] + hdrs):
-        _run([hipcc, "-O2", "-std=c++17", "-fPIC", *inc, *defs, f"-I{os.path.join(CSRC, 'kernels')}",
+        _run([hipcc, "-O2", "-std=c++17", "-fPIC", *inc, *defs, f"-I{os.path.join(CSRC, 'kernels')}", f"-I{ROCM}/include",
               "-x", "c++", "-c", binding, "-o", bobj], verbose)
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, bobj, *libs, "-o", OPS_SO + ".tmp"], verbose)
     os.replace(OPS_SO + ".tmp", OPS_SO)

@@ -1,0 +1,120 @@
+"""Parameter groups: scheduler parameter ids -> the real tensors behind them.
+
+The scheduler reasons about opaque parameter ids (``"layer_3_attn_qkv_weights"``); the
+executor needs bytes. A :class:`ParamGroup` lists the tensors one id stands for, in the
+layout the HIP kernels consume:
+
+* every GEMM weight is stored **[N][K] (K contiguous)**, bf16, so both MFMA operands of
+  ``y = x @ W^T`` stream K-contiguous rows (GPT-2's Conv1D stores [K][N]; the checkpoint
+  converter transposes once at load time, never per call);
+* norms/biases are bf16 vectors (the kernels accumulate in fp32).
+
+Initialisation is deterministic per tensor name (random-init weights of the named
+architecture; there are no checkpoints offline).
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+from typing import Dict, List, Tuple
+
+import torch
+
+
+@dataclass
+class TensorSpec:
+    name: str
+    shape: Tuple[int, ...]
+    init: str = "normal"  # normal | ones | zeros | small
+    std: float = 0.02
+
+    @property
+    def numel(self) -> int:
+        n = 1
+        for s in self.shape:
+            n *= s
+        return n
+
+
+@dataclass
+class ParamGroup:
+    pid: str
+    tensors: List[TensorSpec] = field(default_factory=list)
+
+    def nbytes(self, dtype_bytes: int = 2) -> int:
+        return sum(t.numel for t in self.tensors) * dtype_bytes
+
+
+def _seed(name: str, base: int) -> int:
+    return (int(hashlib.sha1(name.encode()).hexdigest()[:12], 16) + base) % (2 ** 62)
+
+
+def materialize(spec: TensorSpec, dtype=torch.bfloat16, device="cpu", seed: int = 0) -> torch.Tensor:
+    """Deterministic random-init tensor for ``spec`` (fp32 generation, cast once)."""
+    if spec.init == "ones":
+        return torch.ones(spec.shape, dtype=dtype, device=device)
+    if spec.init == "zeros":
+        return torch.zeros(spec.shape, dtype=dtype, device=device)
+    g = torch.Generator().manual_seed(_seed(spec.name, seed))
+    if spec.init == "ln":  # non-trivial LayerNorm/RMSNorm gains so tests exercise them
+        t = 1.0 + 0.1 * torch.randn(spec.shape, generator=g)
+    elif spec.init == "bias":
+        t = 0.02 * torch.randn(spec.shape, generator=g)
+    else:
+        t = spec.std * torch.randn(spec.shape, generator=g)
+    return t.to(dtype=dtype, device=device)
+
+
+class ParamStore:
+    """Host-side master copy of every parameter group (pinned when a GPU is present),
+    materialised lazily; the executor copies groups into its HBM arena on demand."""
+
+    def __init__(self, groups: Dict[str, ParamGroup], dtype=torch.bfloat16, seed: int = 0, pin: bool = None):
+        self.groups = groups
+        self.dtype = dtype
+        self.seed = seed
+        self.pin = torch.cuda.is_available() if pin is None else pin
+        self._host: Dict[str, torch.Tensor] = {}
+        self._specs: Dict[str, TensorSpec] = {s.name: s for g in groups.values() for s in g.tensors}
+
+    def tensor(self, name: str) -> torch.Tensor:
+        t = self._host.get(name)
+        if t is None:
+            spec = self._spec(name)
+            t = materialize(spec, self.dtype, "cpu", self.seed)
+            if self.pin:
+                t = t.pin_memory()
+            self._host[name] = t
+        return t
+
+    def _spec(self, name: str) -> TensorSpec:
+        return self._specs[name]
+
+    def group_tensors(self, pid: str) -> List[Tuple[TensorSpec, torch.Tensor]]:
+        return [(s, self.tensor(s.name)) for s in self.groups[pid].tensors]
+
+    def nbytes(self, pid: str) -> int:
+        """Bytes the group occupies in the HBM parameter arena (256-B aligned tensors)."""
+        return group_layout(self.groups[pid], torch.tensor([], dtype=self.dtype).element_size())[0]
+
+    def set_tensor(self, name: str, value: torch.Tensor) -> None:
+        """Install real weights (e.g. converted from a checkpoint) for ``name``."""
+        spec = self._spec(name)
+        if tuple(value.shape) != tuple(spec.shape):
+            raise ValueError(f"{name}: expected shape {spec.shape}, got {tuple(value.shape)}")
+        t = value.detach().to("cpu", self.dtype).contiguous()
+        self._host[name] = t.pin_memory() if self.pin else t
+
+
+GROUP_ALIGN = 256
+
+
+def group_layout(group: ParamGroup, dtype_bytes: int = 2):
+    """Byte layout of a parameter group inside the HBM parameter arena: every tensor
+    starts 256-B aligned (16-B vector loads, cache-line aligned rows).
+    Returns ``(total_bytes, [(spec, byte_offset), ...])``."""
+    off, out = 0, []
+    for spec in group.tensors:
+        out.append((spec, off))
+        off += (spec.numel * dtype_bytes + GROUP_ALIGN - 1) // GROUP_ALIGN * GROUP_ALIGN
+    return off, out

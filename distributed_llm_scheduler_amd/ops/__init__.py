@@ -1,0 +1,288 @@
+"""Operator layer: hand-written HIP/CDNA4 kernels with fp32 PyTorch references.
+
+``ops.linear(x, w, ...)`` etc. dispatch on the tensor's device:
+
+* GPU tensors run the HIP kernels in ``_dlsched_ops`` (csrc/kernels/*.hip, built for
+  gfx950). If the extension cannot be loaded on a GPU box this raises — there is no
+  silent eager fallback for GPU tensors.
+* CPU tensors run the ``ref_*`` implementations (fp32 math, result cast back to the
+  input dtype). They define the numerics the kernels are tested against and power the
+  CPU "fake device" executor used by the multi-process tests.
+
+Weight layout everywhere: GEMM weights are ``[N][K]`` (K contiguous); ``y = x @ W^T``.
+"""
+from __future__ import annotations
+
+import math
+import os
+import threading
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+ACT = {None: 0, "none": 0, "gelu": 1, "gelu_tanh": 1, "silu": 2, "relu": 3}
+
+_lock = threading.Lock()
+_ext = None
+_ext_err: Optional[BaseException] = None
+
+
+def _load_ext():
+    global _ext, _ext_err
+    if _ext is not None:
+        return _ext
+    with _lock:
+        if _ext is None:
+            try:
+                from .. import _build
+                if os.environ.get("DLS_SKIP_BUILD") != "1":
+                    _build.build_ops()
+                import importlib
+                _ext = importlib.import_module("distributed_llm_scheduler_amd._dlsched_ops")
+            except BaseException as e:  # noqa: BLE001 - re-raised with context in ext()
+                _ext_err = e
+    return _ext
+
+
+def ext():
+    """The compiled HIP op library; raises if it is unavailable (never falls back)."""
+    m = _load_ext()
+    if m is None:
+        raise RuntimeError(f"HIP kernel library _dlsched_ops is not available: {_ext_err!r}")
+    return m
+
+
+def native_available() -> bool:
+    return _load_ext() is not None
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------- references (fp32)
+
+def _act_ref(y: torch.Tensor, act) -> torch.Tensor:
+    a = ACT[act] if not isinstance(act, int) else act
+    if a == 1:
+        return F.gelu(y, approximate="tanh")
+    if a == 2:
+        return F.silu(y)
+    if a == 3:
+        return F.relu(y)
+    return y
+
+
+def ref_linear(x, w, bias=None, act=None, residual=None, alpha=1.0):
+    y = alpha * (x.float() @ w.float().t())
+    if bias is not None:
+        y = y + bias.float()
+    y = _act_ref(y, act)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+def ref_layernorm(x, w, b, eps=1e-5):
+    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), None if b is None else b.float(), eps).to(x.dtype)
+
+
+def ref_rmsnorm(x, w, eps=1e-5):
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(x.dtype)
+
+
+def ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=None):
+    """q [B*S][>=nh*D], k/v [B*S][>=nkv*D] (row views into a packed qkv buffer allowed)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    qh = q[:, :n_head * head_dim].float().reshape(B, S, n_head, head_dim).transpose(1, 2)
+    kh = k[:, :n_kv_head * head_dim].float().reshape(B, S, n_kv_head, head_dim).transpose(1, 2)
+    vh = v[:, :n_kv_head * head_dim].float().reshape(B, S, n_kv_head, head_dim).transpose(1, 2)
+    rep = n_head // n_kv_head
+    if rep > 1:
+        kh = kh.repeat_interleave(rep, dim=1)
+        vh = vh.repeat_interleave(rep, dim=1)
+    s = (qh @ kh.transpose(-1, -2)) * scale
+    if causal:
+        mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    o = torch.softmax(s, dim=-1) @ vh
+    return o.transpose(1, 2).reshape(B * S, n_head * head_dim).to(q.dtype)
+
+
+def rope_tables(S: int, head_dim: int, theta: float, device="cpu") -> Tuple[torch.Tensor, torch.Tensor]:
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    ang = torch.arange(S, dtype=torch.float64)[:, None] * inv[None, :]
+    return ang.cos().float().contiguous().to(device), ang.sin().float().contiguous().to(device)
+
+
+def ref_rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t):
+    M = qkv.shape[0]
+    pos = torch.arange(M, device=qkv.device) % S
+    c, s = cos_t[pos].to(qkv.device), sin_t[pos].to(qkv.device)
+    half = head_dim // 2
+
+    def rot(view, heads):
+        x = view.float().reshape(M, heads, head_dim)
+        x1, x2 = x[..., :half], x[..., half:]
+        cc, ss = c[:, None, :], s[:, None, :]
+        out = torch.cat([x1 * cc - x2 * ss, x2 * cc + x1 * ss], dim=-1)
+        view.copy_(out.reshape(M, heads * head_dim).to(view.dtype))
+
+    rot(qkv[:, :n_head * head_dim], n_head)
+    rot(qkv[:, k_col:k_col + n_kv_head * head_dim], n_kv_head)
+    return qkv
+
+
+# --------------------------------------------------------------------- dispatchers
+
+def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None):
+    """``act(alpha * x @ w^T + bias) + residual`` — one MFMA GEMM kernel with the whole
+    epilogue fused on GPU."""
+    if _gpu(x):
+        a = ACT[act] if not isinstance(act, int) else act
+        shp = x.shape[:-1] + (w.shape[0],)
+        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, -1)
+        return y.view(shp) if out is None else out
+    y = ref_linear(x, w, bias, act, residual, alpha)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def layernorm(x, w, b, eps=1e-5, residual=None, out=None, sum_out=None):
+    """LayerNorm; with ``residual`` returns ``(LN(x + residual), x + residual)``."""
+    if _gpu(x):
+        y, s = ext().norm(x, w, b, float(eps), residual, False, out, sum_out)
+        y = y.view(x.shape)
+        return (y, s.view(x.shape)) if residual is not None else y
+    if residual is not None:
+        s = (x.float() + residual.float()).to(x.dtype)
+        y = ref_layernorm(s, w, b, eps)
+        if sum_out is not None:
+            sum_out.copy_(s)
+        if out is not None:
+            out.copy_(y)
+        return y, s
+    y = ref_layernorm(x, w, b, eps)
+    if out is not None:
+        out.copy_(y)
+    return y
+
+
+def rmsnorm(x, w, eps=1e-5, residual=None, out=None, sum_out=None):
+    if _gpu(x):
+        y, s = ext().norm(x, w, None, float(eps), residual, True, out, sum_out)
+        y = y.view(x.shape)
+        return (y, s.view(x.shape)) if residual is not None else y
+    if residual is not None:
+        s = (x.float() + residual.float()).to(x.dtype)
+        return ref_rmsnorm(s, w, eps), s
+    return ref_rmsnorm(x, w, eps)
+
+
+def attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=None, out=None):
+    scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
+    if _gpu(q):
+        return ext().attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, float(scale), out)
+    y = ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, scale)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def gelu(x, out=None):
+    if _gpu(x):
+        return ext().gelu(x.contiguous(), out)
+    y = F.gelu(x.float(), approximate="tanh").to(x.dtype)
+    return out.copy_(y) if out is not None else y
+
+
+def add(a, b, out=None):
+    if _gpu(a):
+        return ext().add(a.contiguous(), b.contiguous(), out)
+    y = (a.float() + b.float()).to(a.dtype)
+    return out.copy_(y) if out is not None else y
+
+
+def swiglu(gate_up, out=None):
+    if _gpu(gate_up):
+        y = ext().swiglu(gate_up, out)
+        return y.view(gate_up.shape[:-1] + (gate_up.shape[-1] // 2,))
+    f = gate_up.shape[-1] // 2
+    y = (F.silu(gate_up[..., :f].float()) * gate_up[..., f:].float()).to(gate_up.dtype)
+    return out.copy_(y) if out is not None else y
+
+
+def embedding(tokens, wte, wpe=None, S=1, out=None):
+    if _gpu(wte):
+        return ext().embedding(tokens.to(torch.int32).contiguous(), wte, wpe, int(S), out)
+    t = tokens.reshape(-1).long()
+    y = wte.float()[t]
+    if wpe is not None:
+        y = y + wpe.float()[torch.arange(t.numel()) % S]
+    y = y.to(wte.dtype)
+    return out.copy_(y) if out is not None else y
+
+
+def rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t):
+    if _gpu(qkv):
+        ext().rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t)
+        return qkv
+    return ref_rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t)
+
+
+# ------------------------------------------------------------------------- MoE
+
+def moe_router(logits, topk):
+    if _gpu(logits):
+        return tuple(ext().moe_router(logits.contiguous(), int(topk)))
+    lf = logits.float()
+    val, idx = torch.topk(lf, topk, dim=-1)
+    w = torch.softmax(val, dim=-1)
+    return idx.to(torch.int32), w
+
+
+def moe_align(topk_idx, n_experts):
+    """Counting sort of (token, k) assignments by expert -> (src_rows, slot_of, offsets)."""
+    if _gpu(topk_idx):
+        return tuple(ext().moe_align(topk_idx.contiguous(), int(n_experts)))
+    flat = topk_idx.reshape(-1).long()
+    k = topk_idx.shape[1]
+    order = torch.sort(flat, stable=True).indices
+    slot_of = torch.empty_like(order)
+    slot_of[order] = torch.arange(order.numel())
+    counts = torch.bincount(flat, minlength=n_experts)
+    offsets = torch.zeros(n_experts + 1, dtype=torch.int64)
+    offsets[1:] = torch.cumsum(counts, 0)
+    return (order // k).to(torch.int32), slot_of.to(torch.int32), offsets.to(torch.int32)
+
+
+def moe_permute(x, src_rows):
+    if _gpu(x):
+        return ext().moe_permute(x.contiguous(), src_rows)
+    return x[src_rows.long()]
+
+
+def moe_combine(expert_out, slot_of, weights):
+    if _gpu(expert_out):
+        return ext().moe_combine(expert_out.contiguous(), slot_of, weights.contiguous())
+    M, k = weights.shape
+    g = expert_out.float()[slot_of.long()].reshape(M, k, -1)
+    return (g * weights.float()[..., None]).sum(1).to(expert_out.dtype)
+
+
+def grouped_gemm(X, offsets, W, act=None):
+    """Per-expert ``act(X_e @ W_e^T)`` over expert-sorted rows; W is [E][N][K]."""
+    a = ACT[act] if not isinstance(act, int) else act
+    if _gpu(X):
+        return ext().grouped_gemm(X.contiguous(), offsets, W.contiguous(), a)
+    out = torch.empty(X.shape[0], W.shape[1], dtype=X.dtype)
+    off = offsets.tolist()
+    for e in range(W.shape[0]):
+        if off[e + 1] > off[e]:
+            out[off[e]:off[e + 1]] = ref_linear(X[off[e]:off[e + 1]], W[e], act=a)
+    return out

@@ -1,0 +1,349 @@
+"""Per-rank DAG executor.
+
+One process per GPU (``torch.distributed`` world, backend ``nccl`` = RCCL on ROCm, or
+``gloo`` for the CPU fake-device backend). Each rank executes its :class:`Program`:
+
+* activations live in ONE preallocated slab per rank at statically planned offsets
+  (program.py); parameters in a second slab whose size is the per-GPU memory cap;
+* ``load`` copies a parameter group host(pinned)->HBM on the compute stream unless the
+  arena region still holds it from the previous step (steady-state residency);
+* ``recv``/``send`` are RCCL point-to-point ops (``dist.irecv``/``dist.isend``): RCCL runs
+  them on its own stream ordered after the producing kernels, and the consumer waits
+  stream-side (``work.wait()``), so transfers overlap the next independent kernels; a
+  sent buffer is only overwritten after its send completes;
+* ``run`` launches the (fused) kernel group through :mod:`ops` — HIP kernels on GPU;
+* programs without p2p ops are captured once into a hipGraph (``torch.cuda.CUDAGraph``)
+  and replayed, removing per-kernel host launch cost from the step.
+
+``profile=True`` records a start/stop hipEvent pair per kernel group, giving a measured
+per-GPU Gantt (same layout as the reference's simulated one, visu.py:206-248).
+"""
+from __future__ import annotations
+
+import math
+import zlib
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..core.task import Task
+from ..models.params import ParamStore, group_layout
+from .program import Program
+
+
+@dataclass
+class StepStats:
+    wall_ms: float = 0.0
+    kernels: int = 0
+    sends: int = 0
+    recvs: int = 0
+    bytes_sent: int = 0
+    param_fills: int = 0
+    bytes_filled: int = 0
+    timeline: List[Tuple[str, float, float]] = field(default_factory=list)  # (group, start_ms, end_ms)
+
+
+def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.Tensor:
+    """Deterministic synthetic token ids for external input ``name`` — identical on every
+    rank and in tests, whichever rank happens to own the consuming task."""
+    g = torch.Generator().manual_seed((zlib.crc32(name.encode()) ^ seed) & 0x7FFFFFFF)
+    return torch.randint(0, vocab, (n,), generator=g, dtype=torch.int32)
+
+
+class DAGExecutor:
+    def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
+                 model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234):
+        self.tasks = {t.id: t for t in tasks}
+        self.prog = program
+        self.store = store
+        self.device = torch.device(device)
+        self.gpu = self.device.type == "cuda"
+        self.cfg = model_cfg
+        self.pg = pg
+        self.use_graph = use_graph and self.gpu and not program.has_comm
+        self.seed = seed
+        self.dtype = torch.bfloat16
+        self._graph = None
+        self._views: Dict[str, torch.Tensor] = {}     # activation views (output task -> tensor)
+        self._params: Dict[str, Dict[str, torch.Tensor]] = {}  # pid -> {tensor name -> view}
+        self._wflat: Dict[str, torch.Tensor] = {}               # tensor name -> resident view
+        self._valid: List[Tuple[int, int, str]] = []  # param arena regions holding data
+        self._inputs: Dict[str, torch.Tensor] = {}
+        self._pending_sends: List[Tuple[int, int, object]] = []
+        self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
+        self.last = StepStats()
+        self._setup()
+
+    # ------------------------------------------------------------------ setup
+    def _setup(self) -> None:
+        p = self.prog
+        dev = self.device
+        self.act_slab = torch.empty(max(p.act_arena_bytes, 256), dtype=torch.uint8, device=dev)
+        self.param_slab = torch.empty(max(p.param_arena_bytes, 256), dtype=torch.uint8, device=dev)
+        for tid, off in p.act_offset.items():
+            t = self.tasks[tid]
+            shape = tuple(t.op.out_shape) if t.op is not None and t.op.out_shape else (p.act_bytes[tid] // 2,)
+            n = math.prod(shape)
+            self._views[tid] = self.act_slab[off:off + 2 * n].view(self.dtype).view(shape)
+        # workspace for intra-group temporaries (attention qkv / o, mlp gate_up ...)
+        ws = 0
+        for ins in p.instrs:
+            if ins.op == "run":
+                ws = max(ws, self._workspace_bytes(ins))
+        self.ws_slab = torch.empty(max(ws, 256), dtype=torch.uint8, device=dev)
+        # external inputs (token ids per request replica)
+        for ins in p.instrs:
+            if ins.op != "run":
+                continue
+            for tid in ins.group:
+                op = self.tasks[tid].op
+                for name in op.inputs:
+                    if name not in self.tasks and name not in self._inputs:
+                        M = math.prod(op.out_shape[:-1])
+                        vocab = self.cfg.vocab_size if self.cfg is not None else 50257
+                        self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
+
+    def _workspace_bytes(self, ins) -> int:
+        t = self.tasks[ins.group[0]]
+        if t.op is None:
+            return 0
+        k = t.op.kind
+        M = math.prod(t.op.out_shape[:-1]) if t.op.out_shape else 0
+        a = t.op.attrs
+        if k == "attention":
+            D = a["head_dim"]
+            qkv = M * (a["n_head"] + 2 * a["n_kv_head"]) * D
+            return 2 * (qkv + M * a["n_head"] * D) + 512
+        if k == "swiglu_mlp":
+            F = a["ffn"]
+            return 2 * (M * 2 * F + M * F) + 512
+        if k == "moe":
+            return 0
+        return 0
+
+    def _ws(self, offset_elems: int, shape) -> torch.Tensor:
+        n = math.prod(shape)
+        base = (offset_elems * 2 + 255) // 256 * 256
+        return self.ws_slab[base:base + 2 * n].view(self.dtype).view(shape)
+
+    # ------------------------------------------------------------- parameters
+    def _load(self, instr_index: int, pid: str, stats: StepStats) -> None:
+        off = self.prog.param_offset.get((instr_index, pid))
+        if off is None:
+            raise RuntimeError(f"parameter group {pid} did not fit the per-GPU parameter budget")
+        group = self.store.groups[pid]
+        total, layout = group_layout(group)
+        views = {}
+        for spec, sub in layout:
+            n = spec.numel
+            views[spec.name] = self.param_slab[off + sub:off + sub + 2 * n].view(self.dtype).view(spec.shape)
+        self._params[pid] = views
+        self._wflat.update(views)
+        if (off, total, pid) in self._valid:
+            return  # region still holds this group (steady-state residency)
+        self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
+        for spec, _ in layout:
+            views[spec.name].copy_(self.store.tensor(spec.name), non_blocking=True)
+        self._valid.append((off, total, pid))
+        stats.param_fills += 1
+        stats.bytes_filled += total
+
+    def _evict(self, pid: str) -> None:
+        for name in self._params.pop(pid, {}):
+            self._wflat.pop(name, None)
+
+    def _w(self, name: str) -> torch.Tensor:
+        t = self._wflat.get(name)
+        if t is None:
+            raise KeyError(f"parameter tensor {name} is not resident on rank {self.prog.rank}")
+        return t
+
+    # ---------------------------------------------------------------- kernels
+    def _x(self, name: str) -> torch.Tensor:
+        v = self._views.get(name)
+        if v is not None:
+            return v
+        return self._inputs[name]
+
+    def _flat(self, t: torch.Tensor) -> torch.Tensor:
+        return t.reshape(-1, t.shape[-1])
+
+    def _rope_tables(self, S: int, D: int, theta: float):
+        key = (S, D, theta)
+        if key not in self._rope:
+            self._rope[key] = ops.rope_tables(S, D, theta, self.device)
+        return self._rope[key]
+
+    def _run_group(self, ins) -> None:
+        grp = [self.tasks[t] for t in ins.group]
+        head, tail = grp[0], grp[-1]
+        out = self._views[tail.id]
+        k = head.op.kind
+        residual = None
+        if tail.op.kind == "residual" and len(grp) > 1:
+            prod = grp[-2].id
+            other = [d for d in tail.op.inputs if d != prod][0]
+            residual = self._flat(self._x(other))
+        act = "gelu" if any(t.op.kind == "gelu" for t in grp[1:]) else head.op.attrs.get("act")
+        a = head.op.attrs
+        W = head.op.weights
+        if k == "embedding":
+            tok = self._x(head.op.inputs[0])
+            S = head.op.out_shape[1]
+            ops.embedding(tok, self._w(W["wte"]), self._w(W["wpe"]) if "wpe" in W else None, S,
+                          out=self._flat(out))
+        elif k == "layernorm":
+            ops.layernorm(self._flat(self._x(head.op.inputs[0])), self._w(W["w"]), self._w(W["b"]),
+                          a.get("eps", 1e-5), out=self._flat(out))
+        elif k == "rmsnorm":
+            ops.rmsnorm(self._flat(self._x(head.op.inputs[0])), self._w(W["w"]), a.get("eps", 1e-5),
+                        out=self._flat(out))
+        elif k == "residual":
+            ops.add(self._x(head.op.inputs[0]), self._x(head.op.inputs[1]), out=out)
+        elif k == "gelu":
+            ops.gelu(self._x(head.op.inputs[0]), out=out)
+        elif k in ("linear", "lm_head"):
+            ops.linear(self._flat(self._x(head.op.inputs[0])), self._w(W["w"]),
+                       self._w(W["b"]) if "b" in W else None, act=act, residual=residual, out=self._flat(out))
+        elif k == "attention":
+            x = self._flat(self._x(head.op.inputs[0]))
+            M = x.shape[0]
+            B, S = head.op.out_shape[0], head.op.out_shape[1]
+            nh, nkv, D = a["n_head"], a["n_kv_head"], a["head_dim"]
+            width = (nh + 2 * nkv) * D
+            qkv = self._ws(0, (M, width))
+            o = self._ws(M * width, (M, nh * D))
+            ops.linear(x, self._w(W["w_qkv"]), self._w(W["b_qkv"]) if "b_qkv" in W else None, out=qkv)
+            if a.get("rope"):
+                cos, sin = self._rope_tables(S, D, a.get("rope_theta", 10000.0))
+                ops.rope_(qkv, S, nh, nkv, D, nh * D, cos, sin)
+            ops.attention(qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:], B, S, nh, nkv,
+                          D, causal=a.get("causal", True), out=o)
+            ops.linear(o, self._w(W["w_o"]), self._w(W["b_o"]) if "b_o" in W else None, residual=residual,
+                       out=self._flat(out))
+        elif k == "swiglu_mlp":
+            x = self._flat(self._x(head.op.inputs[0]))
+            M, F = x.shape[0], a["ffn"]
+            gu = self._ws(0, (M, 2 * F))
+            h = self._ws(M * 2 * F, (M, F))
+            ops.linear(x, self._w(W["w_gate_up"]), out=gu)
+            ops.swiglu(gu, out=h)
+            ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out))
+        elif k == "moe":
+            self._run_moe(head, residual, out)
+        else:
+            raise NotImplementedError(f"op kind {k!r}")
+
+    def _run_moe(self, t: Task, residual, out) -> None:
+        a, W = t.op.attrs, t.op.weights
+        x = self._flat(self._x(t.op.inputs[0]))
+        E, k = a["n_experts"], a["top_k"]
+        logits = ops.linear(x, self._w(W["w_router"]))
+        idx, gate = ops.moe_router(logits, k)
+        src, slot, off = ops.moe_align(idx, E)
+        xp = ops.moe_permute(x, src)
+        Wgu = torch.stack([self._w(n) for n in W["experts_gate_up"]]) if isinstance(W["experts_gate_up"], list) \
+            else self._w(W["experts_gate_up"])
+        Wd = torch.stack([self._w(n) for n in W["experts_down"]]) if isinstance(W["experts_down"], list) \
+            else self._w(W["experts_down"])
+        gu = ops.grouped_gemm(xp, off, Wgu)
+        h = ops.swiglu(gu)
+        eo = ops.grouped_gemm(h, off, Wd)
+        y = ops.moe_combine(eo, slot, gate)
+        if residual is not None:
+            y = ops.add(y, residual)
+        self._flat(out).copy_(y)
+
+    # ------------------------------------------------------------------- step
+    def _step_body(self, stats: StepStats, timeline: Optional[list] = None) -> None:
+        pg = self.pg
+        self._pending_sends = []
+        recv_work: Dict[str, object] = {}
+        for i, ins in enumerate(self.prog.instrs):
+            if ins.op == "load":
+                self._load(i, ins.param, stats)
+            elif ins.op == "evict":
+                self._evict(ins.param)
+            elif ins.op == "recv":
+                recv_work[ins.task] = dist.irecv(self._views[ins.task], src=ins.peer, group=pg)
+                stats.recvs += 1
+            elif ins.op == "send":
+                buf = self._views[ins.task]
+                w = dist.isend(buf, dst=ins.peer, group=pg)
+                off = self.prog.act_offset[ins.task]
+                self._pending_sends.append((off, self.prog.act_bytes[ins.task], w))
+                stats.sends += 1
+                stats.bytes_sent += buf.numel() * buf.element_size()
+            elif ins.op == "run":
+                for tid in ins.group:
+                    for d in self.tasks[tid].dependencies:
+                        w = recv_work.pop(d, None)
+                        if w is not None:
+                            w.wait()
+                off, nb = self.prog.act_offset[ins.task], self.prog.act_bytes[ins.task]
+                if self._pending_sends:
+                    keep = []
+                    for so, sb, w in self._pending_sends:
+                        if so < off + nb and off < so + sb:
+                            w.wait()  # buffer about to be overwritten: its send must be done
+                        else:
+                            keep.append((so, sb, w))
+                    self._pending_sends = keep
+                if timeline is not None:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    self._run_group(ins)
+                    e1.record()
+                    timeline.append((ins.task, e0, e1))
+                else:
+                    self._run_group(ins)
+                stats.kernels += 1
+        for w in recv_work.values():
+            w.wait()
+        for _, _, w in self._pending_sends:
+            w.wait()
+        self._pending_sends = []
+
+    def step(self, profile: bool = False) -> StepStats:
+        """Execute the rank's program once (asynchronously on the GPU)."""
+        stats = StepStats()
+        if self._graph is not None and not profile:
+            self._graph.replay()
+            stats.kernels = self.prog.n_kernels
+        else:
+            tl = [] if (profile and self.gpu) else None
+            self._step_body(stats, tl)
+            if tl is not None:
+                torch.cuda.synchronize(self.device)
+                t0 = tl[0][1] if tl else None
+                stats.timeline = [(tid, t0.elapsed_time(a), t0.elapsed_time(b)) for tid, a, b in tl]
+        self.last = stats
+        return stats
+
+    def capture(self) -> bool:
+        """Capture the steady-state step into a hipGraph (comm-free programs only)."""
+        if not self.use_graph:
+            return False
+        torch.cuda.synchronize(self.device)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._step_body(StepStats())  # warm the residency state on the capture stream
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_body(StepStats())
+        torch.cuda.synchronize(self.device)
+        self._graph = g
+        return True
+
+    def output(self, tid: str) -> torch.Tensor:
+        return self._views[tid]
+
+    def memory_bytes(self) -> Dict[str, int]:
+        return {"activations": self.act_slab.numel(), "params": self.param_slab.numel(),
+                "workspace": self.ws_slab.numel()}

@@ -1,0 +1,255 @@
+"""Lower a placed DAG into per-GPU programs.
+
+Input: the task list, a placement (task -> rank) and a global order (the order in which
+the scheduler committed tasks — topological by construction). Output: one
+:class:`Program` per rank, built identically on every rank, containing
+
+* ``load(p)`` / ``evict(p)`` — parameter-cache traffic replayed from the scheduler's
+  action trace (``scheduler.events``) or, without a trace, load-on-first-use,
+* ``recv(t, src)`` / ``send(t, dst)`` — one point-to-point transfer per (cross-GPU edge
+  producer, consumer rank) pair, emitted at the PRODUCER's global position on both
+  ends, so every pair of ranks posts its send/recv sequence in the same order (no
+  deadlock, no tag matching; RCCL p2p over one xGMI link),
+* ``run(group)`` — one kernel group. Co-located producer->consumer pairs whose
+  intermediate has no other consumer are fused into one group, e.g.
+  ``linear+gelu`` (GEMM epilogue), ``linear+residual`` and ``attention+residual``
+  (output-projection epilogue) — the fused intermediates never exist in HBM.
+
+Memory is planned statically: every activation gets an offset in the rank's activation
+arena (native best-fit arena, lifetimes from the program), every parameter group an
+offset in its parameter arena (capacity = the per-GPU memory cap). Nothing is allocated
+at run time, so a rank's whole program is hipGraph-capturable.
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from ..core import native as _native
+from ..core.task import Task
+
+ALIGN = 256
+
+
+@dataclass
+class Instr:
+    op: str  # load | evict | recv | send | run
+    task: Optional[str] = None      # producing task (recv/send) or output task (run)
+    group: Tuple[str, ...] = ()     # run: fused task ids, execution order
+    kind: str = ""                  # run: fused kind (e.g. "linear+gelu")
+    peer: int = -1                  # recv: source rank, send: destination rank
+    param: Optional[str] = None     # load/evict
+
+
+@dataclass
+class Program:
+    rank: int
+    instrs: List[Instr] = field(default_factory=list)
+    act_offset: Dict[str, int] = field(default_factory=dict)   # output task -> byte offset
+    act_bytes: Dict[str, int] = field(default_factory=dict)
+    act_arena_bytes: int = 0
+    param_offset: Dict[Tuple[int, str], int] = field(default_factory=dict)  # (load index, pid) -> offset
+    param_arena_bytes: int = 0
+    param_peak_bytes: int = 0
+    failed_loads: List[str] = field(default_factory=list)
+    n_kernels: int = 0
+
+    @property
+    def has_comm(self) -> bool:
+        return any(i.op in ("send", "recv") for i in self.instrs)
+
+    def counts(self) -> Dict[str, int]:
+        c: Dict[str, int] = defaultdict(int)
+        for i in self.instrs:
+            c[i.op] += 1
+        return dict(c)
+
+
+def _fuse_kind(prev_kind: str, nxt: Task) -> Optional[str]:
+    """Kind of the group formed by appending ``nxt`` to a group of kind ``prev_kind``."""
+    if nxt.op is None:
+        return None
+    kb = nxt.op.kind
+    if prev_kind == "linear" and kb == "gelu":
+        return "linear+gelu"        # GELU in the GEMM epilogue
+    if prev_kind in ("linear", "linear+gelu", "attention", "swiglu_mlp", "moe") and kb == "residual":
+        return prev_kind + "+residual"  # residual add in the (output-projection) GEMM epilogue
+    return None
+
+
+def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
+                   param_bytes: Dict[str, int], param_cap_bytes: Optional[Dict[int, int]] = None,
+                   events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
+                   fuse: bool = True) -> List[Program]:
+    """Build every rank's program. ``placement`` maps task id -> rank; tasks absent from it
+    (failed or orphaned by the scheduler) are skipped together with their dependents."""
+    core = _native.load()
+    if core is None:
+        raise RuntimeError("native core (_dlsched_core) is required for memory planning")
+    tmap = {t.id: t for t in tasks}
+    pos = {tid: i for i, tid in enumerate(order)}
+    order = [t for t in order if t in placement]
+    consumers: Dict[str, List[str]] = defaultdict(list)
+    for tid in order:
+        for d in tmap[tid].dependencies:
+            if d in placement:
+                consumers[d].append(tid)
+
+    # --- fusion: chains on one rank, consumer is the producer's only consumer, every
+    # other input of the consumer is produced before the producer runs
+    fused_into: Dict[str, str] = {}   # producer -> consumer that absorbs it
+    group_of: Dict[str, List[str]] = {}
+    if fuse:
+        for tid in order:
+            if tid in fused_into:
+                continue
+            chain = [tid]
+            kind = tmap[tid].op.kind if tmap[tid].op else ""
+            while True:
+                cons = consumers.get(chain[-1], [])
+                if len(cons) != 1 or placement[cons[0]] != placement[chain[-1]]:
+                    break
+                nxt = cons[0]
+                fk = _fuse_kind(kind, tmap[nxt])
+                if fk is None:
+                    break
+                # every other input of nxt must exist before the group starts
+                others = [d for d in tmap[nxt].dependencies if d != chain[-1]]
+                if any(o not in placement or pos.get(o, 1 << 60) > pos[chain[0]] for o in others):
+                    break
+                chain.append(nxt)
+                kind = fk
+            if len(chain) > 1:
+                for a in chain[:-1]:
+                    fused_into[a] = chain[-1]
+                group_of[chain[-1]] = chain
+                group_of[chain[0]] = chain
+
+    # --- parameter plan per node from the scheduler trace (load-on-first-use otherwise)
+    load_before: Dict[str, List[Tuple[str, str]]] = defaultdict(list)  # task -> [(op, pid)] on its rank
+    if events is not None:
+        pending: Dict[int, List[Tuple[str, str]]] = defaultdict(list)
+        for _, act, node, item in events:
+            if act in ("LOAD", "EVICT"):
+                r = node_rank[node] if node_rank else int(node)
+                pending[r].append((act.lower(), item))
+            elif act == "RUN" and item in placement:
+                r = placement[item]
+                load_before[item].extend(pending.pop(r, []))
+
+    programs: List[Program] = []
+    caps = param_cap_bytes or {}
+    for rank in range(world):
+        prog = Program(rank)
+        ins = prog.instrs
+        par = core.Arena(caps.get(rank, 1 << 50), ALIGN)
+        where: Dict[str, int] = {}       # resident pid -> arena offset
+        last_use: Dict[str, int] = {}    # pid -> instruction index of last use (LRU)
+        extent = 0
+
+        def evict(pid):
+            ins.append(Instr("evict", param=pid))
+            par.release(where.pop(pid))
+
+        def load(pid, needed):
+            nonlocal extent
+            nbytes = int(param_bytes.get(pid, 0)) or 1
+            off = par.alloc(nbytes)
+            while off < 0:
+                # fragmentation (the scheduler accounts bytes, not contiguity): evict the
+                # least recently used resident group this task does not need, retry
+                victims = sorted((q for q in where if q not in needed), key=lambda q: last_use.get(q, -1))
+                if not victims:
+                    prog.failed_loads.append(pid)
+                    return
+                evict(victims[0])
+                off = par.alloc(nbytes)
+            where[pid] = off
+            ins.append(Instr("load", param=pid))
+            prog.param_offset[(len(ins) - 1, pid)] = off
+            extent = max(extent, off + nbytes)
+
+        received = set()
+        emitted_group = set()
+        for tid in order:
+            r = placement[tid]
+            t = tmap[tid]
+            if r == rank:
+                needed = set(t.params_needed)
+                if events is not None:  # replay the policy's cache decisions
+                    for op, pid in load_before.get(tid, []):
+                        if op == "evict" and pid in where and pid not in needed:
+                            evict(pid)
+                        elif op == "load" and pid not in where:
+                            load(pid, needed)
+                for pid in sorted(needed):
+                    if pid not in where:
+                        load(pid, needed)
+                    last_use[pid] = len(ins)
+                if tid in fused_into:
+                    continue  # executed as part of its consumer's group
+                grp = tuple(group_of.get(tid, [tid]))
+                if grp in emitted_group:
+                    continue
+                emitted_group.add(grp)
+                kind = _group_kind(tmap, grp)
+                ins.append(Instr("run", task=grp[-1], group=grp, kind=kind))
+                prog.n_kernels += 1
+                dsts = sorted({placement[c] for c in consumers.get(grp[-1], []) if placement[c] != rank})
+                for dst in dsts:
+                    ins.append(Instr("send", task=grp[-1], peer=dst))
+            else:
+                if tid in fused_into:
+                    continue
+                if any(placement[c] == rank for c in consumers.get(tid, [])) and tid not in received:
+                    ins.append(Instr("recv", task=tid, peer=r))
+                    received.add(tid)
+        prog.param_peak_bytes = par.peak
+        prog.param_arena_bytes = extent
+        sinks = {t for t in order if not consumers.get(t)}
+        _plan_activations(core, prog, tmap, sinks)
+        programs.append(prog)
+    return programs
+
+
+def _group_kind(tmap: Dict[str, Task], grp: Tuple[str, ...]) -> str:
+    kind = tmap[grp[0]].op.kind if tmap[grp[0]].op else "noop"
+    for nxt in grp[1:]:
+        kind = _fuse_kind(kind, tmap[nxt]) or kind
+    return kind
+
+
+def _plan_activations(core, prog: Program, tmap: Dict[str, Task], sinks=frozenset()) -> None:
+    """Static activation lifetimes -> offsets in the rank's activation slab. DAG outputs
+    (``sinks``: tasks nobody consumes, e.g. the logits of every request) stay live."""
+    # last use index of each activation on this rank
+    last_use: Dict[str, int] = {}
+    for i, ins in enumerate(prog.instrs):
+        if ins.op == "run":
+            for tid in ins.group:
+                for d in tmap[tid].dependencies:
+                    last_use[d] = i
+            last_use.setdefault(ins.task, i)
+        elif ins.op in ("send", "recv"):
+            last_use[ins.task] = max(last_use.get(ins.task, i), i)
+    act = core.Arena(1 << 50, ALIGN)
+    frees: Dict[int, List[str]] = defaultdict(list)
+    for tid, i in last_use.items():
+        if tid not in sinks:
+            frees[i].append(tid)
+    live: Dict[str, int] = {}
+    extent = 0
+    for i, ins in enumerate(prog.instrs):
+        if ins.op in ("run", "recv"):
+            tid = ins.task
+            nbytes = max(int(tmap[tid].out_bytes), 1)
+            off = act.alloc(nbytes)
+            prog.act_offset[tid] = off
+            prog.act_bytes[tid] = nbytes
+            live[tid] = off
+            extent = max(extent, off + nbytes)
+        for tid in frees.get(i, []):
+            if tid in live:
+                act.release(live.pop(tid))
+    prog.act_arena_bytes = extent  # slab size = highest byte any activation reaches

@@ -1,0 +1,151 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Operands are random (never zero-filled or symmetric); GEMM checks include an
+asymmetric-B identity test that catches a transposed C write
+(cdna_hip_programming.md §3 "Always A=I-check with ASYMMETRIC B").
+"""
+import math
+
+import pytest
+import torch
+
+from distributed_llm_scheduler_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rand(*shape, scale=1.0, dtype=torch.bfloat16, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (scale * torch.randn(*shape, generator=g)).to(dtype).to(DEV)
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    ref = b.float().abs().max().item() + 1e-6
+    assert err <= tol * ref, f"max abs err {err:.4g} vs ref max {ref:.4g} (rel tol {tol})"
+
+
+def test_native_library_loaded():
+    m = ops.ext()
+    assert hasattr(m, "gemm") and hasattr(m, "attention")
+
+
+def test_gemm_identity_asymmetric():
+    n = 64
+    eye = torch.eye(n, dtype=torch.bfloat16, device=DEV)
+    b = (torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) % 97 - 48).to(torch.bfloat16)
+    # y = I @ W^T = W^T  (W stored [N][K])
+    y = ops.linear(eye, b)
+    assert torch.equal(y, b.t().contiguous())
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 2304, 768), (512, 768, 3072), (512, 3072, 768), (77, 130, 200),
+                                   (512, 50257, 768), (1, 64, 64), (1024, 1024, 1024)])
+@pytest.mark.parametrize("config", [-1, 0, 3])
+def test_gemm_shapes(M, N, K, config):
+    x = _rand(M, K, seed=1)
+    w = _rand(N, K, scale=0.05, seed=2)
+    ref = ops.ref_linear(x.cpu(), w.cpu()).float()
+    y = ops.ext().gemm(x, w, None, None, 0, 1.0, None, config)
+    torch.cuda.synchronize()
+    _close(y.cpu(), ref, 2e-2)
+
+
+@pytest.mark.parametrize("act", [None, "gelu", "silu"])
+def test_gemm_epilogue(act):
+    M, N, K = 256, 384, 512
+    x, w = _rand(M, K, seed=3), _rand(N, K, scale=0.05, seed=4)
+    bias, res = _rand(N, scale=0.5, seed=5), _rand(M, N, seed=6)
+    y = ops.linear(x, w, bias=bias, act=act, residual=res)
+    ref = ops.ref_linear(x.cpu(), w.cpu(), bias.cpu(), act, res.cpu())
+    _close(y.cpu(), ref, 2e-2)
+
+
+@pytest.mark.parametrize("B,S,nh,nkv,D,causal", [(1, 512, 12, 12, 64, True), (2, 200, 4, 4, 64, True),
+                                                  (1, 256, 8, 2, 128, True), (1, 130, 4, 4, 64, False),
+                                                  (1, 64, 32, 8, 128, True)])
+def test_attention(B, S, nh, nkv, D, causal):
+    qkv = _rand(B * S, (nh + 2 * nkv) * D, seed=7)
+    q, k, v = qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:]
+    o = ops.attention(q, k, v, B, S, nh, nkv, D, causal=causal)
+    ref = ops.ref_attention(q.cpu(), k.cpu(), v.cpu(), B, S, nh, nkv, D, causal=causal)
+    _close(o.cpu(), ref, 2e-2)
+
+
+def test_attention_spike_forces_rescale():
+    # a large score late in the sequence forces the online-softmax rescale branch
+    B, S, nh, D = 1, 256, 2, 64
+    qkv = _rand(B * S, 3 * nh * D, scale=0.5, seed=8)
+    qkv[:, nh * D:2 * nh * D][200] *= 40.0
+    q, k, v = qkv[:, :nh * D], qkv[:, nh * D:2 * nh * D], qkv[:, 2 * nh * D:]
+    o = ops.attention(q, k, v, B, S, nh, nh, D)
+    ref = ops.ref_attention(q.cpu(), k.cpu(), v.cpu(), B, S, nh, nh, D)
+    _close(o.cpu(), ref, 3e-2)
+
+
+@pytest.mark.parametrize("H", [768, 1024, 4096, 64])
+def test_layernorm_and_residual(H):
+    x, r = _rand(300, H, seed=9), _rand(300, H, seed=10)
+    w, b = (1 + 0.1 * _rand(H, seed=11).float()).to(torch.bfloat16), _rand(H, scale=0.1, seed=12)
+    y = ops.layernorm(x, w, b)
+    _close(y.cpu(), ops.ref_layernorm(x.cpu(), w.cpu(), b.cpu()), 2e-2)
+    y2, s = ops.layernorm(x, w, b, residual=r)
+    s_ref = (x.cpu().float() + r.cpu().float()).to(torch.bfloat16)
+    assert torch.equal(s.cpu(), s_ref)
+    _close(y2.cpu(), ops.ref_layernorm(s_ref, w.cpu(), b.cpu()), 2e-2)
+
+
+def test_rmsnorm():
+    x, w = _rand(100, 4096, seed=13), (1 + 0.1 * _rand(4096, seed=14).float()).to(torch.bfloat16)
+    _close(ops.rmsnorm(x, w).cpu(), ops.ref_rmsnorm(x.cpu(), w.cpu()), 2e-2)
+
+
+def test_elementwise():
+    x, y = _rand(1000, 64, seed=15), _rand(1000, 64, seed=16)
+    _close(ops.gelu(x).cpu(), torch.nn.functional.gelu(x.cpu().float(), approximate="tanh"), 1e-2)
+    _close(ops.add(x, y).cpu(), x.cpu().float() + y.cpu().float(), 1e-2)
+    gu = _rand(50, 2 * 96, seed=17)
+    ref = torch.nn.functional.silu(gu.cpu().float()[:, :96]) * gu.cpu().float()[:, 96:]
+    _close(ops.swiglu(gu).cpu(), ref, 1e-2)
+
+
+def test_embedding():
+    V, H, S = 1000, 256, 64
+    wte, wpe = _rand(V, H, seed=18), _rand(S, H, seed=19)
+    tok = torch.randint(0, V, (2 * S,), device=DEV, dtype=torch.int32)
+    y = ops.embedding(tok, wte, wpe, S)
+    ref = ops.embedding(tok.cpu(), wte.cpu(), wpe.cpu(), S)
+    _close(y.cpu(), ref, 1e-2)
+
+
+def test_rope():
+    S, nh, nkv, D = 64, 4, 2, 128
+    qkv = _rand(2 * S, (nh + 2 * nkv) * D, seed=20)
+    cos, sin = ops.rope_tables(S, D, 10000.0, DEV)
+    ref = ops.ref_rope_(qkv.cpu().clone(), S, nh, nkv, D, nh * D, cos.cpu(), sin.cpu())
+    ops.rope_(qkv, S, nh, nkv, D, nh * D, cos, sin)
+    _close(qkv.cpu(), ref, 1e-2)
+
+
+def test_moe_pipeline():
+    M, E, k, H, F = 300, 8, 2, 128, 96
+    # tie-free logits (bf16 random values collide; top-k order among ties is unspecified)
+    g = torch.Generator().manual_seed(21)
+    logits = torch.stack([torch.randperm(E, generator=g) for _ in range(M)]).float().mul(0.25)
+    logits = logits.to(torch.bfloat16).to(DEV)
+    idx, w = ops.moe_router(logits, k)
+    ridx, rw = ops.moe_router(logits.cpu(), k)
+    assert torch.equal(idx.cpu().sort(-1).values, ridx.sort(-1).values)
+    src, slot, off = ops.moe_align(idx, E)
+    rsrc, rslot, roff = ops.moe_align(idx.cpu(), E)
+    assert torch.equal(off.cpu(), roff) and torch.equal(src.cpu(), rsrc) and torch.equal(slot.cpu(), rslot)
+    x = _rand(M, H, seed=22)
+    xp = ops.moe_permute(x, src)
+    assert torch.equal(xp.cpu(), x.cpu()[rsrc.long()])
+    W = _rand(E, F, H, scale=0.05, seed=23)
+    y = ops.grouped_gemm(xp, off, W, act="silu")
+    yr = ops.grouped_gemm(xp.cpu(), roff, W.cpu(), act="silu")
+    _close(y.cpu(), yr, 2e-2)
+    eo = _rand(M * k, H, seed=24)
+    _close(ops.moe_combine(eo, slot, w).cpu(), ops.moe_combine(eo.cpu(), slot.cpu(), w.cpu()), 1e-2)
