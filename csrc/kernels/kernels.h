@@ -57,7 +57,7 @@ void launch_moe_align(const int32_t* topk_idx, int M, int topk, int E, int32_t* 
                       int32_t* offsets, hipStream_t s);
 void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int rows, int H, hipStream_t s);
 void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
-                        int topk, int H, hipStream_t s);
+                        int topk, int H, const int32_t* range, hipStream_t s);
 // X [rows][K] sorted by expert, offsets [E+1], W [E][N][K] -> Y [rows][N]
 void launch_grouped_gemm(const void* X, const int32_t* offsets, const void* W, void* Y, int E, int N, int K,
                          int max_rows, int act, hipStream_t s);

@@ -97,18 +97,23 @@ __global__ __launch_bounds__(256) void permute_kernel(const bf16* __restrict__ x
   for (int c = lane; c < H / 8; c += 64) o[c] = in[c];
 }
 
+// range (nullable, device int32[2]): only expert-sorted slots in [range[0], range[1]) count —
+// one expert's share of the output (zero for tokens not routed to it)
 __global__ __launch_bounds__(256) void combine_kernel(const bf16* __restrict__ eo, const int32_t* __restrict__ slot_of,
                                                       const float* __restrict__ w, bf16* __restrict__ y, int M,
-                                                      int topk, int H) {
+                                                      int topk, int H, const int32_t* __restrict__ range) {
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (m >= M) return;
+  const int r0 = range ? range[0] : 0, r1 = range ? range[1] : 0x7fffffff;
   bf16x8* yo = reinterpret_cast<bf16x8*>(y + (size_t)m * H);
   for (int c = lane; c < H / 8; c += 64) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int j = 0; j < topk; ++j) {
+      const int sl = slot_of[m * topk + j];
+      if (sl < r0 || sl >= r1) continue;
       const float g = w[m * topk + j];
-      const bf16x8 v = reinterpret_cast<const bf16x8*>(eo + (size_t)slot_of[m * topk + j] * H)[c];
+      const bf16x8 v = reinterpret_cast<const bf16x8*>(eo + (size_t)sl * H)[c];
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += g * bf2f(v[e]);
     }
@@ -139,7 +144,7 @@ void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int r
 }
 
 void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
-                        int topk, int H, hipStream_t s) {
+                        int topk, int H, const int32_t* range, hipStream_t s) {
   hipLaunchKernelGGL(combine_kernel, dim3((M + 3) / 4), dim3(256), 0, s, (const bf16*)expert_out, slot_of, weights,
-                     (bf16*)y, M, topk, H);
+                     (bf16*)y, M, topk, H, range);
 }

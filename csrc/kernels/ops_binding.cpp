@@ -221,15 +221,23 @@ at::Tensor moe_permute(const at::Tensor& x, const at::Tensor& src_rows) {
   return out;
 }
 
-at::Tensor moe_combine(const at::Tensor& eo, const at::Tensor& slot_of, const at::Tensor& w) {
+at::Tensor moe_combine(const at::Tensor& eo, const at::Tensor& slot_of, const at::Tensor& w,
+                       const c10::optional<at::Tensor>& range, const c10::optional<at::Tensor>& out) {
   check_bf16(eo, "expert_out");
   TORCH_CHECK(eo.dim() == 2 && eo.is_contiguous() && eo.size(1) % 8 == 0, "expert_out must be contiguous [R][H]");
   TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kFloat && w.is_contiguous(), "weights must be fp32 [M][k]");
   TORCH_CHECK(slot_of.numel() == w.numel() && slot_of.scalar_type() == at::kInt, "slot_of mismatch");
   const int64_t M = w.size(0), k = w.size(1), H = eo.size(1);
-  auto y = at::empty({M, H}, eo.options());
+  const int32_t* rp = nullptr;
+  if (range.has_value()) {
+    TORCH_CHECK(range->scalar_type() == at::kInt && range->numel() == 2 && range->is_contiguous(),
+                "range must be contiguous int32[2]");
+    rp = range->data_ptr<int32_t>();
+  }
+  at::Tensor y = out.has_value() ? as2d(*out) : at::empty({M, H}, eo.options());
+  TORCH_CHECK(y.is_contiguous() && y.size(0) == M && y.size(1) == H, "out mismatch");
   launch_moe_combine(eo.data_ptr(), slot_of.data_ptr<int32_t>(), w.data_ptr<float>(), y.data_ptr(), (int)M, (int)k,
-                     (int)H, cur_stream());
+                     (int)H, rp, cur_stream());
   return y;
 }
 
@@ -270,6 +278,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_router", &moe_router);
   m.def("moe_align", &moe_align);
   m.def("moe_permute", &moe_permute);
-  m.def("moe_combine", &moe_combine);
+  m.def("moe_combine", &moe_combine, py::arg("expert_out"), py::arg("slot_of"), py::arg("weights"),
+        py::arg("range") = py::none(), py::arg("out") = py::none());
   m.def("grouped_gemm", &grouped_gemm, py::arg("X"), py::arg("offsets"), py::arg("W"), py::arg("act") = 0);
 }

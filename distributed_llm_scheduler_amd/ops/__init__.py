@@ -179,8 +179,14 @@ def rmsnorm(x, w, eps=1e-5, residual=None, out=None, sum_out=None):
         return (y, s.view(x.shape)) if residual is not None else y
     if residual is not None:
         s = (x.float() + residual.float()).to(x.dtype)
-        return ref_rmsnorm(s, w, eps), s
-    return ref_rmsnorm(x, w, eps)
+        y = ref_rmsnorm(s, w, eps)
+        if sum_out is not None:
+            sum_out.copy_(s)
+        if out is not None:
+            out.copy_(y)
+        return y, s
+    y = ref_rmsnorm(x, w, eps)
+    return out.copy_(y) if out is not None else y
 
 
 def attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=None, out=None):
@@ -267,12 +273,35 @@ def moe_permute(x, src_rows):
     return x[src_rows.long()]
 
 
-def moe_combine(expert_out, slot_of, weights):
+def moe_combine(expert_out, slot_of, weights, slot_range=None, out=None):
+    """y[m] = sum_j w[m,j] * expert_out[slot_of[m,j]]; with ``slot_range`` (device int32[2])
+    only slots in [r0, r1) contribute (one expert's share, zero elsewhere)."""
     if _gpu(expert_out):
-        return ext().moe_combine(expert_out.contiguous(), slot_of, weights.contiguous())
+        return ext().moe_combine(expert_out.contiguous(), slot_of, weights.contiguous(), slot_range, out)
     M, k = weights.shape
-    g = expert_out.float()[slot_of.long()].reshape(M, k, -1)
-    return (g * weights.float()[..., None]).sum(1).to(expert_out.dtype)
+    sl = slot_of.long().reshape(M, k)
+    keep = torch.ones_like(sl, dtype=torch.bool)
+    if slot_range is not None:
+        keep = (sl >= int(slot_range[0])) & (sl < int(slot_range[1]))
+    g = expert_out.float()[sl.clamp(0, expert_out.shape[0] - 1).reshape(-1)].reshape(M, k, -1)
+    g = torch.where(keep[..., None], g, torch.zeros_like(g))  # rows outside the range are never read
+    y = (g * weights.float()[..., None]).sum(1).to(expert_out.dtype)
+    return out.copy_(y) if out is not None else y
+
+
+def moe_expert(h, router_logits, w_gate_up, w_down, expert, n_experts, top_k, out=None):
+    """One expert's contribution for every token (zero where it is not routed): routing
+    is recomputed from the router logits, only the expert's routed rows are gathered and
+    run through gate_up GEMM -> SwiGLU -> down GEMM (grouped GEMM over a device-side row
+    range: no host synchronisation)."""
+    idx, gate = moe_router(router_logits, top_k)
+    src, slot, off = moe_align(idx, n_experts)
+    xp = moe_permute(h, src)
+    rng = off[expert:expert + 2].contiguous()
+    gu = grouped_gemm(xp, rng, w_gate_up.unsqueeze(0))
+    a = swiglu(gu)
+    y = grouped_gemm(a, rng, w_down.unsqueeze(0))
+    return moe_combine(y, slot, gate, rng, out)
 
 
 def grouped_gemm(X, offsets, W, act=None):
@@ -280,7 +309,7 @@ def grouped_gemm(X, offsets, W, act=None):
     a = ACT[act] if not isinstance(act, int) else act
     if _gpu(X):
         return ext().grouped_gemm(X.contiguous(), offsets, W.contiguous(), a)
-    out = torch.empty(X.shape[0], W.shape[1], dtype=X.dtype)
+    out = torch.zeros(X.shape[0], W.shape[1], dtype=X.dtype)
     off = offsets.tolist()
     for e in range(W.shape[0]):
         if off[e + 1] > off[e]:

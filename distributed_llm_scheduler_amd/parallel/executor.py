@@ -232,30 +232,18 @@ class DAGExecutor:
             ops.linear(x, self._w(W["w_gate_up"]), out=gu)
             ops.swiglu(gu, out=h)
             ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out))
-        elif k == "moe":
-            self._run_moe(head, residual, out)
+        elif k == "moe_expert":
+            h = self._flat(self._x(head.op.inputs[0]))
+            logits = self._flat(self._x(head.op.inputs[1]))
+            ops.moe_expert(h, logits, self._w(W["w_gate_up"]), self._w(W["w_down"]), a["expert"], a["n_experts"],
+                           a["top_k"], out=self._flat(out))
+        elif k == "moe_combine":
+            acc = self._x(head.op.inputs[-1])
+            for name in head.op.inputs[:-1]:
+                ops.add(self._x(name), acc, out=out)
+                acc = out
         else:
             raise NotImplementedError(f"op kind {k!r}")
-
-    def _run_moe(self, t: Task, residual, out) -> None:
-        a, W = t.op.attrs, t.op.weights
-        x = self._flat(self._x(t.op.inputs[0]))
-        E, k = a["n_experts"], a["top_k"]
-        logits = ops.linear(x, self._w(W["w_router"]))
-        idx, gate = ops.moe_router(logits, k)
-        src, slot, off = ops.moe_align(idx, E)
-        xp = ops.moe_permute(x, src)
-        Wgu = torch.stack([self._w(n) for n in W["experts_gate_up"]]) if isinstance(W["experts_gate_up"], list) \
-            else self._w(W["experts_gate_up"])
-        Wd = torch.stack([self._w(n) for n in W["experts_down"]]) if isinstance(W["experts_down"], list) \
-            else self._w(W["experts_down"])
-        gu = ops.grouped_gemm(xp, off, Wgu)
-        h = ops.swiglu(gu)
-        eo = ops.grouped_gemm(h, off, Wd)
-        y = ops.moe_combine(eo, slot, gate)
-        if residual is not None:
-            y = ops.add(y, residual)
-        self._flat(out).copy_(y)
 
     # ------------------------------------------------------------------- step
     def _step_body(self, stats: StepStats, timeline: Optional[list] = None) -> None:

@@ -104,3 +104,51 @@ def test_two_ranks_gloo(placement, scheduler):
         assert err < 0.02 * scale
     if placement == "pipeline":
         assert sum(r["sends"] for r in results) > 0 and sum(r["recvs"] for r in results) > 0
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+def test_llama_family_matches_reference(model):
+    p = runtime.plan(model, world=1, scheduler="EFT", seq=32, batch=2)
+    assert p.completed == p.total
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, "cpu", store)
+    ex.step()
+    err, scale = _ref_check(p, ex, store)
+    assert err < 0.03 * scale
+
+
+def _ep_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # tiny caps force the scheduler to spread expert nodes over both ranks (EP)
+        p = runtime.plan("tiny-mixtral", world=world, scheduler="MRU_spec", seq=32, batch=1, cap_gb=0.0006)
+        store = runtime.make_store(p)
+        ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
+        st = ex.step()
+        experts = {r for t, r in p.placement.items() if "_expert_" in t}
+        res = {"rank": rank, "sends": st.sends, "experts_on": sorted(experts), "completed": p.completed,
+               "total": p.total, "errs": []}
+        if p.placement.get("output_projection") == rank:
+            res["errs"].append(_ref_check(p, ex, store))
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_mixtral_expert_parallel_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ep_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs)
+    res = [q.get(timeout=5) for _ in range(2)]
+    assert res[0]["completed"] == res[0]["total"]
+    assert res[0]["experts_on"] == [0, 1]  # experts really are split across GPUs
+    assert sum(r["sends"] for r in res) > 0
+    errs = [e for r in res for e in r["errs"]]
+    assert len(errs) == 1 and errs[0][0] < 0.03 * errs[0][1]
