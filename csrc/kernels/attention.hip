@@ -1,177 +1,209 @@
-// Flash-style attention forward on MFMA (causal or full, MHA or GQA), bf16 in/out.
+// Flash attention forward on MFMA (causal or full, MHA or GQA), bf16 in/out — v2.
 //
-// One workgroup = 64 query rows of one (batch, head): 4 waves x 16 rows. Per 64-key
-// tile: K is staged row-major into LDS (16-B chunks XOR-swizzled by row, T2) and V is
-// staged transposed (V^T[d][key]) so both MFMA products read their B fragments as
-// contiguous 16-byte LDS vectors:
-//   S  = Q K^T   mfma_f32_16x16x32_bf16, Q fragments held in registers for the whole loop
-//   O += P V     P goes through a per-wave LDS tile to move from the accumulator layout
-//                (row = 4*(l>>4)+i) to the A-operand layout (row = l&15)
-// Online softmax keeps (m, l) per row in fp32 with exp2 and a log2(e)-prescaled scale;
-// rows reduce across the 16 lanes of an MFMA column group with 4 xor-shuffles.
-// The score matrix never touches HBM. Causal blocks stop at their diagonal tile.
+// Workgroup = 64 queries of one (batch, head): 4 waves x 16 queries; 64-key tiles.
+// Swapped-operand formulation (cdna_hip_programming.md §3 "accumulator tile as the
+// next MFMA's operand", T10, T12 idea without the permlanes):
+//   S^T = K Q^T    A = K rows straight from LDS (16-B reads), B = Q^T from registers.
+//                  Each lane then holds 16 scores of ONE query -> the online-softmax max and
+//                  sum need 2 cross-lane shuffles (xor 16, 32) instead of a 16-lane tree.
+//   O^T += V^T P^T B = P^T is taken from the S^T accumulators IN PLACE (no LDS round
+//                  trip): the MFMA's k order is permuted identically on both operands
+//                  (element j of lane group g <-> key 16*(j>>2) + 4g + (j&3)), and the
+//                  matching V^T fragment is two ds_read_b64_tr_b16 transposed reads of the
+//                  row-major V tile.
+// K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4; XOR chunk swizzle applied to the
+// per-lane source address, rule 21), double-buffered: wait(tile t) -> ONE barrier ->
+// issue(tile t+1 into the buffer everyone finished in t-1) -> compute t.
+// Causal blocks stop at the diagonal tile and are launched heaviest-first.
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
-template <int D>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ Q, int ldq,
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int D, int NW_>
+struct AttnCfg {
+  static constexpr int NW = NW_;                 // waves per block (16 queries each)
+  static constexpr int QB = 16 * NW;             // queries per block
+  static constexpr int KT = 64;                  // keys per tile
+  static constexpr int RB = D * 2;               // bytes per K/V row
+  static constexpr int CH = D / 8;               // 16-B chunks per row
+  static constexpr int ROWS_PER_INSTR = 1024 / RB;
+  static constexpr int INSTR = KT / ROWS_PER_INSTR;  // per operand per tile
+  static constexpr int PW = 2 * INSTR / NW;           // per wave per tile (K and V)
+  static constexpr int TILE_BYTES = KT * RB;          // one operand
+  static constexpr int BUF_BYTES = 2 * TILE_BYTES;    // K + V
+  static constexpr int NQK = D / 32;                  // k-steps of S^T
+  static constexpr int ND = D / 16;                   // output d-subtiles
+};
+
+__device__ __forceinline__ int swz(int row, int ch_mask) { return row & ch_mask; }
+
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ Q, int ldq,
                                                        const bf16* __restrict__ Kp, int ldk,
                                                        const bf16* __restrict__ Vp, int ldv, bf16* __restrict__ O,
                                                        int ldo, int S, int n_head, int n_kv_head, float scale_log2,
-                                                       int causal) {
-  constexpr int KT = 64;            // keys per tile
-  constexpr int CH = D / 8;         // 16-B chunks per K row
-  constexpr int VCH = KT / 8;       // 16-B chunks per V^T row
-  constexpr int ND = D / 16;        // output fragments per wave
-  constexpr int NQK = D / 32;       // k-steps of Q K^T
-  __shared__ bf16x8 smem[KT * CH + D * VCH + 4 * 16 * VCH];
-  bf16x8* Ks = smem;
-  bf16x8* Vt = smem + KT * CH;
-  bf16x8* Ps = Vt + D * VCH;
-  bf16* Vt_e = reinterpret_cast<bf16*>(Vt);
-
+                                                       int causal, int n_qtiles) {
+  using C = AttnCfg<D, NW>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::BUF_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-  const int g = h / (n_head / n_kv_head);
-  const int q0 = qt * 64;
+  const int g = lane >> 4, li = lane & 15;
+  const int qt = causal ? (n_qtiles - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heaviest first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kvh = h / (n_head / n_kv_head);
+  const int q0 = qt * C::QB + wave * 16;  // this wave's 16 queries
   const size_t tok0 = (size_t)b * S;
 
-  // Q fragments for this wave's 16 rows (A operand: row l&15, k = 8*(l>>4)+j)
-  bf16x8 qf[NQK];
+  // Q^T as the B operand: lane holds Q[q0 + li][32*ks + 8*g + j]
+  bf16x8 qf[C::NQK];
   {
-    const int row = q0 + wave * 16 + (lane & 15);
+    const int qrow = min(q0 + li, S - 1);
 #pragma unroll
-    for (int kk = 0; kk < NQK; ++kk) {
-      const int d = kk * 32 + 8 * (lane >> 4);
-      qf[kk] = row < S ? *reinterpret_cast<const bf16x8*>(Q + (tok0 + row) * ldq + h * D + d) : bf16x8{};
-    }
-  }
-  f32x4 o[ND];
-#pragma unroll
-  for (int i = 0; i < ND; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_i[4], l_i[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    m_i[i] = -INFINITY;
-    l_i[i] = 0.f;
+    for (int ks = 0; ks < C::NQK; ++ks)
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + qrow) * ldq + h * D + 32 * ks + 8 * g);
   }
 
-  const int kv_end = causal ? min(S, q0 + 64) : S;
-  for (int k0 = 0; k0 < kv_end; k0 += KT) {
-    __syncthreads();  // previous tile fully consumed
-    // stage K (row-major, swizzled) and V^T
+  // LDS-DMA source pointers: instruction j of this wave -> operand (K or V) rows
+  const int kv_end = causal ? min(S, qt * C::QB + C::QB) : S;
+  const int ntiles = (kv_end + C::KT - 1) / C::KT;
+  auto issue = [&](int t) {
+    char* buf = smem + (t & 1) * C::BUF_BYTES;
 #pragma unroll
-    for (int it = 0; it < (KT * CH) / 256; ++it) {
-      const int qd = tid + it * 256, row = qd / CH, c = qd % CH;
-      const int key = k0 + row;
-      bf16x8 kv = {}, vv = {};
-      if (key < S) {
-        kv = *reinterpret_cast<const bf16x8*>(Kp + (tok0 + key) * ldk + g * D + c * 8);
-        vv = *reinterpret_cast<const bf16x8*>(Vp + (tok0 + key) * ldv + g * D + c * 8);
-      }
-      Ks[row * CH + (c ^ (row & (CH - 1)))] = kv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int d = c * 8 + e;
-        Vt_e[(d * VCH + ((row >> 3) ^ (d & 7))) * 8 + (row & 7)] = vv[e];
-      }
+    for (int j = 0; j < C::PW; ++j) {
+      const int ins = wave * C::PW + j;            // 0 .. 2*INSTR-1
+      const int op = ins / C::INSTR;               // 0 = K, 1 = V
+      const int r0 = (ins % C::INSTR) * C::ROWS_PER_INSTR;
+      const int row = r0 + lane / C::CH;
+      const int pos = lane % C::CH;
+      const int key = min(t * C::KT + row, S - 1);
+      const int gch = pos ^ swz(row, C::CH - 1);
+      const bf16* base = op == 0 ? (Kp + (tok0 + key) * ldk) : (Vp + (tok0 + key) * ldv);
+      __builtin_amdgcn_global_load_lds((const void*)(base + kvh * D + gch * 8),
+                                       (__attribute__((address_space(3))) void*)(buf + op * C::TILE_BYTES + r0 * C::RB),
+                                       16, 0, 0);
     }
-    __syncthreads();
+  };
 
-    // S = Q K^T : 16 rows x 64 keys per wave
+  f32x4 o[C::ND];
+#pragma unroll
+  for (int i = 0; i < C::ND; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;  // for query q0 + li (replicated over the 4 lane groups)
+  const int my_q = q0 + li;
+
+  issue(0);
+  for (int t = 0; t < ntiles; ++t) {
+    wait_vm0();
+    raw_barrier();
+    if (t + 1 < ntiles) issue(t + 1);
+    const char* kb = smem + (t & 1) * C::BUF_BYTES;
+    const char* vb = kb + C::TILE_BYTES;
+    const int key0 = t * C::KT;
+
+    // ---- S^T = K Q^T : 4 key-subtiles x 16 queries
     f32x4 s[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       s[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int row = n * 16 + (lane & 15);
+      const int row = 16 * n + li;
 #pragma unroll
-      for (int kk = 0; kk < NQK; ++kk) {
-        const int chunk = kk * 4 + (lane >> 4);
-        s[n] = mfma16x16x32(qf[kk], Ks[row * CH + (chunk ^ (row & (CH - 1)))], s[n]);
+      for (int ks = 0; ks < C::NQK; ++ks) {
+        const int c = 4 * ks + g;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * C::RB + ((c ^ swz(row, C::CH - 1)) << 4));
+        s[n] = mfma16x16x32(kf, qf[ks], s[n]);
       }
     }
-    // mask + online softmax (rows 4*(l>>4)+i, keys n*16 + (l&15))
-    const int qrow_base = q0 + wave * 16 + 4 * (lane >> 4);
-    float p[4][4];
+    // ---- online softmax for query my_q; scores s[n][i] <-> key key0 + 16n + 4g + i
+    const bool diag = causal && (key0 + C::KT > qt * C::QB);
+    float mx = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int qrow = qrow_base + i;
-      float mx = -INFINITY;
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int key = k0 + n * 16 + (lane & 15);
+      for (int i = 0; i < 4; ++i) {
+        const int key = key0 + 16 * n + 4 * g + i;
         float v = s[n][i] * scale_log2;
-        if (key >= S || (causal && key > qrow)) v = -INFINITY;
-        p[n][i] = v;
+        if (key >= S || (diag && key > my_q)) v = -INFINITY;
+        s[n][i] = v;
         mx = fmaxf(mx, v);
       }
-      mx = group16_max(mx);
-      const float m_new = fmaxf(m_i[i], mx);
-      const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_i[i] - m_new);
-      float sum = 0.f;
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_run - m_new);
+    float sum = 0.f;
+    bf16x8 pf[2];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const float e = (m_new == -INFINITY) ? 0.f : exp2f(p[n][i] - m_new);
-        p[n][i] = e;
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = (m_new == -INFINITY) ? 0.f : exp2f(s[n][i] - m_new);
         sum += e;
+        pf[n >> 1][4 * (n & 1) + i] = f2bf(e);
       }
-      sum = group16_sum(sum);
-      l_i[i] = l_i[i] * alpha + sum;
-      m_i[i] = m_new;
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    l_run = l_run * alpha + sum;
+    m_run = m_new;
 #pragma unroll
-      for (int dn = 0; dn < ND; ++dn) o[dn][i] *= alpha;
-    }
-    // P -> per-wave LDS tile [16 rows][64 keys], swizzled by row
-    bf16* Pw = reinterpret_cast<bf16*>(Ps + wave * 16 * VCH);
+    for (int dn = 0; dn < C::ND; ++dn) o[dn] *= alpha;
+
+    // ---- O^T += V^T P^T ; V^T fragment element j <-> key 32ks + 16(j>>2) + 4g + (j&3)
+    const int q4 = li >> 2, p4 = li & 3;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 4 * (lane >> 4) + i;
+    for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int col = n * 16 + (lane & 15);
-        Pw[(r * VCH + ((col >> 3) ^ (r & 7))) * 8 + (col & 7)] = f2bf(p[n][i]);
-      }
-    }
-    __syncthreads();
-    // O += P V
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int r = lane & 15, chunk = kk * 4 + (lane >> 4);
-      const bf16x8 pf = Ps[wave * 16 * VCH + r * VCH + (chunk ^ (r & 7))];
-#pragma unroll
-      for (int dn = 0; dn < ND; ++dn) {
-        const int d = dn * 16 + (lane & 15);
-        o[dn] = mfma16x16x32(pf, Vt[d * VCH + (chunk ^ (d & 7))], o[dn]);
+      for (int dn = 0; dn < C::ND; ++dn) {
+        const int c = 2 * dn + (p4 >> 1);
+        const int row0 = 32 * ks + 4 * g + q4;
+        const int row1 = row0 + 16;
+        const lds_bf16x4* a0 = (const lds_bf16x4*)(vb + row0 * C::RB + ((c ^ swz(row0, C::CH - 1)) << 4) + (p4 & 1) * 8);
+        const lds_bf16x4* a1 = (const lds_bf16x4*)(vb + row1 * C::RB + ((c ^ swz(row1, C::CH - 1)) << 4) + (p4 & 1) * 8);
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dn] = mfma16x16x32(vf, pf[ks], o[dn]);
       }
     }
   }
-  // normalise and store
+  // ---- normalise and store O[q][d]: lane holds d = 16dn + 4g + i for query my_q
+  if (my_q < S) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    bf16* orow = O + (tok0 + my_q) * ldo + h * D;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int qrow = q0 + wave * 16 + 4 * (lane >> 4) + i;
-    if (qrow >= S) continue;
-    const float inv = l_i[i] > 0.f ? 1.f / l_i[i] : 0.f;
-    bf16* orow = O + (tok0 + qrow) * ldo + h * D;
+    for (int dn = 0; dn < C::ND; ++dn) {
+      bf16x4 v;
 #pragma unroll
-    for (int dn = 0; dn < ND; ++dn) orow[dn * 16 + (lane & 15)] = f2bf(o[dn][i] * inv);
+      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dn][i] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * dn + 4 * g) = v;
+    }
   }
 }
 
 }  // namespace
 
-void launch_attention_fwd(const AttnArgs& a, hipStream_t s) {
-  dim3 grid((a.S + 63) / 64, a.n_head, a.B), block(256);
+template <int D, int NW>
+static void launch_attn(const AttnArgs& a, hipStream_t s) {
+  const int nq = (a.S + 16 * NW - 1) / (16 * NW);
+  dim3 grid(nq, a.n_head, a.B), block(64 * NW);
   const float sl2 = a.scale * 1.4426950408889634f;
-  const bf16* q = static_cast<const bf16*>(a.q);
-  const bf16* k = static_cast<const bf16*>(a.k);
-  const bf16* v = static_cast<const bf16*>(a.v);
-  bf16* o = static_cast<bf16*>(a.o);
-  if (a.D == 64)
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, s, q, a.ldq, k, a.ldk, v, a.ldv, o, a.ldo, a.S,
-                       a.n_head, a.n_kv_head, sl2, a.causal);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, block, 0, s, q, a.ldq, k, a.ldk, v, a.ldv, o, a.ldo, a.S,
-                       a.n_head, a.n_kv_head, sl2, a.causal);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NW>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
+                     static_cast<const bf16*>(a.k), a.ldk, static_cast<const bf16*>(a.v), a.ldv,
+                     static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq);
+}
+
+void launch_attention_fwd(const AttnArgs& a, hipStream_t s) {
+  // small grids (few heads x short sequences) use 32-query blocks to fill more CUs
+  const long blocks64 = (long)((a.S + 63) / 64) * a.n_head * a.B;
+  const bool small = blocks64 < 512;
+  if (a.D == 64) {
+    if (small) launch_attn<64, 2>(a, s);
+    else launch_attn<64, 4>(a, s);
+  } else {
+    if (small) launch_attn<128, 2>(a, s);
+    else launch_attn<128, 4>(a, s);
+  }
 }

@@ -1,0 +1,389 @@
+// Multistage bf16 GEMM with LDS-DMA staging (global_load_lds_dwordx4), optional split-K.
+//
+//   C = act(alpha * A @ W^T + bias) + R      A [M][K], W [N][K] (K contiguous), K % 64 == 0
+//
+// Why this structure (cdna_hip_programming.md §5 "Pipelining across barriers", T1, T2):
+//  * GPT-2 / Llama serving GEMMs have M = 512 rows: a grid barely covers the 256 CUs, so
+//    each CU runs ~1 block and a K-loop that keeps ONE tile in flight is latency-bound —
+//    especially when the weights stream cold from HBM (measured 1.6-2x slower inside the
+//    DAG than in a hot-cache loop). Here STAGES-1 K-tiles are in flight per block.
+//  * LDS-DMA needs no staging VGPRs and no ds_write pass; the image is lane-linear (1 KiB
+//    per wave instruction = 8 rows x 128 B), so the XOR swizzle (chunk ^ (row & 7)) is
+//    applied to the per-lane SOURCE address and again on the ds_read (rule 21).
+//  * ONE raw s_barrier per K-tile: wait(tile kt) -> barrier -> issue(tile kt+STAGES-1 into
+//    the buffer everyone finished reading before this barrier) -> MFMAs on tile kt. The
+//    wait is a counted vmcnt (never 0 in steady state); __syncthreads() is avoided because
+//    its fence drains every outstanding DMA.
+//  * Split-K (host-chosen) multiplies the block count for skinny N; partial fp32 tiles go
+//    to a workspace slab and a vectorised reduce kernel applies the fused epilogue.
+//  * XCD-aware tile order (T1): the blocks of one weight panel share an XCD's L2.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until at most `ahead` tiles (PW DMA instructions each) are still in flight; the
+// immediate must be a compile-time constant, so unroll over the possible values
+template <int PW, int A>
+__device__ __forceinline__ void wait_tiles(int ahead) {
+  if constexpr (A == 0) {
+    wait_vm<0>();
+  } else {
+    if (ahead >= A) wait_vm<PW * A>();
+    else wait_tiles<PW, A - 1>(ahead);
+  }
+}
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_;
+  static constexpr int BK = 64, CH = 8;
+  static constexpr int NW = WM * WN, T = 64 * NW;
+  static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static constexpr int ROWS = BM + BN, INSTR = ROWS / 8, PW = INSTR / NW;
+  static constexpr int STAGE = ROWS * CH;  // bf16x8 units
+  static_assert(INSTR % NW == 0, "stage rows must split evenly over waves");
+  static_assert(FM >= 1 && FN >= 1, "wave tile too small");
+  static_assert(PW * (STAGES - 2) <= 63, "vmcnt range");
+  static_assert(STAGES >= 2 && STAGES <= 8, "stages");
+};
+
+template <class C>
+__global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
+                                                         const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
+                                                         int ldc, const bf16* __restrict__ bias,
+                                                         const bf16* __restrict__ R, int ldr,
+                                                         float* __restrict__ part, int M, int N, int K, int act,
+                                                         float alpha, int tiles_m, int tiles_n, int splitk,
+                                                         int kslice, const float* __restrict__ ln_colsum,
+                                                         int ln_mode, float ln_eps) {
+  __shared__ bf16x8 smem[C::STAGES * C::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int ntile = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, ntile * splitk);
+  const int ks = bid / ntile, tile = bid % ntile;
+  const int tm = tile % tiles_m, tn = tile / tiles_m;
+  const int m0 = tm * C::BM, n0 = tn * C::BN;
+  const int kbeg = ks * kslice;
+  const int nk = kslice / C::BK;
+
+  // per-lane DMA source rows (fixed over the K loop): instruction j of this wave covers
+  // stage rows 8*(wave*PW + j) .. +7; lane -> row +lane/8, LDS chunk position lane%8,
+  // global chunk (lane%8) ^ (row & 7). Rows past M/N are clamped (results discarded).
+  const bf16* src[C::PW];
+#pragma unroll
+  for (int j = 0; j < C::PW; ++j) {
+    const int row = 8 * (wave * C::PW + j) + (lane >> 3);
+    const int gch = (lane & 7) ^ (row & 7);
+    if (row < C::BM) {
+      const int gm = min(m0 + row, M - 1);
+      src[j] = A + (size_t)gm * lda + kbeg + gch * 8;
+    } else {
+      const int gn = min(n0 + row - C::BM, N - 1);
+      src[j] = W + (size_t)gn * ldw + kbeg + gch * 8;
+    }
+  }
+  auto issue = [&](int kt) {
+    bf16x8* stage = smem + (kt % C::STAGES) * C::STAGE;
+#pragma unroll
+    for (int j = 0; j < C::PW; ++j) {
+      __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * C::BK),
+                                       (__attribute__((address_space(3))) void*)(stage + (wave * C::PW + j) * 64),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused LayerNorm/RMSNorm prologue: row statistics of A accumulated from the A fragments
+  // that stream through LDS anyway (waves with wn == 0; full K per block, splitk == 1)
+  const bool ln_acc = ln_mode != 0 && wn == 0;
+  float st_s[C::FM], st_q[C::FM];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < C::STAGES - 1; ++s)
+    if (s < nk) issue(s);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(C::STAGES - 2, nk - 1 - kt);  // tiles issued after kt, still allowed in flight
+    wait_tiles<C::PW, C::STAGES - 2>(ahead);
+    raw_barrier();
+    if (kt + C::STAGES - 1 < nk) issue(kt + C::STAGES - 1);
+    const bf16x8* s = smem + (kt % C::STAGES) * C::STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8 af[C::FM], bw[C::FN];
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int row = wm * C::WTM + i * 16 + (lane & 15);
+        af[i] = s[row * C::CH + (chunk ^ (row & 7))];
+      }
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int row = C::BM + wn * C::WTN + j * 16 + (lane & 15);
+        bw[j] = s[row * C::CH + (chunk ^ (row & 7))];
+      }
+      if (ln_acc) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = bf2f(af[i][e]);
+            st_s[i] += x;
+            st_q[i] += x * x;
+          }
+      }
+      // swapped operands: acc = (W A^T) tile, i.e. C^T — lane holds 4 consecutive output
+      // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[j], af[i], acc[i][j]);
+    }
+  }
+
+  // epilogue: lane (g = lane>>4, r = lane&15) of fragment (i, j) holds C[row][col..col+3]
+  // with row = m0 + wm*WTM + 16i + r, col = n0 + wn*WTN + 16j + 4g
+  const int g4 = (lane >> 4) * 4, r16 = lane & 15;
+  float ln_rs[C::FM], ln_mu[C::FM];
+  if (ln_mode != 0) {
+    // reduce the 4 lane groups (k-chunks) -> full-row sums, publish per row via LDS
+    float* stats = reinterpret_cast<float*>(smem);
+    raw_barrier();  // every wave is past its last LDS read of the staging buffers
+    if (ln_acc) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        float a = st_s[i], q = st_q[i];
+        a += __shfl_xor(a, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (lane < 16) {
+          const int lr = wm * C::WTM + i * 16 + lane;
+          stats[2 * lr] = a;
+          stats[2 * lr + 1] = q;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const int lr = wm * C::WTM + i * 16 + r16;
+      const float a = stats[2 * lr], q = stats[2 * lr + 1];
+      const float inv_k = 1.0f / (float)K;
+      if (ln_mode == 1) {
+        const float mu = a * inv_k;
+        const float var = fmaxf(q * inv_k - mu * mu, 0.f);
+        ln_mu[i] = mu;
+        ln_rs[i] = rsqrtf(var + ln_eps);
+      } else {
+        ln_mu[i] = 0.f;
+        ln_rs[i] = rsqrtf(q * inv_k + ln_eps);
+      }
+    }
+  }
+  // 8-byte vector stores need 8-B aligned rows (ldc % 4 == 0) — N itself may be ragged
+  // (the LM head writes 50257 columns into rows padded to 50304); a fragment whose 4
+  // columns straddle N falls back to scalars.
+  const bool vec_ok = (ldc % 4 == 0) && (!R || ldr % 4 == 0);
+  if (splitk > 1) {
+    float* P = part + (size_t)ks * M * N;
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const int row = m0 + wm * C::WTM + i * 16 + r16;
+      if (row >= M) continue;
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int col = n0 + wn * C::WTN + j * 16 + g4;
+        if (N % 4 == 0 && col + 3 < N) {
+          *reinterpret_cast<f32x4*>(P + (size_t)row * N + col) = acc[i][j];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < N) P[(size_t)row * N + col + e] = acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < C::FN; ++j) {
+    const int col = n0 + wn * C::WTN + j * 16 + g4;
+    if (col >= N) continue;
+    const bool full = vec_ok && col + 3 < N;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+      if (full) {
+        const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = bf2f(b4[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const int row = m0 + wm * C::WTM + i * 16 + r16;
+      if (row >= M) continue;
+      float v[4];
+      if (ln_mode != 0) {
+        // W.LN(x) = rstd * (W' x - mu * colsum(W')) + (bias + W b), W' = W * ln_w (host-derived)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float cs = (col + e < N) ? ln_colsum[col + e] : 0.f;
+          v[e] = apply_act(ln_rs[i] * (acc[i][j][e] - ln_mu[i] * cs) + bv[e], act);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = apply_act(alpha * acc[i][j][e] + bv[e], act);
+      }
+      if (full) {
+        if (R) {
+          const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(R + (size_t)row * ldr + col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bf2f(r4[e]);
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x4*>(Cp + (size_t)row * ldc + col) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (col + e >= N) continue;
+          float x = v[e];
+          if (R) x += bf2f(R[(size_t)row * ldr + col + e]);
+          Cp[(size_t)row * ldc + col + e] = f2bf(x);
+        }
+      }
+    }
+  }
+}
+
+// out = act(alpha * sum_s P[s] + bias) + R, 8 columns per lane (N % 8 == 0 path) or scalar
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splitk, int M, int N,
+                                                            bf16* __restrict__ C, int ldc,
+                                                            const bf16* __restrict__ bias,
+                                                            const bf16* __restrict__ R, int ldr, int act,
+                                                            float alpha) {
+  const int nv = N / 8;
+  const int64_t total = (int64_t)M * nv;
+  const size_t slab = (size_t)M * N;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / nv), c = (int)(i % nv) * 8;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < splitk; ++s) {
+      const f32x4* p = reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c);
+      const f32x4 a = p[0], b = p[1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += a[e];
+        v[4 + e] += b[e];
+      }
+    }
+    bf16x8 bv = {}, rv = {};
+    if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
+    if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = apply_act(alpha * v[e] + (bias ? bf2f(bv[e]) : 0.f), act);
+      if (R) x += bf2f(rv[e]);
+      o[e] = f2bf(x);
+    }
+    *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + c) = o;
+  }
+}
+
+template <class C>
+void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
+            float ln_eps) {
+  static_assert(2 * C::BM * sizeof(float) <= C::STAGES * C::STAGE * 16, "LN stats must fit the staging LDS");
+  const int tiles_m = (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
+  const int kslice = a.K / splitk;
+  dim3 grid(tiles_m * tiles_n * splitk), block(C::T);
+  hipLaunchKernelGGL((gemm_glds_kernel<C>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, a.ldw,
+                     (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act,
+                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps);
+  if (splitk > 1) {
+    const int64_t nvec = (int64_t)a.M * (a.N / 8);
+    const int g = (int)std::min<int64_t>(2048, (nvec + 255) / 256);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, ws, splitk, a.M, a.N, (bf16*)a.C, a.ldc,
+                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha);
+  }
+}
+
+using C0 = Cfg<256, 128, 4, 2, 3>;  // 8 waves, 64x64 per wave: large GEMMs
+using C1 = Cfg<128, 128, 2, 2, 3>;  // 4 waves, 64x64 per wave
+using C2 = Cfg<128, 64, 2, 2, 4>;   // 4 waves, 64x32 per wave
+using C3 = Cfg<64, 64, 2, 2, 4>;    // 4 waves, 32x32 per wave
+using C4 = Cfg<64, 128, 2, 2, 4>;
+using C5 = Cfg<64, 64, 2, 2, 8>;    // deep pipeline: 7 K-tiles in flight (cold-weight latency)
+using C6 = Cfg<128, 64, 2, 2, 6>;   // 5 in flight, 2x rows per block
+using C7 = Cfg<128, 128, 2, 2, 4>;
+
+struct Shape {
+  int bm, bn;
+};
+constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}, {64, 128}, {64, 64}, {128, 64}, {128, 128}};
+constexpr int kNumCfg = 8;
+
+}  // namespace
+
+int gemm_glds_num_configs() { return kNumCfg; }
+
+// Heuristic: largest tile whose grid (times a split-K factor that keeps >= 4 K-tiles per
+// block) reaches ~256 blocks; split-K only when the output grid alone is too small.
+void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk) {
+  const int order[] = {0, 1, 2, 4, 3};
+  for (int oi = 0; oi < kNumCfg; ++oi) {
+    const int c = order[oi];
+    const long tiles = (long)((M + kShapes[c].bm - 1) / kShapes[c].bm) * ((N + kShapes[c].bn - 1) / kShapes[c].bn);
+    if (tiles >= 240) {
+      *cfg = c;
+      *splitk = 1;
+      return;
+    }
+  }
+  // skinny: 64x64 tiles + split-K
+  const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
+  int best = 1;
+  for (int s : {2, 3, 4, 6, 8}) {
+    if (K % (64 * s) != 0 || K / (64 * s) < 4) continue;
+    best = s;
+    if (tiles * s >= 240) break;
+  }
+  *cfg = (N % 8 == 0) ? 3 : 3;
+  *splitk = (N % 8 == 0) ? best : 1;
+}
+
+size_t gemm_glds_workspace_bytes(int M, int N, int splitk) { return splitk > 1 ? (size_t)splitk * M * N * 4 : 0; }
+
+void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s, const float* ln_colsum,
+                      int ln_mode, float ln_eps) {
+  float* ws = static_cast<float*>(workspace);
+  if (ln_mode != 0) splitk = 1;  // row statistics need the whole K range in one block
+  switch (cfg) {
+    case 0: launch<C0>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    case 1: launch<C1>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    case 2: launch<C2>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    case 4: launch<C4>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    case 5: launch<C5>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    case 6: launch<C6>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    case 7: launch<C7>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    default: launch<C3>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+  }
+}

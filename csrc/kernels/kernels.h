@@ -22,7 +22,16 @@ struct GemmArgs {
 };
 
 int gemm_pick_config(int M, int N, int K);
-void launch_gemm_bf16(const GemmArgs& a, hipStream_t s);
+void launch_gemm_bf16(const GemmArgs& a, hipStream_t s);  // register-staged, any K % 8 == 0
+
+// LDS-DMA multistage GEMM (K % 64 == 0); split-K partials need workspace_bytes of fp32
+int gemm_glds_num_configs();
+void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk);
+size_t gemm_glds_workspace_bytes(int M, int N, int splitk);
+// ln_mode: 0 none, 1 LayerNorm, 2 RMSNorm folded into the GEMM (A = raw input rows,
+// W pre-scaled by the norm gain, ln_colsum[n] = sum_k W[n][k], bias = bias + W.ln_bias)
+void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s,
+                      const float* ln_colsum = nullptr, int ln_mode = 0, float ln_eps = 1e-5f);
 
 struct AttnArgs {
   const void* q; int ldq;   // bf16, row = token (b*S + s), head h at column h*D

@@ -29,9 +29,12 @@ void check_rows(const at::Tensor& t, const char* name) {
 
 at::Tensor as2d(const at::Tensor& t) { return t.dim() == 2 ? t : t.reshape({-1, t.size(-1)}); }
 
+// config: -1 auto; 0..4 LDS-DMA multistage configs; 10..13 register-staged configs.
+// splitk: 0 auto (LDS-DMA path), otherwise forced.
 at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& residual, int64_t act, double alpha,
-                const c10::optional<at::Tensor>& out, int64_t config) {
+                const c10::optional<at::Tensor>& out, int64_t config, int64_t splitk,
+                const c10::optional<at::Tensor>& ln_colsum, int64_t ln_mode, double ln_eps) {
   check_bf16(a_in, "A");
   check_bf16(w, "W");
   at::Tensor a = as2d(a_in);
@@ -65,8 +68,35 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   }
   if (M == 0 || N == 0) return c;
   GemmArgs g{a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0), c.data_ptr(), (int)c.stride(0),
-             bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, (int)config};
-  launch_gemm_bf16(g, cur_stream());
+             bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1};
+  const bool glds_ok = (K % 64 == 0);
+  const float* csp = nullptr;
+  if (ln_mode != 0) {
+    TORCH_CHECK(glds_ok, "fused norm-GEMM needs K % 64 == 0");
+    TORCH_CHECK(ln_colsum.has_value() && ln_colsum->scalar_type() == at::kFloat && ln_colsum->is_contiguous() &&
+                    ln_colsum->numel() == N,
+                "fused norm-GEMM needs fp32 ln_colsum [N]");
+    csp = ln_colsum->data_ptr<float>();
+    if (config >= 10) config = -1;
+  }
+  if (config >= 10 || !glds_ok) {
+    g.config = config >= 10 ? (int)(config - 10) : -1;
+    launch_gemm_bf16(g, cur_stream());
+    return c;
+  }
+  int cfg = (int)config, sk = (int)splitk;
+  if (cfg < 0 || sk <= 0) {
+    int acfg, ask;
+    gemm_glds_pick((int)M, (int)N, (int)K, &acfg, &ask);
+    if (cfg < 0) cfg = acfg;
+    if (sk <= 0) sk = ask;
+  }
+  const bool split_ok = (N % 8 == 0) && (c.stride(0) % 8 == 0) && (ldr % 8 == 0) && K % (64 * sk) == 0;
+  if (!split_ok) sk = 1;
+  at::Tensor ws;
+  if (sk > 1) ws = at::empty({(int64_t)gemm_glds_workspace_bytes((int)M, (int)N, sk) / 4}, a.options().dtype(at::kFloat));
+  if (ln_mode != 0) sk = 1;
+  launch_gemm_glds(g, cfg, sk, sk > 1 ? ws.data_ptr() : nullptr, cur_stream(), csp, (int)ln_mode, (float)ln_eps);
   return c;
 }
 
@@ -261,8 +291,15 @@ at::Tensor grouped_gemm(const at::Tensor& X, const at::Tensor& offsets, const at
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Hand-written HIP/CDNA4 (gfx950) kernels for distributed_llm_scheduler_amd";
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),
-        py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1);
+        py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1,
+        py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5);
   m.def("gemm_pick_config", &gemm_pick_config);
+  m.def("gemm_glds_num_configs", &gemm_glds_num_configs);
+  m.def("gemm_glds_pick", [](int M, int N, int K) {
+    int c, s;
+    gemm_glds_pick(M, N, K, &c, &s);
+    return std::make_pair(c, s);
+  });
   m.def("attention", &attention, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"),
         py::arg("n_head"), py::arg("n_kv_head"), py::arg("head_dim"), py::arg("causal") = true,
         py::arg("scale") = 0.125, py::arg("out") = py::none());

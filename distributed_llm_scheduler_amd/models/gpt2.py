@@ -28,6 +28,18 @@ HBM_BW = 5.0e12
 LAUNCH_S = 3e-6
 
 
+# Logits rows are stored with their stride padded to a multiple of 64 columns (50257 ->
+# 50304): 16-B aligned rows let the LM-head GEMM epilogue use vector stores. The logical
+# shape stays [B, S, V]; the executor exposes a strided view.
+LOGITS_PAD = 64
+
+
+def _padded_cols(op) -> int:
+    n = op.out_shape[-1]
+    pad = op.attrs.get("ld_pad", 1)
+    return (n + pad - 1) // pad * pad
+
+
 def gpt2_param_groups(cfg: ModelConfig) -> Dict[str, ParamGroup]:
     H, V, F = cfg.n_embd, cfg.vocab_size, cfg.ffn
     g: Dict[str, ParamGroup] = {
@@ -83,10 +95,10 @@ def build_gpt2_dag(cfg: "ModelConfig | str" = "gpt2", batch: int = 1, seq: int =
     tasks: List[Task] = []
 
     def add(name, mem_ref, t_ref, deps, params, op, flops, extra_bytes=0):
-        out_b = 1
-        for s in op.out_shape:
+        out_b = dtype_bytes
+        for s in op.out_shape[:-1]:
             out_b *= s
-        out_b *= dtype_bytes if op.kind != "lm_head" else 2
+        out_b *= _padded_cols(op)
         if ref:
             mem, comp = mem_ref, t_ref
         else:
@@ -140,7 +152,7 @@ def build_gpt2_dag(cfg: "ModelConfig | str" = "gpt2", batch: int = 1, seq: int =
         OpSpec("layernorm", [tid(last)], {"w": "ln_f.weight", "b": "ln_f.bias"}, {"eps": cfg.norm_eps}, shape),
         8.0 * M * H)
     add("output_projection", emb_mem, 0.1, ["final_ln"], ["embedding_weights"],
-        OpSpec("lm_head", [tid("final_ln")], {"w": "wte"}, {"vocab": V}, (batch, seq, V)), 2.0 * M * H * V)
+        OpSpec("lm_head", [tid("final_ln")], {"w": "wte"}, {"vocab": V, "ld_pad": LOGITS_PAD}, (batch, seq, V)), 2.0 * M * H * V)
     return tasks
 
 

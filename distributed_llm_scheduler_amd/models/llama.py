@@ -18,7 +18,7 @@ from typing import Dict, List
 
 from ..core.task import OpSpec, Task
 from .config import ModelConfig, get_config
-from .gpt2 import LAUNCH_S, _roofline
+from .gpt2 import LOGITS_PAD, _padded_cols, _roofline
 from .params import ParamGroup, TensorSpec
 
 
@@ -70,8 +70,9 @@ def build_llama_dag(cfg: "ModelConfig | str" = "llama3-8b", batch: int = 1, seq:
 
     def add(name, t_ref, deps, params, op, flops, extra=0):
         out_b = dtype_bytes
-        for s in op.out_shape:
+        for s in op.out_shape[:-1]:
             out_b *= s
+        out_b *= _padded_cols(op)
         if ref:
             mem = sum(pbytes[p] for p in params) * 2 / 1e9 + 0.01  # fp32 params + activation-ish, GPT-2 style
             comp = t_ref
@@ -131,6 +132,7 @@ def build_llama_dag(cfg: "ModelConfig | str" = "llama3-8b", batch: int = 1, seq:
     add("final_ln", 0.01, [last], ["final_norm_weights"],
         OpSpec("rmsnorm", [tid(last)], {"w": "norm.weight"}, {"eps": cfg.norm_eps}, shape), 4.0 * M * H)
     add("output_projection", 0.1, ["final_ln"], ["output_weights"],
-        OpSpec("lm_head", [tid("final_ln")], {"w": "output.weight"}, {"vocab": V}, (batch, seq, V)),
+        OpSpec("lm_head", [tid("final_ln")], {"w": "output.weight"}, {"vocab": V, "ld_pad": LOGITS_PAD},
+               (batch, seq, V)),
         2.0 * M * H * V)
     return tasks

@@ -21,6 +21,8 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from . import tuning
+
 ACT = {None: 0, "none": 0, "gelu": 1, "gelu_tanh": 1, "silu": 2, "relu": 3}
 
 _lock = threading.Lock()
@@ -143,13 +145,40 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None):
     if _gpu(x):
         a = ACT[act] if not isinstance(act, int) else act
         shp = x.shape[:-1] + (w.shape[0],)
-        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, -1)
+        cfg, sk = tuning.lookup(x.numel() // x.shape[-1], w.shape[0], w.shape[1])
+        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk)
         return y.view(shp) if out is None else out
     y = ref_linear(x, w, bias, act, residual, alpha)
     if out is not None:
         out.copy_(y)
         return out
     return y
+
+
+def derive_norm_gemm(w, ln_w, ln_b=None, bias=None):
+    """Fold a norm's affine into the following GEMM: returns (W' = W * ln_w, colsum(W') in
+    fp32, bias' = bias + W @ ln_b). W' is rounded to bf16 BEFORE the column sums, so the
+    epilogue's mean correction matches exactly what the MFMAs multiply."""
+    wf = w.float()
+    wd = (wf * ln_w.float()[None, :]).to(w.dtype)
+    cs = wd.float().sum(1).contiguous()
+    b = torch.zeros(w.shape[0], device=w.device) if bias is None else bias.float()
+    if ln_b is not None:
+        b = b + wf @ ln_b.float()
+    return wd, cs, b.to(w.dtype).contiguous()
+
+
+def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, residual=None, out=None):
+    """``act(W . norm(x) + bias) + residual`` in ONE GEMM on the raw rows ``x`` (GPU), with
+    ``(w_derived, colsum, bias_derived)`` from :func:`derive_norm_gemm`. ``mode`` is
+    "layernorm" or "rmsnorm"."""
+    m = {"layernorm": 1, "rmsnorm": 2}[mode]
+    a = ACT[act] if not isinstance(act, int) else act
+    shp = x.shape[:-1] + (w_derived.shape[0],)
+    cfg, _ = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1])
+    y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < 10 else -1, 1, colsum, m,
+                   float(eps))
+    return y.view(shp) if out is None else out
 
 
 def layernorm(x, w, b, eps=1e-5, residual=None, out=None, sum_out=None):

@@ -55,7 +55,7 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
 
 class DAGExecutor:
     def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
-                 model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234):
+                 model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True):
         self.tasks = {t.id: t for t in tasks}
         self.prog = program
         self.store = store
@@ -70,12 +70,16 @@ class DAGExecutor:
         self._views: Dict[str, torch.Tensor] = {}     # activation views (output task -> tensor)
         self._params: Dict[str, Dict[str, torch.Tensor]] = {}  # pid -> {tensor name -> view}
         self._wflat: Dict[str, torch.Tensor] = {}               # tensor name -> resident view
+        self._derived_cache: Dict[tuple, tuple] = {}             # (weight, ptr) -> (colsum, bias') for folded norms
         self._valid: List[Tuple[int, int, str]] = []  # param arena regions holding data
         self._inputs: Dict[str, torch.Tensor] = {}
         self._pending_sends: List[Tuple[int, int, object]] = []
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._setup()
+        if autotune and self.gpu:
+            from ..ops import tuning
+            tuning.ensure_tuned(self.gemm_shapes(), self.device)
 
     # ------------------------------------------------------------------ setup
     def _setup(self) -> None:
@@ -86,8 +90,13 @@ class DAGExecutor:
         for tid, off in p.act_offset.items():
             t = self.tasks[tid]
             shape = tuple(t.op.out_shape) if t.op is not None and t.op.out_shape else (p.act_bytes[tid] // 2,)
-            n = math.prod(shape)
-            self._views[tid] = self.act_slab[off:off + 2 * n].view(self.dtype).view(shape)
+            pad = t.op.attrs.get("ld_pad", 1) if t.op is not None else 1
+            cols = (shape[-1] + pad - 1) // pad * pad
+            rows = math.prod(shape[:-1])
+            v = self.act_slab[off:off + 2 * rows * cols].view(self.dtype).view(rows, cols)
+            if cols != shape[-1]:
+                v = v[:, :shape[-1]]  # padded row stride (16-B aligned rows for vector stores)
+            self._views[tid] = v.view(shape)
         # workspace for intra-group temporaries (attention qkv / o, mlp gate_up ...)
         ws = 0
         for ins in p.instrs:
@@ -106,8 +115,34 @@ class DAGExecutor:
                         vocab = self.cfg.vocab_size if self.cfg is not None else 50257
                         self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
 
+    def gemm_shapes(self):
+        """(M, N, K) of every GEMM this rank's program launches (for autotuning)."""
+        shapes = set()
+        for ins in self.prog.instrs:
+            if ins.op != "run":
+                continue
+            for t in (self.tasks[x] for x in ins.group):
+                shapes |= self._gemm_shapes_of(t)
+        return sorted(shapes)
+
+    def _gemm_shapes_of(self, t):
+        shapes = set()
+        op = t.op
+        if op is not None and op.out_shape:
+            M = math.prod(op.out_shape[:-1])
+            g = self.store.groups
+            spec = {s.name: s for pid in t.params_needed for s in g[pid].tensors}
+            names = [v for k, v in op.weights.items() if k.startswith("w") and isinstance(v, str)]
+            for n in names:
+                if n in spec and len(spec[n].shape) == 2 and op.kind not in ("embedding", "layernorm", "rmsnorm"):
+                    N, K = spec[n].shape
+                    shapes.add((M, N, K))
+        return shapes
+
     def _workspace_bytes(self, ins) -> int:
-        t = self.tasks[ins.group[0]]
+        grp = [self.tasks[x] for x in ins.group]
+        t = grp[1] if len(grp) > 1 and grp[0].op is not None and grp[0].op.kind in ("layernorm", "rmsnorm") \
+            else grp[0]
         if t.op is None:
             return 0
         k = t.op.kind
@@ -145,6 +180,8 @@ class DAGExecutor:
         if (off, total, pid) in self._valid:
             return  # region still holds this group (steady-state residency)
         self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
+        for spec, _ in layout:  # these weights are original again: drop stale folded-norm state
+            self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
         for spec, _ in layout:
             views[spec.name].copy_(self.store.tensor(spec.name), non_blocking=True)
         self._valid.append((off, total, pid))
@@ -177,8 +214,45 @@ class DAGExecutor:
             self._rope[key] = ops.rope_tables(S, D, theta, self.device)
         return self._rope[key]
 
+    # --- norm folding (GPU): derived weights, recomputed after every real fill of W ---
+    def _derived(self, norm: Task, w_name: str, b_name: Optional[str]):
+        """(W', colsum, bias') for a norm folded into the GEMM on weight ``w_name``; W is
+        overwritten IN PLACE by W' (it is read by this fused group only)."""
+        W = self._w(w_name)
+        key = (w_name, W.data_ptr())
+        d = self._derived_cache.get(key)
+        if d is None:
+            nw = self._w(norm.op.weights["w"])
+            nb = self._w(norm.op.weights["b"]) if "b" in norm.op.weights else None
+            bias = self._w(b_name) if b_name else None
+            wd, cs, bd = ops.derive_norm_gemm(W, nw, nb, bias)
+            W.copy_(wd)
+            d = (cs, bd if (bias is not None or nb is not None) else None)
+            self._derived_cache[key] = d
+        return W, d[0], d[1]
+
+    def _gemm(self, x, w_name, b_name, norm: Optional[Task], act=None, residual=None, out=None):
+        """One GEMM node, optionally with a preceding norm folded in."""
+        if norm is None:
+            return ops.linear(x, self._w(w_name), self._w(b_name) if b_name else None, act=act,
+                              residual=residual, out=out)
+        if self.gpu:
+            W, cs, bd = self._derived(norm, w_name, b_name)
+            return ops.linear_norm(x, W, cs, bd, norm.op.kind, norm.op.attrs.get("eps", 1e-5), act=act,
+                                   residual=residual, out=out)
+        nw = self._w(norm.op.weights["w"])
+        if norm.op.kind == "layernorm":
+            xn = ops.layernorm(x, nw, self._w(norm.op.weights["b"]), norm.op.attrs.get("eps", 1e-5))
+        else:
+            xn = ops.rmsnorm(x, nw, norm.op.attrs.get("eps", 1e-5))
+        return ops.linear(xn, self._w(w_name), self._w(b_name) if b_name else None, act=act, residual=residual,
+                          out=out)
+
     def _run_group(self, ins) -> None:
         grp = [self.tasks[t] for t in ins.group]
+        norm = None
+        if len(grp) > 1 and grp[0].op.kind in ("layernorm", "rmsnorm"):
+            norm, grp = grp[0], grp[1:]
         head, tail = grp[0], grp[-1]
         out = self._views[tail.id]
         k = head.op.kind
@@ -190,33 +264,33 @@ class DAGExecutor:
         act = "gelu" if any(t.op.kind == "gelu" for t in grp[1:]) else head.op.attrs.get("act")
         a = head.op.attrs
         W = head.op.weights
+        src = norm.op.inputs[0] if norm is not None else (head.op.inputs[0] if head.op.inputs else None)
         if k == "embedding":
             tok = self._x(head.op.inputs[0])
             S = head.op.out_shape[1]
             ops.embedding(tok, self._w(W["wte"]), self._w(W["wpe"]) if "wpe" in W else None, S,
                           out=self._flat(out))
         elif k == "layernorm":
-            ops.layernorm(self._flat(self._x(head.op.inputs[0])), self._w(W["w"]), self._w(W["b"]),
-                          a.get("eps", 1e-5), out=self._flat(out))
+            ops.layernorm(self._flat(self._x(src)), self._w(W["w"]), self._w(W["b"]), a.get("eps", 1e-5),
+                          out=self._flat(out))
         elif k == "rmsnorm":
-            ops.rmsnorm(self._flat(self._x(head.op.inputs[0])), self._w(W["w"]), a.get("eps", 1e-5),
-                        out=self._flat(out))
+            ops.rmsnorm(self._flat(self._x(src)), self._w(W["w"]), a.get("eps", 1e-5), out=self._flat(out))
         elif k == "residual":
             ops.add(self._x(head.op.inputs[0]), self._x(head.op.inputs[1]), out=out)
         elif k == "gelu":
-            ops.gelu(self._x(head.op.inputs[0]), out=out)
+            ops.gelu(self._x(src), out=out)
         elif k in ("linear", "lm_head"):
-            ops.linear(self._flat(self._x(head.op.inputs[0])), self._w(W["w"]),
-                       self._w(W["b"]) if "b" in W else None, act=act, residual=residual, out=self._flat(out))
+            self._gemm(self._flat(self._x(src)), W["w"], W.get("b"), norm, act=act, residual=residual,
+                       out=self._flat(out))
         elif k == "attention":
-            x = self._flat(self._x(head.op.inputs[0]))
+            x = self._flat(self._x(src))
             M = x.shape[0]
             B, S = head.op.out_shape[0], head.op.out_shape[1]
             nh, nkv, D = a["n_head"], a["n_kv_head"], a["head_dim"]
             width = (nh + 2 * nkv) * D
             qkv = self._ws(0, (M, width))
             o = self._ws(M * width, (M, nh * D))
-            ops.linear(x, self._w(W["w_qkv"]), self._w(W["b_qkv"]) if "b_qkv" in W else None, out=qkv)
+            self._gemm(x, W["w_qkv"], W.get("b_qkv"), norm, out=qkv)
             if a.get("rope"):
                 cos, sin = self._rope_tables(S, D, a.get("rope_theta", 10000.0))
                 ops.rope_(qkv, S, nh, nkv, D, nh * D, cos, sin)
@@ -225,11 +299,11 @@ class DAGExecutor:
             ops.linear(o, self._w(W["w_o"]), self._w(W["b_o"]) if "b_o" in W else None, residual=residual,
                        out=self._flat(out))
         elif k == "swiglu_mlp":
-            x = self._flat(self._x(head.op.inputs[0]))
+            x = self._flat(self._x(src))
             M, F = x.shape[0], a["ffn"]
             gu = self._ws(0, (M, 2 * F))
             h = self._ws(M * 2 * F, (M, F))
-            ops.linear(x, self._w(W["w_gate_up"]), out=gu)
+            self._gemm(x, W["w_gate_up"], None, norm, out=gu)
             ops.swiglu(gu, out=h)
             ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out))
         elif k == "moe_expert":

@@ -38,8 +38,10 @@ def test_fusion_reduces_kernels():
     plain = runtime.plan("tiny-gpt2", world=1, seq=16, fuse=False)
     n = fused.programs[0].n_kernels
     assert plain.programs[0].n_kernels == fused.total == 19
-    # per layer: ffn_expand+gelu, ffn_contract+output, attention+attn_residual fused
-    assert n == 19 - 3 * 2
+    # per layer: [ln1+attention+attn_residual], [ln2+ffn_expand+gelu], [ffn_contract+output]
+    assert n == 3 * 2 + 3
+    kinds = [i.kind for i in fused.programs[0].instrs if i.op == "run"]
+    assert kinds[:4] == ["embedding", "layernorm+attention+residual", "layernorm+linear+gelu", "linear+residual"]
 
 
 def test_memory_cap_enforced_by_scheduler():

@@ -42,13 +42,24 @@ def test_gemm_identity_asymmetric():
 
 @pytest.mark.parametrize("M,N,K", [(512, 2304, 768), (512, 768, 3072), (512, 3072, 768), (77, 130, 200),
                                    (512, 50257, 768), (1, 64, 64), (1024, 1024, 1024)])
-@pytest.mark.parametrize("config", [-1, 0, 3])
-def test_gemm_shapes(M, N, K, config):
+@pytest.mark.parametrize("config,splitk", [(-1, 0), (10, 1), (13, 1), (0, 1), (1, 1), (2, 1), (3, 1), (4, 1),
+                                           (3, 2), (3, 4), (2, 3)])
+def test_gemm_shapes(M, N, K, config, splitk):
     x = _rand(M, K, seed=1)
     w = _rand(N, K, scale=0.05, seed=2)
     ref = ops.ref_linear(x.cpu(), w.cpu()).float()
-    y = ops.ext().gemm(x, w, None, None, 0, 1.0, None, config)
+    y = ops.ext().gemm(x, w, None, None, 0, 1.0, None, config, splitk)
     torch.cuda.synchronize()
+    _close(y.cpu(), ref, 2e-2)
+
+
+@pytest.mark.parametrize("splitk", [1, 2, 4])
+def test_gemm_splitk_epilogue(splitk):
+    M, N, K = 512, 768, 3072
+    x, w = _rand(M, K, seed=30), _rand(N, K, scale=0.02, seed=31)
+    bias, res = _rand(N, scale=0.5, seed=32), _rand(M, N, seed=33)
+    y = ops.ext().gemm(x, w, bias, res, 1, 1.0, None, 3, splitk)
+    ref = ops.ref_linear(x.cpu(), w.cpu(), bias.cpu(), "gelu", res.cpu())
     _close(y.cpu(), ref, 2e-2)
 
 
@@ -149,3 +160,22 @@ def test_moe_pipeline():
     _close(y.cpu(), yr, 2e-2)
     eo = _rand(M * k, H, seed=24)
     _close(ops.moe_combine(eo, slot, w).cpu(), ops.moe_combine(eo.cpu(), slot.cpu(), w.cpu()), 1e-2)
+
+
+@pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
+@pytest.mark.parametrize("M,N,K,cfg", [(512, 2304, 768, -1), (300, 1024, 4096, 0), (512, 3072, 768, 2)])
+def test_gemm_with_folded_norm(mode, M, N, K, cfg):
+    x = _rand(M, K, scale=2.0, seed=40) + 0.5  # non-zero mean rows exercise the mean correction
+    w = _rand(N, K, scale=0.03, seed=41)
+    nw = (1 + 0.2 * _rand(K, seed=42).float()).to(torch.bfloat16)
+    nb = _rand(K, scale=0.1, seed=43) if mode == "layernorm" else None
+    bias = _rand(N, scale=0.1, seed=44)
+    res = _rand(M, N, seed=45)
+    if mode == "layernorm":
+        xn = ops.ref_layernorm(x.cpu(), nw.cpu(), nb.cpu())
+    else:
+        xn = ops.ref_rmsnorm(x.cpu(), nw.cpu())
+    ref = ops.ref_linear(xn, w.cpu(), bias.cpu(), "gelu", res.cpu())
+    wd, cs, bd = ops.derive_norm_gemm(w, nw, nb, bias)
+    y = ops.linear_norm(x, wd, cs, bd, mode, act="gelu", residual=res)
+    _close(y.cpu(), ref, 3e-2)
