@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import hashlib
 from dataclasses import dataclass, field
-from typing import Dict, List, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -25,8 +25,10 @@ import torch
 class TensorSpec:
     name: str
     shape: Tuple[int, ...]
-    init: str = "normal"  # normal | ones | zeros | small
+    init: str = "normal"  # normal | ln | bias | ones | zeros
     std: float = 0.02
+    parent: Optional["TensorSpec"] = None  # shard of a larger tensor (tensor parallelism)
+    slc: Optional[tuple] = None            # (dim, start, stop) or ("rows", ((a, b), ...))
 
     @property
     def numel(self) -> int:
@@ -49,8 +51,18 @@ def _seed(name: str, base: int) -> int:
     return (int(hashlib.sha1(name.encode()).hexdigest()[:12], 16) + base) % (2 ** 62)
 
 
+def _take(full: torch.Tensor, slc) -> torch.Tensor:
+    if slc[0] == "rows":
+        return torch.cat([full[a:b] for a, b in slc[1]], 0).contiguous()
+    dim, a, b = slc
+    return full.narrow(dim, a, b - a).contiguous()
+
+
 def materialize(spec: TensorSpec, dtype=torch.bfloat16, device="cpu", seed: int = 0) -> torch.Tensor:
-    """Deterministic random-init tensor for ``spec`` (fp32 generation, cast once)."""
+    """Deterministic random-init tensor for ``spec`` (fp32 generation, cast once). A shard
+    is the matching slice of its parent, so sharded and unsharded models are identical."""
+    if spec.parent is not None:
+        return _take(materialize(spec.parent, dtype, device, seed), spec.slc)
     if spec.init == "ones":
         return torch.ones(spec.shape, dtype=dtype, device=device)
     if spec.init == "zeros":
@@ -75,13 +87,21 @@ class ParamStore:
         self.seed = seed
         self.pin = torch.cuda.is_available() if pin is None else pin
         self._host: Dict[str, torch.Tensor] = {}
-        self._specs: Dict[str, TensorSpec] = {s.name: s for g in groups.values() for s in g.tensors}
+        self._specs: Dict[str, TensorSpec] = {}
+        for g in groups.values():
+            for sp in g.tensors:
+                while sp is not None:  # shards and the full tensors they slice
+                    self._specs.setdefault(sp.name, sp)
+                    sp = sp.parent
 
     def tensor(self, name: str) -> torch.Tensor:
         t = self._host.get(name)
         if t is None:
             spec = self._spec(name)
-            t = materialize(spec, self.dtype, "cpu", self.seed)
+            if spec.parent is not None:
+                t = _take(self.tensor(spec.parent.name), spec.slc)
+            else:
+                t = materialize(spec, self.dtype, "cpu", self.seed)
             if self.pin:
                 t = t.pin_memory()
             self._host[name] = t

@@ -29,11 +29,16 @@ def build_dag(cfg: ModelConfig, batch: int = 1, seq: int = 512, cost_model: str 
     raise KeyError(cfg.family)
 
 
-def build(model: str, batch: int = 1, seq: int = 512, replicas: int = 1,
-          cost_model: str = "bytes") -> Tuple[List[Task], Dict[str, ParamGroup], ModelConfig]:
-    """``replicas`` independent requests (task ids prefixed ``r{k}/``) sharing weights."""
+def build(model: str, batch: int = 1, seq: int = 512, replicas: int = 1, cost_model: str = "bytes",
+          tp: int = 1) -> Tuple[List[Task], Dict[str, ParamGroup], ModelConfig]:
+    """``replicas`` independent requests (task ids prefixed ``r{k}/``) sharing weights;
+    ``tp > 1`` splits every layer into tensor-parallel shards (models/transforms.py)."""
     cfg = get_config(model)
     tasks: List[Task] = []
     for r in range(replicas):
         tasks.extend(build_dag(cfg, batch, seq, cost_model, prefix=f"r{r}/" if replicas > 1 else ""))
-    return tasks, param_groups(cfg), cfg
+    groups = param_groups(cfg)
+    if tp > 1:
+        from .transforms import tensor_parallel
+        tasks, groups = tensor_parallel(tasks, groups, cfg, tp)
+    return tasks, groups, cfg

@@ -311,9 +311,11 @@ class DAGExecutor:
             logits = self._flat(self._x(head.op.inputs[1]))
             ops.moe_expert(h, logits, self._w(W["w_gate_up"]), self._w(W["w_down"]), a["expert"], a["n_experts"],
                            a["top_k"], out=self._flat(out))
-        elif k == "moe_combine":
-            acc = self._x(head.op.inputs[-1])
-            for name in head.op.inputs[:-1]:
+        elif k in ("moe_combine", "sum"):
+            # sum of partial outputs (expert contributions + residual, or TP shard partials)
+            ins_ = head.op.inputs
+            acc = self._x(ins_[-1])
+            for name in ins_[:-1]:
                 ops.add(self._x(name), acc, out=out)
                 acc = out
         else:

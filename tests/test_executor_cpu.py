@@ -154,3 +154,49 @@ def test_mixtral_expert_parallel_two_ranks():
     assert sum(r["sends"] for r in res) > 0
     errs = [e for r in res for e in r["errs"]]
     assert len(errs) == 1 and errs[0][0] < 0.03 * errs[0][1]
+
+
+@pytest.mark.parametrize("model", ["tiny-gpt2", "tiny-llama"])
+def test_tensor_parallel_transform_single_rank(model):
+    p = runtime.plan(model, world=1, seq=32, batch=1, tp=2)
+    ids = [t.id for t in p.tasks]
+    assert any(i.endswith(".tp1") for i in ids) and any(i.endswith(".sum") for i in ids)
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, "cpu", store)
+    ex.step()
+    err, scale = _ref_check(p, ex, store)
+    assert err < 0.03 * scale
+
+
+def _tp_worker(rank, world, port, model, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = runtime.plan(model, world=world, seq=32, batch=1, tp=world, placement="tensor")
+        store = runtime.make_store(p)
+        ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
+        st = ex.step()
+        res = {"rank": rank, "sends": st.sends, "recvs": st.recvs, "errs": [],
+               "shards": sum(1 for t, r in p.placement.items() if r == rank and ".tp" in t)}
+        if p.placement.get("output_projection") == rank:
+            res["errs"].append(_ref_check(p, ex, store))
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model", ["tiny-gpt2", "tiny-llama"])
+def test_tensor_parallel_two_ranks(model):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, model, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs)
+    res = sorted([q.get(timeout=5) for _ in range(2)], key=lambda r: r["rank"])
+    assert res[1]["shards"] > 0 and res[1]["sends"] > 0 and res[1]["recvs"] > 0
+    errs = [e for r in res for e in r["errs"]]
+    assert len(errs) == 1 and errs[0][0] < 0.03 * errs[0][1]
