@@ -47,9 +47,16 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--cap-gb", type=float, default=288.0, help="per-GPU HBM budget for parameters")
+    ap.add_argument("--placement", default="scheduler", choices=["scheduler", "replica", "pipeline", "tensor"])
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel shards per layer (DAG transform)")
+    ap.add_argument("--init", default="auto", choices=["auto", "host", "device"],
+                    help="weight init: device RNG straight into HBM, or host master copy (auto: device "
+                         "unless the program re-loads evicted groups, whose cost must be a real copy)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-fuse", action="store_true")
     ap.add_argument("--profile", action="store_true", help="also print a measured per-kernel timeline")
+    ap.add_argument("--trace-out", default=None, help="write a measured Chrome trace (all ranks) to this path")
+    ap.add_argument("--roctx", action="store_true", help="roctx range per DAG instruction (rocprofv3 --marker-trace)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -70,10 +77,16 @@ def main():
     replicas = world * args.replicas_per_gpu
     t0 = time.time()
     plan = runtime.plan(args.model, world=world, scheduler=args.scheduler, cap_gb=args.cap_gb, replicas=replicas,
-                        batch=args.batch, seq=args.seq, cost_model="bytes", fuse=not args.no_fuse)
+                        batch=args.batch, seq=args.seq, cost_model="bytes", fuse=not args.no_fuse,
+                        placement=args.placement, tp=args.tp)
     log(f"[bench] rank {rank}: planned {plan.stats['tasks_completed']}/{plan.stats['tasks_total']} tasks in "
         f"{(time.time() - t0) * 1e3:.1f} ms; {plan.stats}")
-    ex = runtime.make_executor(plan, rank, device, pg=pg, use_graph=not args.no_graph)
+    loads = [i.param for i in plan.programs[rank].instrs if i.op == "load"]
+    dev_init = args.init == "device" or (args.init == "auto" and gpu and len(loads) == len(set(loads)))
+    store = runtime.make_store(plan, device_init=dev_init)
+    t0 = time.time()
+    ex = runtime.make_executor(plan, rank, device, store, pg=pg, use_graph=not args.no_graph, trace=args.roctx)
+    log(f"[bench] rank {rank}: executor ready in {(time.time() - t0):.1f} s (device_init={dev_init})")
 
     def sync():
         if gpu:
@@ -103,9 +116,21 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     timeline = None
-    if args.profile:
+    if args.profile or args.trace_out:
         st = ex.step(profile=True)
         timeline = [(tid, round(a, 4), round(b, 4)) for tid, a, b in st.timeline]
+        if args.trace_out:
+            from distributed_llm_scheduler_amd.utils.tracing import chrome_trace
+            evs = [None] * world
+            if world > 1:
+                dist.all_gather_object(evs, st.events)
+            else:
+                evs = [st.events]
+            if rank == 0:
+                chrome_trace(dict(enumerate(evs)), args.trace_out,
+                             meta={"model": args.model, "scheduler": plan.scheduler_name, "world": world})
+        if not args.profile:
+            timeline = None
 
     if rank == 0:
         tokens = replicas * args.batch * args.seq
@@ -123,7 +148,8 @@ def main():
             "dtype": "bf16",
             "data": "synthetic",
             "config": {"model": {"gpt2": "gpt2-small"}.get(args.model, args.model), "global_batch": replicas * args.batch, "seq_len": args.seq,
-                       "parallelism": f"dag-placement x{world} ({plan.scheduler_name}, {replicas} request DAGs)"},
+                       "parallelism": f"dag-placement x{world} ({plan.scheduler_name if args.placement == 'scheduler' else args.placement}"
+                                      f"{f', tp{args.tp}' if args.tp > 1 else ''}, {replicas} request DAGs)"},
             "tasks_completed": plan.stats["tasks_completed"],
             "tasks_total": plan.stats["tasks_total"],
             "mem_cap_gb_per_gpu": args.cap_gb,

@@ -62,6 +62,12 @@ PRESETS: Dict[str, ModelConfig] = {
                               tie_embeddings=False),
     "tiny-mixtral": ModelConfig("tiny-mixtral", "mixtral", 2, 64, 4, 256, n_positions=128, ffn_dim=96, n_kv_head=2,
                                 n_experts=4, top_k=2, tie_embeddings=False),
+    # smallest shapes the GPU kernels take (head_dim 64, 128-multiple GEMM dims): GPU tests
+    "mini-gpt2": ModelConfig("mini-gpt2", "gpt2", 2, 256, 4, 1024, n_positions=256),
+    "mini-llama": ModelConfig("mini-llama", "llama", 2, 256, 4, 1024, n_positions=256, ffn_dim=512, n_kv_head=2,
+                              tie_embeddings=False),
+    "mini-mixtral": ModelConfig("mini-mixtral", "mixtral", 2, 256, 4, 1024, n_positions=256, ffn_dim=256,
+                                n_kv_head=2, n_experts=4, top_k=2, tie_embeddings=False),
 }
 PRESETS["gpt2-small"] = PRESETS["gpt2"].with_(name="gpt2-small")
 PRESETS["llama-3-8b"] = PRESETS["llama3-8b"]

@@ -77,15 +77,44 @@ def materialize(spec: TensorSpec, dtype=torch.bfloat16, device="cpu", seed: int 
     return t.to(dtype=dtype, device=device)
 
 
+def fill_on_device(spec: TensorSpec, out: torch.Tensor, seed: int = 0) -> None:
+    """Random-init ``out`` (already in HBM) for ``spec`` with the device RNG: no host
+    master copy, no PCIe traffic — how the large-model benchmarks (Llama-3-8B 16 GB,
+    Mixtral-8x7B 93 GB) get their weights. Deterministic per name, but a different
+    stream from :func:`materialize` (so not comparable to the CPU reference)."""
+    if spec.parent is not None:
+        full = torch.empty(spec.parent.shape, dtype=out.dtype, device=out.device)
+        fill_on_device(spec.parent, full, seed)
+        out.copy_(_take(full, spec.slc))
+        return
+    if spec.init == "ones":
+        out.fill_(1.0)
+        return
+    if spec.init == "zeros":
+        out.zero_()
+        return
+    g = torch.Generator(device=out.device).manual_seed(_seed(spec.name, seed))
+    if spec.init == "ln":
+        out.normal_(1.0, 0.1, generator=g)
+    elif spec.init == "bias":
+        out.normal_(0.0, 0.02, generator=g)
+    else:
+        out.normal_(0.0, spec.std, generator=g)
+
+
 class ParamStore:
     """Host-side master copy of every parameter group (pinned when a GPU is present),
-    materialised lazily; the executor copies groups into its HBM arena on demand."""
+    materialised lazily; the executor copies groups into its HBM arena on demand.
+    ``device_init=True`` skips the host copy: groups are random-initialised directly in
+    the arena (benchmarks of models whose host materialisation would dominate setup)."""
 
-    def __init__(self, groups: Dict[str, ParamGroup], dtype=torch.bfloat16, seed: int = 0, pin: bool = None):
+    def __init__(self, groups: Dict[str, ParamGroup], dtype=torch.bfloat16, seed: int = 0, pin: bool = None,
+                 device_init: bool = False):
         self.groups = groups
         self.dtype = dtype
         self.seed = seed
-        self.pin = torch.cuda.is_available() if pin is None else pin
+        self.device_init = device_init
+        self.pin = (torch.cuda.is_available() and not device_init) if pin is None else pin
         self._host: Dict[str, torch.Tensor] = {}
         self._specs: Dict[str, TensorSpec] = {}
         for g in groups.values():
@@ -109,6 +138,13 @@ class ParamStore:
 
     def _spec(self, name: str) -> TensorSpec:
         return self._specs[name]
+
+    def fill(self, name: str, out: torch.Tensor) -> None:
+        """Write tensor ``name`` into ``out`` (an HBM arena view)."""
+        if self.device_init and out.is_cuda and name not in self._host:
+            fill_on_device(self._spec(name), out, self.seed)
+        else:
+            out.copy_(self.tensor(name), non_blocking=True)
 
     def group_tensors(self, pid: str) -> List[Tuple[TensorSpec, torch.Tensor]]:
         return [(s, self.tensor(s.name)) for s in self.groups[pid].tensors]

@@ -69,8 +69,10 @@ def _rms(x, w, eps):
 
 
 @torch.no_grad()
-def llama_forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor) -> torch.Tensor:
-    """Llama-3 / Mixtral forward (fp32): tokens [B, S] -> logits [B, S, V]."""
+def llama_forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor, router_margins: list = None) -> torch.Tensor:
+    """Llama-3 / Mixtral forward (fp32): tokens [B, S] -> logits [B, S, V]. ``router_margins``
+    (if a list) receives, per MoE layer, the [B, S] gap between the k-th and (k+1)-th router
+    logit: tokens with a tiny gap may legitimately route differently under bf16 logits."""
     B, S = tokens.shape
     nh, nkv, D = cfg.n_head, cfg.kv_heads, cfg.head_dim
     x = _w(store, "tok_embeddings")[tokens.long()]
@@ -85,6 +87,9 @@ def llama_forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor) -> 
         if cfg.n_experts:
             logits = h @ _w(store, p + "moe.gate").t()
             val, idx = torch.topk(logits, cfg.top_k, -1)
+            if router_margins is not None:
+                srt = torch.sort(logits, -1, descending=True).values
+                router_margins.append(srt[..., cfg.top_k - 1] - srt[..., cfg.top_k])
             gate = torch.softmax(val, -1)
             out = torch.zeros_like(h)
             for e in range(cfg.n_experts):
@@ -101,5 +106,7 @@ def llama_forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor) -> 
     return x @ _w(store, "output.weight").t()
 
 
-def forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor) -> torch.Tensor:
-    return gpt2_forward(cfg, store, tokens) if cfg.family == "gpt2" else llama_forward(cfg, store, tokens)
+def forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor, router_margins: list = None) -> torch.Tensor:
+    if cfg.family == "gpt2":
+        return gpt2_forward(cfg, store, tokens)
+    return llama_forward(cfg, store, tokens, router_margins)

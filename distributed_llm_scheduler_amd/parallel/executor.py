@@ -21,6 +21,7 @@ per-GPU Gantt (same layout as the reference's simulated one, visu.py:206-248).
 from __future__ import annotations
 
 import math
+import time
 import zlib
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -31,6 +32,7 @@ import torch.distributed as dist
 from .. import ops
 from ..core.task import Task
 from ..models.params import ParamStore, group_layout
+from ..utils.tracing import Roctx
 from .program import Program
 
 
@@ -44,6 +46,7 @@ class StepStats:
     param_fills: int = 0
     bytes_filled: int = 0
     timeline: List[Tuple[str, float, float]] = field(default_factory=list)  # (group, start_ms, end_ms)
+    events: List[Tuple[str, str, float, float]] = field(default_factory=list)  # (name, category, start, end)
 
 
 def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.Tensor:
@@ -55,7 +58,8 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
 
 class DAGExecutor:
     def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
-                 model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True):
+                 model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True,
+                 trace: bool = False):
         self.tasks = {t.id: t for t in tasks}
         self.prog = program
         self.store = store
@@ -65,6 +69,7 @@ class DAGExecutor:
         self.pg = pg
         self.use_graph = use_graph and self.gpu and not program.has_comm
         self.seed = seed
+        self.trace = trace  # roctx range per instruction (eager steps; a graph replay is one range)
         self.dtype = torch.bfloat16
         self._graph = None
         self._views: Dict[str, torch.Tensor] = {}     # activation views (output task -> tensor)
@@ -183,7 +188,7 @@ class DAGExecutor:
         for spec, _ in layout:  # these weights are original again: drop stale folded-norm state
             self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
         for spec, _ in layout:
-            views[spec.name].copy_(self.store.tensor(spec.name), non_blocking=True)
+            self.store.fill(spec.name, views[spec.name])
         self._valid.append((off, total, pid))
         stats.param_fills += 1
         stats.bytes_filled += total
@@ -322,31 +327,53 @@ class DAGExecutor:
             raise NotImplementedError(f"op kind {k!r}")
 
     # ------------------------------------------------------------------- step
-    def _step_body(self, stats: StepStats, timeline: Optional[list] = None) -> None:
+    def _mark(self):
+        """A timestamp token: a recorded hipEvent on GPU, host time on the CPU backend."""
+        if self.gpu:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def _step_body(self, stats: StepStats, events: Optional[list] = None) -> None:
+        """Issue the program. ``events`` (profiling) collects (name, category, t0, t1) tokens."""
         pg = self.pg
+        tr = self.trace
         self._pending_sends = []
-        recv_work: Dict[str, object] = {}
+        recv_work: Dict[str, Tuple[object, object]] = {}
         for i, ins in enumerate(self.prog.instrs):
+            if tr:
+                Roctx.push(f"{ins.op}:{ins.task or ins.param}")
             if ins.op == "load":
+                t0 = self._mark() if events is not None else None
+                fills = stats.param_fills
                 self._load(i, ins.param, stats)
+                if events is not None and stats.param_fills != fills:
+                    events.append((ins.param, "load", t0, self._mark()))
             elif ins.op == "evict":
                 self._evict(ins.param)
             elif ins.op == "recv":
-                recv_work[ins.task] = dist.irecv(self._views[ins.task], src=ins.peer, group=pg)
+                t0 = self._mark() if events is not None else None
+                recv_work[ins.task] = (dist.irecv(self._views[ins.task], src=ins.peer, group=pg), t0)
                 stats.recvs += 1
             elif ins.op == "send":
                 buf = self._views[ins.task]
+                t0 = self._mark() if events is not None else None
                 w = dist.isend(buf, dst=ins.peer, group=pg)
                 off = self.prog.act_offset[ins.task]
                 self._pending_sends.append((off, self.prog.act_bytes[ins.task], w))
+                if events is not None:
+                    events.append((f"{ins.task}->gpu{ins.peer}", "send", t0, self._mark()))
                 stats.sends += 1
                 stats.bytes_sent += buf.numel() * buf.element_size()
             elif ins.op == "run":
                 for tid in ins.group:
                     for d in self.tasks[tid].dependencies:
-                        w = recv_work.pop(d, None)
-                        if w is not None:
-                            w.wait()
+                        rw = recv_work.pop(d, None)
+                        if rw is not None:
+                            rw[0].wait()
+                            if events is not None:
+                                events.append((d, "recv", rw[1], self._mark()))
                 off, nb = self.prog.act_offset[ins.task], self.prog.act_bytes[ins.task]
                 if self._pending_sends:
                     keep = []
@@ -356,34 +383,46 @@ class DAGExecutor:
                         else:
                             keep.append((so, sb, w))
                     self._pending_sends = keep
-                if timeline is not None:
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
+                if events is not None:
+                    t0 = self._mark()
                     self._run_group(ins)
-                    e1.record()
-                    timeline.append((ins.task, e0, e1))
+                    events.append((ins.task, "kernel", t0, self._mark()))
                 else:
                     self._run_group(ins)
                 stats.kernels += 1
-        for w in recv_work.values():
+            if tr:
+                Roctx.pop()
+        for w, _ in recv_work.values():
             w.wait()
         for _, _, w in self._pending_sends:
             w.wait()
         self._pending_sends = []
 
     def step(self, profile: bool = False) -> StepStats:
-        """Execute the rank's program once (asynchronously on the GPU)."""
+        """Execute the rank's program once (asynchronously on the GPU). ``profile=True`` runs
+        it eagerly with a timestamp pair around every instruction and fills
+        ``stats.timeline`` (kernel groups) and ``stats.events`` (kernels, parameter fills,
+        p2p sends/recvs), in ms from the step start."""
         stats = StepStats()
         if self._graph is not None and not profile:
+            if self.trace:
+                Roctx.push(f"graph_step:rank{self.prog.rank}")
             self._graph.replay()
+            if self.trace:
+                Roctx.pop()
             stats.kernels = self.prog.n_kernels
         else:
-            tl = [] if (profile and self.gpu) else None
-            self._step_body(stats, tl)
-            if tl is not None:
-                torch.cuda.synchronize(self.device)
-                t0 = tl[0][1] if tl else None
-                stats.timeline = [(tid, t0.elapsed_time(a), t0.elapsed_time(b)) for tid, a, b in tl]
+            ev = [] if profile else None
+            t_begin = self._mark() if profile else None
+            self._step_body(stats, ev)
+            if ev is not None:
+                if self.gpu:
+                    torch.cuda.synchronize(self.device)
+                    el = lambda a: t_begin.elapsed_time(a)  # noqa: E731
+                else:
+                    el = lambda a: (a - t_begin) * 1e3  # noqa: E731
+                stats.events = [(n, c, el(a), el(b)) for n, c, a, b in ev]
+                stats.timeline = [(n, a, b) for n, c, a, b in stats.events if c == "kernel"]
         self.last = stats
         return stats
 

@@ -146,12 +146,13 @@ def plan_stats(p: Plan) -> Dict:
     }
 
 
-def make_store(p: Plan, seed: int = 0) -> ParamStore:
-    return ParamStore(p.groups, seed=seed)
+def make_store(p: Plan, seed: int = 0, device_init: bool = False) -> ParamStore:
+    return ParamStore(p.groups, seed=seed, device_init=device_init)
 
 
-def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None, pg=None, use_graph: bool = True):
+def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None, pg=None, use_graph: bool = True,
+                  trace: bool = False):
     from .executor import DAGExecutor
 
     return DAGExecutor(p.tasks, p.programs[rank], store or make_store(p), device, model_cfg=p.cfg,
-                       use_graph=use_graph, pg=pg)
+                       use_graph=use_graph, pg=pg, trace=trace)
