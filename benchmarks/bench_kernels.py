@@ -54,7 +54,7 @@ def bench_gemm(quick):
         row["auto"] = list(ext.gemm_glds_pick(M, N, K))
         row["auto_us"] = round(t_auto, 2)
         row["auto_tflops"] = round(flops / t_auto / 1e6, 1)
-        t_old = timeit(lambda: ext.gemm(x, w, None, None, 0, 1.0, out, 10 + ext.gemm_pick_config(M, N, K), 1))
+        t_old = timeit(lambda: ext.gemm(x, w, None, None, 0, 1.0, out, ext.REGSTAGE + ext.gemm_pick_config(M, N, K), 1))
         row["regstage_us"] = round(t_old, 2)
         best = None
         for cfg in range(ext.gemm_glds_num_configs()):

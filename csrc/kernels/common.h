@@ -70,7 +70,9 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-enum DlsAct : int { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_SILU = 2, ACT_RELU = 3 };
+// ACT_SWIGLU: GEMM epilogue silu(gate) * up over a weight whose rows interleave gate and up
+// in blocks of 16 (W' rows 32c..32c+15 = gate 16c.., 32c+16..32c+31 = up 16c..); output N/2 wide
+enum DlsAct : int { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_SILU = 2, ACT_RELU = 3, ACT_SWIGLU = 4 };
 
 __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {

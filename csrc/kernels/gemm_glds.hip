@@ -39,9 +39,9 @@ __device__ __forceinline__ void wait_tiles(int ahead) {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_>
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_;
   static constexpr int BK = 64, CH = 8;
   static constexpr int NW = WM * WN, T = 64 * NW;
   static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
                                                          float* __restrict__ part, int M, int N, int K, int act,
                                                          float alpha, int tiles_m, int tiles_n, int splitk,
                                                          int kslice, const float* __restrict__ ln_colsum,
-                                                         int ln_mode, float ln_eps) {
+                                                         int ln_mode, float ln_eps, const int* __restrict__ rows) {
   __shared__ bf16x8 smem[C::STAGES * C::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WN, wn = wave % C::WN;
@@ -70,6 +70,16 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   const int ks = bid / ntile, tile = bid % ntile;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
+  const int Mmax = M;
+  if (rows != nullptr) {  // device-side row range (MoE expert): M is only the grid's bound
+    const int r0 = rows[0];
+    M = rows[1] - r0;
+    A += (size_t)r0 * lda;
+    Cp += (size_t)r0 * ldc;
+    if (R) R += (size_t)r0 * ldr;
+    if (part) part += (size_t)r0 * N;
+  }
+  if (m0 >= M) return;  // whole block idle (uniform: before any barrier)
   const int kbeg = ks * kslice;
   const int nk = kslice / C::BK;
 
@@ -147,10 +157,12 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
       }
       // swapped operands: acc = (W A^T) tile, i.e. C^T — lane holds 4 consecutive output
       // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[j], af[i], acc[i][j]);
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
 
@@ -199,7 +211,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   // columns straddle N falls back to scalars.
   const bool vec_ok = (ldc % 4 == 0) && (!R || ldr % 4 == 0);
   if (splitk > 1) {
-    float* P = part + (size_t)ks * M * N;
+    float* P = part + (size_t)ks * Mmax * N;
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
       const int row = m0 + wm * C::WTM + i * 16 + r16;
@@ -213,6 +225,55 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (col + e < N) P[(size_t)row * N + col + e] = acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
+  if (act == ACT_SWIGLU) {
+    // fragment pairs (2jj, 2jj+1) hold gate and up for the same 16 output columns
+    const int NO = N / 2;
+#pragma unroll
+    for (int jj = 0; jj < C::FN / 2; ++jj) {
+      const int gcol = n0 + wn * C::WTN + jj * 32 + g4;  // gate column in W' space
+      const int ocol = (n0 + wn * C::WTN) / 2 + jj * 16 + g4;
+      if (ocol >= NO) continue;
+      float bg[4] = {0.f, 0.f, 0.f, 0.f}, bu[4] = {0.f, 0.f, 0.f, 0.f};
+      float cg[4] = {0.f, 0.f, 0.f, 0.f}, cu[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (bias) {
+          bg[e] = bf2f(bias[gcol + e]);
+          bu[e] = bf2f(bias[gcol + 16 + e]);
+        }
+        if (ln_mode != 0) {
+          cg[e] = ln_colsum[gcol + e];
+          cu[e] = ln_colsum[gcol + 16 + e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int row = m0 + wm * C::WTM + i * 16 + r16;
+        if (row >= M) continue;
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float g = acc[i][2 * jj][e], u = acc[i][2 * jj + 1][e];
+          if (ln_mode != 0) {
+            g = ln_rs[i] * (g - ln_mu[i] * cg[e]);
+            u = ln_rs[i] * (u - ln_mu[i] * cu[e]);
+          } else {
+            g *= alpha;
+            u *= alpha;
+          }
+          o[e] = f2bf(silu(g + bg[e]) * (u + bu[e]));
+        }
+        if (vec_ok && ocol + 3 < NO) {
+          *reinterpret_cast<bf16x4*>(Cp + (size_t)row * ldc + ocol) = o;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (ocol + e < NO) Cp[(size_t)row * ldc + ocol + e] = o[e];
         }
       }
     }
@@ -273,36 +334,63 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   }
 }
 
-// out = act(alpha * sum_s P[s] + bias) + R, 8 columns per lane (N % 8 == 0 path) or scalar
+// out = act(alpha * sum_s P[s] + bias) + R, 8 columns per lane (N % 8 == 0). ACT_SWIGLU: P is in
+// the interleaved W' space (N wide), out is N/2 wide: out col c <- gate 32(c/16) + c%16, up +16.
+// rows (optional device int32[2]) restricts to a row range as in the GEMM.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ P, int splitk, int M, int N,
                                                             bf16* __restrict__ C, int ldc,
                                                             const bf16* __restrict__ bias,
                                                             const bf16* __restrict__ R, int ldr, int act,
-                                                            float alpha) {
-  const int nv = N / 8;
-  const int64_t total = (int64_t)M * nv;
+                                                            float alpha, const int* __restrict__ rows) {
   const size_t slab = (size_t)M * N;
+  int r0 = 0, nrows = M;
+  if (rows != nullptr) {
+    r0 = rows[0];
+    nrows = rows[1] - r0;
+  }
+  const bool sw = act == ACT_SWIGLU;
+  const int NO = sw ? N / 2 : N;
+  const int nv = NO / 8;
+  const int64_t total = (int64_t)nrows * nv;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int m = (int)(i / nv), c = (int)(i % nv) * 8;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int m = r0 + (int)(i / nv), c = (int)(i % nv) * 8;
+    const int pc = sw ? 32 * (c / 16) + (c % 16) : c;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0}, u[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int s = 0; s < splitk; ++s) {
-      const f32x4* p = reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c);
+      const f32x4* p = reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + pc);
       const f32x4 a = p[0], b = p[1];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         v[e] += a[e];
         v[4 + e] += b[e];
       }
-    }
-    bf16x8 bv = {}, rv = {};
-    if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
-    if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
-    bf16x8 o;
+      if (sw) {
+        const f32x4 a2 = p[4], b2 = p[5];  // +16 floats: the up half
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float x = apply_act(alpha * v[e] + (bias ? bf2f(bv[e]) : 0.f), act);
-      if (R) x += bf2f(rv[e]);
-      o[e] = f2bf(x);
+        for (int e = 0; e < 4; ++e) {
+          u[e] += a2[e];
+          u[4 + e] += b2[e];
+        }
+      }
+    }
+    bf16x8 o;
+    if (sw) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = alpha * v[e] + (bias ? bf2f(bias[pc + e]) : 0.f);
+        const float up = alpha * u[e] + (bias ? bf2f(bias[pc + 16 + e]) : 0.f);
+        o[e] = f2bf(silu(g) * up);
+      }
+    } else {
+      bf16x8 bv = {}, rv = {};
+      if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
+      if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = apply_act(alpha * v[e] + (bias ? bf2f(bv[e]) : 0.f), act);
+        if (R) x += bf2f(rv[e]);
+        o[e] = f2bf(x);
+      }
     }
     *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + c) = o;
   }
@@ -310,19 +398,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 template <class C>
 void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
-            float ln_eps) {
+            float ln_eps, const int* rows) {
   static_assert(2 * C::BM * sizeof(float) <= C::STAGES * C::STAGE * 16, "LN stats must fit the staging LDS");
   const int tiles_m = (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;
   dim3 grid(tiles_m * tiles_n * splitk), block(C::T);
   hipLaunchKernelGGL((gemm_glds_kernel<C>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, a.ldw,
                      (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act,
-                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps);
+                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows);
   if (splitk > 1) {
     const int64_t nvec = (int64_t)a.M * (a.N / 8);
     const int g = (int)std::min<int64_t>(2048, (nvec + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, ws, splitk, a.M, a.N, (bf16*)a.C, a.ldc,
-                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha);
+                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows);
   }
 }
 
@@ -334,12 +422,17 @@ using C4 = Cfg<64, 128, 2, 2, 4>;
 using C5 = Cfg<64, 64, 2, 2, 8>;    // deep pipeline: 7 K-tiles in flight (cold-weight latency)
 using C6 = Cfg<128, 64, 2, 2, 6>;   // 5 in flight, 2x rows per block
 using C7 = Cfg<128, 128, 2, 2, 4>;
+using C8 = Cfg<256, 256, 2, 4, 2>;     // 8 waves, 128x64 per wave, 2 x 64 KiB stages: big square-ish GEMMs
+using C9 = Cfg<256, 256, 2, 4, 2, 1>;  // same with s_setprio(1) around the MFMA cluster (T5)
+using C10 = Cfg<256, 128, 4, 2, 3, 1>; // C0 with s_setprio
+using C11 = Cfg<128, 128, 2, 2, 4, 1>; // C7 with s_setprio
 
 struct Shape {
   int bm, bn;
 };
-constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64}, {64, 64}, {64, 128}, {64, 64}, {128, 64}, {128, 128}};
-constexpr int kNumCfg = 8;
+constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64}, {64, 64},  {64, 128}, {64, 64},
+                             {128, 64},  {128, 128}, {256, 256}, {256, 256}, {256, 128}, {128, 128}};
+constexpr int kNumCfg = 12;
 
 }  // namespace
 
@@ -349,7 +442,7 @@ int gemm_glds_num_configs() { return kNumCfg; }
 // block) reaches ~256 blocks; split-K only when the output grid alone is too small.
 void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk) {
   const int order[] = {0, 1, 2, 4, 3};
-  for (int oi = 0; oi < kNumCfg; ++oi) {
+  for (int oi = 0; oi < 5; ++oi) {
     const int c = order[oi];
     const long tiles = (long)((M + kShapes[c].bm - 1) / kShapes[c].bm) * ((N + kShapes[c].bn - 1) / kShapes[c].bn);
     if (tiles >= 240) {
@@ -373,17 +466,23 @@ void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk) {
 size_t gemm_glds_workspace_bytes(int M, int N, int splitk) { return splitk > 1 ? (size_t)splitk * M * N * 4 : 0; }
 
 void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s, const float* ln_colsum,
-                      int ln_mode, float ln_eps) {
+                      int ln_mode, float ln_eps, const int* rows) {
   float* ws = static_cast<float*>(workspace);
   if (ln_mode != 0) splitk = 1;  // row statistics need the whole K range in one block
+#define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows)
   switch (cfg) {
-    case 0: launch<C0>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
-    case 1: launch<C1>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
-    case 2: launch<C2>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
-    case 4: launch<C4>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
-    case 5: launch<C5>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
-    case 6: launch<C6>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
-    case 7: launch<C7>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
-    default: launch<C3>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps); break;
+    case 0: DLS_L(C0); break;
+    case 1: DLS_L(C1); break;
+    case 2: DLS_L(C2); break;
+    case 4: DLS_L(C4); break;
+    case 5: DLS_L(C5); break;
+    case 6: DLS_L(C6); break;
+    case 7: DLS_L(C7); break;
+    case 8: DLS_L(C8); break;
+    case 9: DLS_L(C9); break;
+    case 10: DLS_L(C10); break;
+    case 11: DLS_L(C11); break;
+    default: DLS_L(C3); break;
   }
+#undef DLS_L
 }

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+constexpr int kActSwiglu = 4;  // == ACT_SWIGLU in common.h (device-side enum)
+
 struct GemmArgs {
   const void* A;  // bf16 [M][lda]
   int lda;
@@ -30,8 +32,11 @@ void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk);
 size_t gemm_glds_workspace_bytes(int M, int N, int splitk);
 // ln_mode: 0 none, 1 LayerNorm, 2 RMSNorm folded into the GEMM (A = raw input rows,
 // W pre-scaled by the norm gain, ln_colsum[n] = sum_k W[n][k], bias = bias + W.ln_bias)
+// rows (device int32[2], optional): only rows [rows[0], rows[1]) of A/C/R take part (M is then
+// the maximum row count, sizing the grid) — an MoE expert's routed rows without a host sync.
 void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s,
-                      const float* ln_colsum = nullptr, int ln_mode = 0, float ln_eps = 1e-5f);
+                      const float* ln_colsum = nullptr, int ln_mode = 0, float ln_eps = 1e-5f,
+                      const int* rows = nullptr);
 
 struct AttnArgs {
   const void* q; int ldq;   // bf16, row = token (b*S + s), head h at column h*D

@@ -29,27 +29,36 @@ void check_rows(const at::Tensor& t, const char* name) {
 
 at::Tensor as2d(const at::Tensor& t) { return t.dim() == 2 ? t : t.reshape({-1, t.size(-1)}); }
 
-// config: -1 auto; 0..4 LDS-DMA multistage configs; 10..13 register-staged configs.
 // splitk: 0 auto (LDS-DMA path), otherwise forced.
+// config: -1 auto, 0..gemm_glds_num_configs()-1 LDS-DMA kernel, >= kRegStage register-staged kernel.
+// act ACT_SWIGLU: W rows interleave gate/up blocks of 16 (see common.h); the output is N/2 wide.
+// rows (int32[2] on device): only rows [rows[0], rows[1]) of A / out take part (MoE expert ranges).
+constexpr int64_t kRegStage = 100;
+
 at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& residual, int64_t act, double alpha,
                 const c10::optional<at::Tensor>& out, int64_t config, int64_t splitk,
-                const c10::optional<at::Tensor>& ln_colsum, int64_t ln_mode, double ln_eps) {
+                const c10::optional<at::Tensor>& ln_colsum, int64_t ln_mode, double ln_eps,
+                const c10::optional<at::Tensor>& rows) {
   check_bf16(a_in, "A");
   check_bf16(w, "W");
   at::Tensor a = as2d(a_in);
   check_rows(a, "A");
   check_rows(w, "W");
   const int64_t M = a.size(0), K = a.size(1), N = w.size(0);
+  const bool swiglu = act == kActSwiglu;
+  const int64_t NO = swiglu ? N / 2 : N;
   TORCH_CHECK(w.size(1) == K, "W must be [N][K] with K = ", K, ", got ", w.sizes());
   TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8");
+  TORCH_CHECK(!swiglu || (N % 32 == 0 && K % 64 == 0 && !residual.has_value()),
+              "SwiGLU epilogue needs N % 32 == 0, K % 64 == 0 and no residual");
   at::Tensor c;
   if (out.has_value()) {
     c = as2d(*out);
     check_bf16(c, "out");
-    TORCH_CHECK(c.size(0) == M && c.size(1) == N && c.stride(1) == 1, "out must be [M][N]");
+    TORCH_CHECK(c.size(0) == M && c.size(1) == NO && c.stride(1) == 1, "out must be [M][N_out]");
   } else {
-    c = at::empty({M, N}, a.options());
+    c = at::empty({M, NO}, a.options());
   }
   const void* bptr = nullptr;
   if (bias.has_value()) {
@@ -66,6 +75,14 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
     rptr = r.data_ptr();
     ldr = (int)r.stride(0);
   }
+  const int* rowp = nullptr;
+  if (rows.has_value()) {
+    TORCH_CHECK(rows->scalar_type() == at::kInt && rows->numel() == 2 && rows->is_contiguous() &&
+                    rows->device() == a.device(),
+                "rows must be a contiguous int32[2] device tensor");
+    TORCH_CHECK(K % 64 == 0 && ln_mode == 0, "row-ranged GEMM needs K % 64 == 0 and no folded norm");
+    rowp = rows->data_ptr<int>();
+  }
   if (M == 0 || N == 0) return c;
   GemmArgs g{a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0), c.data_ptr(), (int)c.stride(0),
              bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1};
@@ -77,10 +94,12 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                     ln_colsum->numel() == N,
                 "fused norm-GEMM needs fp32 ln_colsum [N]");
     csp = ln_colsum->data_ptr<float>();
-    if (config >= 10) config = -1;
   }
-  if (config >= 10 || !glds_ok) {
-    g.config = config >= 10 ? (int)(config - 10) : -1;
+  if (ln_mode != 0 || swiglu || rowp) {
+    if (config >= kRegStage) config = -1;  // these epilogues live in the LDS-DMA kernel only
+  }
+  if (config >= kRegStage || !glds_ok) {
+    g.config = config >= kRegStage ? (int)(config - kRegStage) : -1;
     launch_gemm_bf16(g, cur_stream());
     return c;
   }
@@ -91,12 +110,14 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
     if (cfg < 0) cfg = acfg;
     if (sk <= 0) sk = ask;
   }
-  const bool split_ok = (N % 8 == 0) && (c.stride(0) % 8 == 0) && (ldr % 8 == 0) && K % (64 * sk) == 0;
-  if (!split_ok) sk = 1;
+  TORCH_CHECK(cfg < gemm_glds_num_configs(), "unknown GEMM config ", cfg);
+  const bool split_ok = (N % 8 == 0) && (c.stride(0) % 8 == 0) && (ldr % 8 == 0) && K % (64 * sk) == 0 &&
+                        (!swiglu || N % 32 == 0);
+  if (!split_ok || ln_mode != 0) sk = 1;
   at::Tensor ws;
   if (sk > 1) ws = at::empty({(int64_t)gemm_glds_workspace_bytes((int)M, (int)N, sk) / 4}, a.options().dtype(at::kFloat));
-  if (ln_mode != 0) sk = 1;
-  launch_gemm_glds(g, cfg, sk, sk > 1 ? ws.data_ptr() : nullptr, cur_stream(), csp, (int)ln_mode, (float)ln_eps);
+  launch_gemm_glds(g, cfg, sk, sk > 1 ? ws.data_ptr() : nullptr, cur_stream(), csp, (int)ln_mode, (float)ln_eps,
+                   rowp);
   return c;
 }
 
@@ -292,7 +313,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Hand-written HIP/CDNA4 (gfx950) kernels for distributed_llm_scheduler_amd";
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),
         py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1,
-        py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5);
+        py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5,
+        py::arg("rows") = py::none());
+  m.attr("REGSTAGE") = kRegStage;
   m.def("gemm_pick_config", &gemm_pick_config);
   m.def("gemm_glds_num_configs", &gemm_glds_num_configs);
   m.def("gemm_glds_pick", [](int M, int N, int K) {

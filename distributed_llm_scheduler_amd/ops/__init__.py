@@ -23,7 +23,9 @@ import torch.nn.functional as F
 
 from . import tuning
 
-ACT = {None: 0, "none": 0, "gelu": 1, "gelu_tanh": 1, "silu": 2, "relu": 3}
+ACT = {None: 0, "none": 0, "gelu": 1, "gelu_tanh": 1, "silu": 2, "relu": 3, "swiglu": 4}
+SWIGLU = 4
+SWIGLU_BLOCK = 16  # gate/up interleave granularity of a SwiGLU-epilogue weight (csrc common.h)
 
 _lock = threading.Lock()
 _ext = None
@@ -76,10 +78,32 @@ def _act_ref(y: torch.Tensor, act) -> torch.Tensor:
     return y
 
 
+def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
+    """[gate (F rows); up (F rows)] -> rows interleaved in blocks of 16 (gate 16c..16c+15, then
+    up 16c..16c+15) — the layout the GEMM's SwiGLU epilogue pairs fragments in. Works for a
+    weight [2F, K] or a per-row vector [2F] (bias, colsum)."""
+    F2 = w.shape[0]
+    assert F2 % (2 * SWIGLU_BLOCK) == 0, "SwiGLU width must be a multiple of 16"
+    F = F2 // 2
+    rest = tuple(w.shape[1:])
+    g = w[:F].reshape((F // SWIGLU_BLOCK, SWIGLU_BLOCK) + rest)
+    u = w[F:].reshape((F // SWIGLU_BLOCK, SWIGLU_BLOCK) + rest)
+    return torch.stack([g, u], 1).reshape((F2,) + rest).contiguous()
+
+
+def _swiglu_interleaved(y: torch.Tensor) -> torch.Tensor:
+    F2 = y.shape[-1]
+    v = y.reshape(y.shape[:-1] + (F2 // (2 * SWIGLU_BLOCK), 2, SWIGLU_BLOCK))
+    return (F.silu(v[..., 0, :]) * v[..., 1, :]).reshape(y.shape[:-1] + (F2 // 2,))
+
+
 def ref_linear(x, w, bias=None, act=None, residual=None, alpha=1.0):
     y = alpha * (x.float() @ w.float().t())
     if bias is not None:
         y = y + bias.float()
+    if (ACT[act] if not isinstance(act, int) else act) == SWIGLU:
+        y = _swiglu_interleaved(y)
+        return (y if residual is None else y + residual.float()).to(x.dtype)
     y = _act_ref(y, act)
     if residual is not None:
         y = y + residual.float()
@@ -139,15 +163,28 @@ def ref_rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t):
 
 # --------------------------------------------------------------------- dispatchers
 
-def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None):
+def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=None, rows_hint=None):
     """``act(alpha * x @ w^T + bias) + residual`` — one MFMA GEMM kernel with the whole
-    epilogue fused on GPU."""
+    epilogue fused on GPU. ``act="swiglu"`` takes a gate/up-interleaved weight
+    (:func:`interleave_gate_up`) and returns the N/2-wide ``silu(gate) * up``. ``rows``
+    (int32[2] tensor on x's device) restricts the GEMM to rows [rows[0], rows[1]) of x and
+    ``out`` without a host sync (MoE experts); ``rows_hint`` is the expected row count used
+    to pick the tuned kernel config."""
+    a = ACT[act] if not isinstance(act, int) else act
+    n_out = w.shape[0] // 2 if a == SWIGLU else w.shape[0]
     if _gpu(x):
-        a = ACT[act] if not isinstance(act, int) else act
-        shp = x.shape[:-1] + (w.shape[0],)
-        cfg, sk = tuning.lookup(x.numel() // x.shape[-1], w.shape[0], w.shape[1])
-        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk)
+        shp = x.shape[:-1] + (n_out,)
+        M = x.numel() // x.shape[-1]
+        cfg, sk = tuning.lookup(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
+        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows)
         return y.view(shp) if out is None else out
+    if rows is not None:
+        r0, r1 = (int(v) for v in rows.tolist())
+        if out is None:
+            out = torch.zeros(x.shape[:-1] + (n_out,), dtype=x.dtype)
+        res = residual[r0:r1] if residual is not None else None
+        out[r0:r1] = ref_linear(x[r0:r1], w, bias, act, res, alpha)
+        return out
     y = ref_linear(x, w, bias, act, residual, alpha)
     if out is not None:
         out.copy_(y)
@@ -174,9 +211,9 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
     "layernorm" or "rmsnorm"."""
     m = {"layernorm": 1, "rmsnorm": 2}[mode]
     a = ACT[act] if not isinstance(act, int) else act
-    shp = x.shape[:-1] + (w_derived.shape[0],)
-    cfg, _ = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1])
-    y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < 10 else -1, 1, colsum, m,
+    shp = x.shape[:-1] + (w_derived.shape[0] // 2 if a == SWIGLU else w_derived.shape[0],)
+    cfg, _ = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
+    y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, 1, colsum, m,
                    float(eps))
     return y.view(shp) if out is None else out
 

@@ -21,11 +21,16 @@ import torch
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _lock = threading.Lock()
 _table: Optional[Dict[str, Tuple[int, int]]] = None
-REGSTAGE = 10  # config ids >= 10 select the register-staged kernel
+REGSTAGE = 100  # config ids >= 100 select the register-staged kernel (csrc ops_binding kRegStage)
 
 
-def _key(M: int, N: int, K: int) -> str:
-    return f"{M}x{N}x{K}"
+def _key(M: int, N: int, K: int, tg: str = "") -> str:
+    return f"{M}x{N}x{K}{tg}"
+
+
+def tag(act: int = 0, ranged: bool = False) -> str:
+    """Variant suffix of a tuning key: SwiGLU epilogue ("s"), device row range ("r")."""
+    return ("s" if act == 4 else "") + ("r" if ranged else "")
 
 
 def table() -> Dict[str, Tuple[int, int]]:
@@ -42,9 +47,16 @@ def table() -> Dict[str, Tuple[int, int]]:
         return _table
 
 
-def lookup(M: int, N: int, K: int) -> Tuple[int, int]:
-    """(config, splitk) for this shape: tuned if known, else (-1, 0) = kernel heuristic."""
-    return table().get(_key(M, N, K), (-1, 0))
+def lookup(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
+    """(config, splitk) for this shape/variant: tuned if known (a variant falls back to the
+    plain shape's LDS-DMA choice), else (-1, 0) = kernel heuristic."""
+    t = table()
+    v = t.get(_key(M, N, K, tg))
+    if v is None and tg:
+        v = t.get(_key(M, N, K))
+        if v is not None and v[0] >= REGSTAGE:
+            v = None
+    return v if v is not None else (-1, 0)
 
 
 def _save() -> None:
@@ -82,8 +94,8 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
     return statistics.median(res)
 
 
-def candidates(M: int, N: int, K: int, n_cfg: int):
-    out = [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1)]
+def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
+    out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1)]
     for cfg in range(n_cfg):
         for sk in (1, 2, 3, 4, 6, 8):
             if K % 64 or K % (64 * sk) or (sk > 1 and N % 8) or K // (64 * sk) < 2:
@@ -94,22 +106,29 @@ def candidates(M: int, N: int, K: int, n_cfg: int):
     return out
 
 
-def tune(M: int, N: int, K: int, device=None, cold: bool = True, save: bool = True, verbose: bool = False):
-    """Time every candidate for (M, N, K) and record the fastest. Returns (cfg, splitk, us)."""
+def tune(M: int, N: int, K: int, device=None, cold: bool = True, save: bool = True, verbose: bool = False,
+         tg: str = ""):
+    """Time every candidate for (M, N, K[, variant]) and record the fastest. Returns
+    ((cfg, splitk, us), {candidate: us}). A ranged variant ("r") is timed as an M-row range
+    inside a grid sized for 4 M rows (how MoE experts launch)."""
     from . import ext
 
     e = ext()
     dev = device or torch.device("cuda")
-    x = (torch.randn(M, K, device=dev) * 0.5).bfloat16()
+    act = 4 if "s" in tg else 0
+    rows_total = 4 * M if "r" in tg else M
+    x = (torch.randn(rows_total, K, device=dev) * 0.5).bfloat16()
+    rng = torch.tensor([M, 2 * M], dtype=torch.int32, device=dev) if "r" in tg else None
     wbytes = N * K * 2
     copies = max(1, min(64, (512 << 20) // max(wbytes, 1) + 1)) if cold else 1
     ws = [(torch.randn(N, K, device=dev) * 0.05).bfloat16() for _ in range(copies)]
-    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(rows_total, N // 2 if act == 4 else N, device=dev, dtype=torch.bfloat16)
     best = None
     results = {}
-    for cfg, sk in candidates(M, N, K, e.gemm_glds_num_configs()):
+    for cfg, sk in candidates(M, N, K, e.gemm_glds_num_configs(), tg):
         try:
-            t = _graph_time(lambda i: e.gemm(x, ws[i % copies], None, None, 0, 1.0, out, cfg, sk))
+            t = _graph_time(lambda i: e.gemm(x, ws[i % copies], None, None, act, 1.0, out, cfg, sk, None, 0, 1e-5,
+                                             rng))
         except RuntimeError:
             continue
         results[(cfg, sk)] = t
@@ -119,15 +138,17 @@ def tune(M: int, N: int, K: int, device=None, cold: bool = True, save: bool = Tr
             print(f"  {M}x{N}x{K} cfg={cfg} splitk={sk}: {t:.2f} us")
     del ws
     if best is not None:
-        table()[_key(M, N, K)] = (best[0], best[1])
+        table()[_key(M, N, K, tg)] = (best[0], best[1])
         if save:
             _save()
     return best, results
 
 
-def ensure_tuned(shapes: Iterable[Tuple[int, int, int]], device=None) -> None:
-    """Tune every shape not yet in the table (called by the executor at setup)."""
-    for M, N, K in sorted(set(shapes)):
-        if _key(M, N, K) not in table():
-            tune(M, N, K, device=device, save=False)
+def ensure_tuned(shapes: Iterable[tuple], device=None) -> None:
+    """Tune every (M, N, K[, variant]) not yet in the table (called by the executor at setup)."""
+    for sh in sorted(set(shapes)):
+        M, N, K = sh[:3]
+        tg = sh[3] if len(sh) > 3 else ""
+        if _key(M, N, K, tg) not in table():
+            tune(M, N, K, device=device, save=False, tg=tg)
     _save()

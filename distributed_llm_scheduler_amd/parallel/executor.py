@@ -56,6 +56,9 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
     return torch.randint(0, vocab, (n,), generator=g, dtype=torch.int32)
 
 
+FOLD_MAX_K = 1024  # fold a preceding norm into the GEMM only up to this K (see DAGExecutor._gemm)
+
+
 class DAGExecutor:
     def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
                  model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True,
@@ -78,6 +81,8 @@ class DAGExecutor:
         self._derived_cache: Dict[tuple, tuple] = {}             # (weight, ptr) -> (colsum, bias') for folded norms
         self._valid: List[Tuple[int, int, str]] = []  # param arena regions holding data
         self._inputs: Dict[str, torch.Tensor] = {}
+        self._scratch_bufs: Dict[str, torch.Tensor] = {}
+        self._moe_memo: Dict[tuple, tuple] = {}
         self._pending_sends: List[Tuple[int, int, object]] = []
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
@@ -131,17 +136,24 @@ class DAGExecutor:
         return sorted(shapes)
 
     def _gemm_shapes_of(self, t):
+        """(M, N, K, variant) of the GEMMs task ``t`` launches (see ops.tuning.tag)."""
         shapes = set()
         op = t.op
         if op is not None and op.out_shape:
             M = math.prod(op.out_shape[:-1])
             g = self.store.groups
             spec = {s.name: s for pid in t.params_needed for s in g[pid].tensors}
-            names = [v for k, v in op.weights.items() if k.startswith("w") and isinstance(v, str)]
-            for n in names:
+            names = [(k, v) for k, v in op.weights.items() if k.startswith("w") and isinstance(v, str)]
+            for wk, n in names:
                 if n in spec and len(spec[n].shape) == 2 and op.kind not in ("embedding", "layernorm", "rmsnorm"):
                     N, K = spec[n].shape
-                    shapes.add((M, N, K))
+                    if op.kind == "moe_expert":
+                        hint = max(1, M * op.attrs["top_k"] // op.attrs["n_experts"])
+                        shapes.add((hint, N, K, "sr" if wk == "w_gate_up" else "r"))
+                    elif op.kind == "swiglu_mlp" and wk == "w_gate_up":
+                        shapes.add((M, N, K, "s"))
+                    else:
+                        shapes.add((M, N, K, ""))
         return shapes
 
     def _workspace_bytes(self, ins) -> int:
@@ -219,39 +231,101 @@ class DAGExecutor:
             self._rope[key] = ops.rope_tables(S, D, theta, self.device)
         return self._rope[key]
 
-    # --- norm folding (GPU): derived weights, recomputed after every real fill of W ---
-    def _derived(self, norm: Task, w_name: str, b_name: Optional[str]):
-        """(W', colsum, bias') for a norm folded into the GEMM on weight ``w_name``; W is
-        overwritten IN PLACE by W' (it is read by this fused group only)."""
+    # --- derived weights, recomputed after every real fill of W (cache keyed by W's address) ---
+    def _prep(self, w_name: str, norm: Optional[Task] = None, b_name: Optional[str] = None,
+              interleave: bool = False):
+        """(W, colsum, bias) for the GEMM on weight ``w_name``, transformed IN PLACE once per
+        fill: a preceding norm folded in (W' = W*gain, colsum(W'), bias' = bias + W.beta) and/or
+        the gate/up rows interleaved for the SwiGLU epilogue (every per-row vector with them).
+        W is read by this fused group only, so overwriting it is safe."""
         W = self._w(w_name)
         key = (w_name, W.data_ptr())
         d = self._derived_cache.get(key)
         if d is None:
-            nw = self._w(norm.op.weights["w"])
-            nb = self._w(norm.op.weights["b"]) if "b" in norm.op.weights else None
             bias = self._w(b_name) if b_name else None
-            wd, cs, bd = ops.derive_norm_gemm(W, nw, nb, bias)
-            W.copy_(wd)
-            d = (cs, bd if (bias is not None or nb is not None) else None)
+            cs = None
+            if norm is not None:
+                nw = self._w(norm.op.weights["w"])
+                nb = self._w(norm.op.weights["b"]) if "b" in norm.op.weights else None
+                wd, cs, bd = ops.derive_norm_gemm(W, nw, nb, bias)
+                bias = bd if (bias is not None or nb is not None) else None
+            else:
+                wd = W
+            if interleave:
+                wd = ops.interleave_gate_up(wd)
+                cs = ops.interleave_gate_up(cs) if cs is not None else None
+                bias = ops.interleave_gate_up(bias) if bias is not None else None
+            if wd is not W:
+                W.copy_(wd)
+            d = (cs, bias)
             self._derived_cache[key] = d
         return W, d[0], d[1]
 
     def _gemm(self, x, w_name, b_name, norm: Optional[Task], act=None, residual=None, out=None):
-        """One GEMM node, optionally with a preceding norm folded in."""
-        if norm is None:
-            return ops.linear(x, self._w(w_name), self._w(b_name) if b_name else None, act=act,
-                              residual=residual, out=out)
-        if self.gpu:
-            W, cs, bd = self._derived(norm, w_name, b_name)
+        """One GEMM node, optionally with a preceding norm folded in (GPU, K <= FOLD_MAX_K:
+        the in-kernel row statistics cost more than a separate norm pass at larger K and
+        force split-K off; measured on MI355X, Llama-3-8B K=4096: 109 vs 45+8 us).
+        ``act="swiglu"``: W is a [gate; up] weight, interleaved on first use."""
+        sw = act == "swiglu"
+        if norm is not None and self.gpu and x.shape[-1] <= FOLD_MAX_K:
+            W, cs, bd = self._prep(w_name, norm, b_name, interleave=sw)
             return ops.linear_norm(x, W, cs, bd, norm.op.kind, norm.op.attrs.get("eps", 1e-5), act=act,
                                    residual=residual, out=out)
-        nw = self._w(norm.op.weights["w"])
-        if norm.op.kind == "layernorm":
-            xn = ops.layernorm(x, nw, self._w(norm.op.weights["b"]), norm.op.attrs.get("eps", 1e-5))
+        if norm is not None:
+            nw = self._w(norm.op.weights["w"])
+            xn = self._scratch("norm", x.shape)
+            if norm.op.kind == "layernorm":
+                ops.layernorm(x, nw, self._w(norm.op.weights["b"]), norm.op.attrs.get("eps", 1e-5), out=xn)
+            else:
+                ops.rmsnorm(x, nw, norm.op.attrs.get("eps", 1e-5), out=xn)
+            x = xn
+        if sw:
+            W, _, bias = self._prep(w_name, None, b_name, interleave=True)
         else:
-            xn = ops.rmsnorm(x, nw, norm.op.attrs.get("eps", 1e-5))
-        return ops.linear(xn, self._w(w_name), self._w(b_name) if b_name else None, act=act, residual=residual,
-                          out=out)
+            W, bias = self._w(w_name), (self._w(b_name) if b_name else None)
+        return ops.linear(x, W, bias, act=act, residual=residual, out=out)
+
+    def _scratch(self, tag: str, shape) -> torch.Tensor:
+        """Reusable per-rank buffer (allocated on first use, i.e. in an eager warm-up step,
+        never during hipGraph capture)."""
+        n = math.prod(shape)
+        buf = self._scratch_bufs.get(tag)
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(n, dtype=self.dtype, device=self.device)
+            self._scratch_bufs[tag] = buf
+        return buf[:n].view(shape)
+
+    def _moe_routing(self, h_name: str, r_name: str, E: int, top_k: int):
+        """Routing of one MoE layer on this rank, computed ONCE per step and shared by every
+        expert node placed here: top-k gates, expert-sorted token rows (permuted copy of the
+        normalised hidden states), slot map and per-expert row offsets — all on device."""
+        key = (h_name, r_name)
+        r = self._moe_memo.get(key)
+        if r is None:
+            h = self._flat(self._x(h_name))
+            idx, gate = ops.moe_router(self._flat(self._x(r_name)), top_k)
+            src, slot, off = ops.moe_align(idx, E)
+            xp = ops.moe_permute(h, src)
+            r = (xp, gate, slot, off)
+            self._moe_memo[key] = r
+        return r
+
+    def _moe_expert(self, t: Task, out: torch.Tensor) -> None:
+        """One expert node: its routed rows (a device-side range of the permuted rows) run
+        gate_up GEMM with the SwiGLU epilogue and the down GEMM, then are gate-weighted into
+        this node's [M, H] output (zero for tokens not routed here)."""
+        a, W = t.op.attrs, t.op.weights
+        E, K, e = a["n_experts"], a["top_k"], a["expert"]
+        xp, gate, slot, off = self._moe_routing(t.op.inputs[0], t.op.inputs[1], E, K)
+        rows = off[e:e + 2]
+        R, F = xp.shape[0], a["ffn"]
+        hint = max(1, R // E)
+        hbuf = self._scratch("moe_h", (R, F))
+        ybuf = self._scratch("moe_y", (R, xp.shape[1]))
+        W13, _, _ = self._prep(W["w_gate_up"], None, None, interleave=True)
+        ops.linear(xp, W13, act="swiglu", out=hbuf, rows=rows, rows_hint=hint)
+        ops.linear(hbuf, self._w(W["w_down"]), out=ybuf, rows=rows, rows_hint=hint)
+        ops.moe_combine(ybuf, slot, gate, rows, out)
 
     def _run_group(self, ins) -> None:
         grp = [self.tasks[t] for t in ins.group]
@@ -306,16 +380,11 @@ class DAGExecutor:
         elif k == "swiglu_mlp":
             x = self._flat(self._x(src))
             M, F = x.shape[0], a["ffn"]
-            gu = self._ws(0, (M, 2 * F))
-            h = self._ws(M * 2 * F, (M, F))
-            self._gemm(x, W["w_gate_up"], None, norm, out=gu)
-            ops.swiglu(gu, out=h)
+            h = self._ws(0, (M, F))
+            self._gemm(x, W["w_gate_up"], None, norm, act="swiglu", out=h)  # SwiGLU in the epilogue
             ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out))
         elif k == "moe_expert":
-            h = self._flat(self._x(head.op.inputs[0]))
-            logits = self._flat(self._x(head.op.inputs[1]))
-            ops.moe_expert(h, logits, self._w(W["w_gate_up"]), self._w(W["w_down"]), a["expert"], a["n_experts"],
-                           a["top_k"], out=self._flat(out))
+            self._moe_expert(head, self._flat(out))
         elif k in ("moe_combine", "sum"):
             # sum of partial outputs (expert contributions + residual, or TP shard partials)
             ins_ = head.op.inputs
@@ -340,6 +409,7 @@ class DAGExecutor:
         pg = self.pg
         tr = self.trace
         self._pending_sends = []
+        self._moe_memo = {}
         recv_work: Dict[str, Tuple[object, object]] = {}
         for i, ins in enumerate(self.prog.instrs):
             if tr:
