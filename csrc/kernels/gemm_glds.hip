@@ -53,32 +53,18 @@ struct Cfg {
   static_assert(STAGES >= 2 && STAGES <= 8, "stages");
 };
 
+// One output tile (tm, tn) over K-slice ks. Everything from here to the end of the epilogue
+// is per tile; the kernel below maps blocks to tiles (or loops over a device-side row range).
 template <class C>
-__global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
-                                                         const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
-                                                         int ldc, const bf16* __restrict__ bias,
-                                                         const bf16* __restrict__ R, int ldr,
-                                                         float* __restrict__ part, int M, int N, int K, int act,
-                                                         float alpha, int tiles_m, int tiles_n, int splitk,
-                                                         int kslice, const float* __restrict__ ln_colsum,
-                                                         int ln_mode, float ln_eps, const int* __restrict__ rows) {
-  __shared__ bf16x8 smem[C::STAGES * C::STAGE];
+__device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
+                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
+                                          const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
+                                          float* __restrict__ part, int M, int Mmax, int N, int K, int act,
+                                          float alpha, int ks, int kslice, int tm, int tn,
+                                          const float* __restrict__ ln_colsum, int ln_mode, float ln_eps) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WN, wn = wave % C::WN;
-  const int ntile = tiles_m * tiles_n;
-  const int bid = xcd_remap(blockIdx.x, ntile * splitk);
-  const int ks = bid / ntile, tile = bid % ntile;
-  const int tm = tile % tiles_m, tn = tile / tiles_m;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
-  const int Mmax = M;
-  if (rows != nullptr) {  // device-side row range (MoE expert): M is only the grid's bound
-    const int r0 = rows[0];
-    M = rows[1] - r0;
-    A += (size_t)r0 * lda;
-    Cp += (size_t)r0 * ldc;
-    if (R) R += (size_t)r0 * ldr;
-    if (part) part += (size_t)r0 * N;
-  }
   if (m0 >= M) return;  // whole block idle (uniform: before any barrier)
   const int kbeg = ks * kslice;
   const int nk = kslice / C::BK;
@@ -210,7 +196,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   // (the LM head writes 50257 columns into rows padded to 50304); a fragment whose 4
   // columns straddle N falls back to scalars.
   const bool vec_ok = (ldc % 4 == 0) && (!R || ldr % 4 == 0);
-  if (splitk > 1) {
+  if (part != nullptr) {  // split-K: fp32 partial slab, reduced by splitk_reduce_kernel
     float* P = part + (size_t)ks * Mmax * N;
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
@@ -334,6 +320,39 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   }
 }
 
+template <class C>
+__global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
+                                                         const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
+                                                         int ldc, const bf16* __restrict__ bias,
+                                                         const bf16* __restrict__ R, int ldr,
+                                                         float* __restrict__ part, int M, int N, int K, int act,
+                                                         float alpha, int tiles_m, int tiles_n, int splitk,
+                                                         int kslice, const float* __restrict__ ln_colsum,
+                                                         int ln_mode, float ln_eps, const int* __restrict__ rows) {
+  __shared__ bf16x8 smem[C::STAGES * C::STAGE];
+  const int ntile = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, ntile * splitk);
+  const int ks = bid / ntile, tile = bid % ntile;
+  const int tm = tile % tiles_m, tn = tile / tiles_m;
+  if (rows == nullptr) {
+    glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn,
+                 ln_colsum, ln_mode, ln_eps);
+    return;
+  }
+  // device-side row range (MoE expert): the host launched ONE tile row (tiles_m == 1) — no
+  // idle blocks holding CUs — and each block walks the range's M tiles of its column panel
+  const int r0 = rows[0], Mr = rows[1] - r0;
+  A += (size_t)r0 * lda;
+  Cp += (size_t)r0 * ldc;
+  if (R) R += (size_t)r0 * ldr;
+  if (part) part += (size_t)r0 * N;
+  for (int t = 0; t * C::BM < Mr; ++t) {
+    if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
+    glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, Mr, M, N, K, act, alpha, ks, kslice, t, tn,
+                 ln_colsum, ln_mode, ln_eps);
+  }
+}
+
 // out = act(alpha * sum_s P[s] + bias) + R, 8 columns per lane (N % 8 == 0). ACT_SWIGLU: P is in
 // the interleaved W' space (N wide), out is N/2 wide: out col c <- gate 32(c/16) + c%16, up +16.
 // rows (optional device int32[2]) restricts to a row range as in the GEMM.
@@ -400,7 +419,7 @@ template <class C>
 void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
             float ln_eps, const int* rows) {
   static_assert(2 * C::BM * sizeof(float) <= C::STAGES * C::STAGE * 16, "LN stats must fit the staging LDS");
-  const int tiles_m = (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
+  const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;
   dim3 grid(tiles_m * tiles_n * splitk), block(C::T);
   hipLaunchKernelGGL((gemm_glds_kernel<C>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, a.ldw,
