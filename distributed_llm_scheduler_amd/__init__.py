@@ -10,11 +10,12 @@ Layers (see README.md):
   utils/     tracing (Chrome trace, roctx), config, serialization
 """
 from .core import (ALL_SCHEDULERS, SCHEDULERS, BaseScheduler, CriticalPathScheduler, DFSScheduler, EFTScheduler,
-                   GreedyScheduler, MRUScheduler, Node, OpSpec, Task, get_scheduler)
+                   GreedyChainScheduler, GreedyScheduler, MRUPaperScheduler, MRUScheduler, Node, OpSpec, Task,
+                   get_scheduler)
 
 __version__ = "0.1.0"
 
 __all__ = [
     "Task", "Node", "OpSpec", "BaseScheduler", "DFSScheduler", "GreedyScheduler", "CriticalPathScheduler",
-    "MRUScheduler", "EFTScheduler", "SCHEDULERS", "ALL_SCHEDULERS", "get_scheduler",
+    "MRUScheduler", "EFTScheduler", "GreedyChainScheduler", "MRUPaperScheduler", "SCHEDULERS", "ALL_SCHEDULERS", "get_scheduler",
 ]

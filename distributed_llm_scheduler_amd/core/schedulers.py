@@ -535,6 +535,133 @@ class EFTScheduler(BaseScheduler):
                            f"{_native.error()}")
 
 
+class GreedyChainScheduler(GreedyScheduler):
+    """Chain-first greedy, as the paper describes it (PDF p.6 Alg. 4; the reference keeps
+    ``identify_sequential_chains`` as dead code, schedulers.py:213-242).
+
+    Phase 1: every sequential chain (from a source, following single dependents whose only
+    dependency is the previous link) goes, in order, to the node with the most available
+    memory at the time the chain is considered, until a link does not fit. Phase 2: the
+    remaining tasks run through the round loop; each picks, among nodes it fits on, the
+    one caching most of its parameters (ties: most available memory).
+    """
+
+    native_policy = None  # python engine only
+    name = "Greedy_chain"
+
+    def identify_sequential_chains(self) -> List[List[str]]:
+        chains, seen = [], set()
+        for start in (t for t in self._insertion if not self.tasks[t].dependencies):
+            chain, cur = [], start
+            while cur is not None and cur not in seen:
+                chain.append(cur)
+                seen.add(cur)
+                nxt = self.task_dependencies.get(cur, [])
+                cur = nxt[0] if (len(nxt) == 1 and nxt[0] in self.tasks
+                                 and list(self.tasks[nxt[0]].dependencies) == [chain[-1]]) else None
+            if len(chain) > 1:
+                chains.append(chain)
+        return chains
+
+    def _schedule_python(self):
+        placed: Dict[str, List[str]] = {}
+        for chain in self.identify_sequential_chains():
+            node = max(self.nodes.values(), key=lambda n: n.available_memory)  # first wins ties
+            for tid in chain:
+                task = self.tasks[tid]
+                if tid not in self.pending_tasks or not self.is_task_ready(tid) or not self.can_fit_on_node(task, node):
+                    break
+                if self.assign_task_to_node(task, node):
+                    placed.setdefault(node.id, []).append(tid)
+
+        def choose(task):
+            best, key = None, None
+            for node in self.nodes.values():
+                if not self.can_fit_on_node(task, node):
+                    continue
+                k = (len(task.params_needed & node.cached_params), node.available_memory)
+                if key is None or k > key:
+                    best, key = node, k
+            return best
+
+        for nid, tids in self._rounds(None, choose).items():
+            placed.setdefault(nid, []).extend(tids)
+        return placed
+
+
+class MRUPaperScheduler(MRUScheduler):
+    """MRU exactly as the paper's Alg. 5 writes it (PDF p.16): node score
+    ``20·|P∩C| + 0.1·A − 0.5·|completed|``, −10 when the task only fits after eviction, and
+    parameters scoring ≥ 1000 (needed by a ready task) are never eviction candidates. The
+    code's variant (``MRU_spec``) uses ``+A``, ``+5`` and no filter."""
+
+    native_policy = None  # python engine only
+    name = "MRU_paper"
+
+    def evict_params_for_task(self, node: Node, task: Task) -> bool:
+        shortage = self.calculate_memory_requirement(task, node) - node.available_memory
+        if shortage <= 0:
+            return True
+        cands = []
+        for p in node.cached_params:
+            if p in task.params_needed:
+                continue
+            sc = self.calculate_eviction_score(p, node)
+            if sc < 1000:
+                cands.append((sc, p))
+        freed, gone = 0, []
+        for _, p in sorted(cands):
+            if freed >= shortage:
+                break
+            node.cached_params.remove(p)
+            node.available_memory += self.param_size(p)
+            self.param_locations[p].discard(node.id)
+            freed += self.param_size(p)
+            gone.append(p)
+        if freed >= shortage:
+            for p in gone:
+                self._event("EVICT", node.id, p)
+            return True
+        for p in gone:
+            node.cached_params.add(p)
+            node.available_memory -= self.param_size(p)
+            self.param_locations[p].add(node.id)
+        return False
+
+    def _schedule_python(self):
+        def bump():
+            self.time_step += 1
+
+        def rank(ready):
+            u = {t.id: len([d for d in self.task_dependencies.get(t.id, []) if d in self.pending_tasks])
+                 for t in ready}
+            return sorted(ready, key=lambda t: u[t.id], reverse=True)
+
+        def choose(task):
+            best, best_score = None, -float("inf")
+            for node in self.nodes.values():
+                score = len(task.params_needed & node.cached_params) * 20 + node.available_memory * 0.1
+                score -= len(node.completed_tasks) * 0.5
+                if self.can_fit_on_node(task, node):
+                    pass
+                elif self.evict_params_for_task(node, task):
+                    score -= 10
+                else:
+                    continue
+                if score > best_score:
+                    best, best_score = node, score
+            if best is not None and not self.can_fit_on_node(task, best):
+                self.evict_params_for_task(best, task)
+            return best
+
+        def account(task):
+            for p in task.params_needed:
+                self.param_usage_count[p] += 1
+                self.param_last_used[p] = self.time_step
+
+        return self._rounds(rank, choose, before_round=bump, after_assign=account)
+
+
 #: name -> class, using the reference's evaluation names (simulation.py:570-575)
 SCHEDULERS = {
     "DFS": DFSScheduler,
@@ -542,7 +669,7 @@ SCHEDULERS = {
     "Critical": CriticalPathScheduler,
     "MRU_spec": MRUScheduler,
 }
-ALL_SCHEDULERS = dict(SCHEDULERS, EFT=EFTScheduler)
+ALL_SCHEDULERS = dict(SCHEDULERS, EFT=EFTScheduler, Greedy_chain=GreedyChainScheduler, MRU_paper=MRUPaperScheduler)
 
 
 def get_scheduler(name: str) -> type:

@@ -306,9 +306,13 @@ def print_summaries(df) -> None:
     print(s[["completion_rate", "makespan", "cache_hit_rate"]])
 
 
-def main(num_runs: int = 3, seed: int = 0, out_dir: str = "evaluation_results", engine: Optional[str] = None):
+def main(num_runs: int = 3, seed: int = 0, out_dir: str = "evaluation_results", engine: Optional[str] = None,
+         schedulers: Optional[Sequence[str]] = None):
+    """``schedulers``: names from ALL_SCHEDULERS (default: the reference's four)."""
     print("Starting Scheduler Evaluation...")
-    ev = ImprovedSchedulerEvaluator(SCHEDULERS, seed=seed, engine=engine)
+    from ..core.schedulers import ALL_SCHEDULERS
+    table = SCHEDULERS if not schedulers else {n: ALL_SCHEDULERS[n] for n in schedulers}
+    ev = ImprovedSchedulerEvaluator(table, seed=seed, engine=engine)
     ev.run_experiments(num_runs=num_runs)
     ev.analyze_results(out_dir)
     print(f"\nEvaluation complete! Check '{out_dir}' directory for outputs.")

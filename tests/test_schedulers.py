@@ -215,3 +215,46 @@ def test_greedy_chain_identification():
     for t in DAGGenerator.generate_pipeline_dag(2, width=1):
         s.add_task(t)
     assert s.identify_sequential_chains() == [["stage_0_worker_0", "stage_1_worker_0", "final_output"]]
+
+
+def test_greedy_chain_places_chains_on_roomiest_node():
+    from distributed_llm_scheduler_amd.core import GreedyChainScheduler
+    tasks = [Task("a", 0.1, 0.1, [], {"pa"}), Task("b", 0.1, 0.1, ["a"], {"pb"}), Task("c", 0.1, 0.1, ["b"], {"pc"}),
+             Task("x", 0.1, 0.1, [], {"px"}), Task("y", 0.1, 0.1, ["x", "c"], {"pa"})]
+    nodes = [Node("n1", 2.0), Node("n2", 3.0)]
+    s, sch = run(GreedyChainScheduler, tasks, nodes)
+    assert s.identify_sequential_chains() == [["a", "b", "c"]]
+    assert sch["n2"][:3] == ["a", "b", "c"]
+    assert len(s.completed_tasks) == 5
+    # y needs pa, cached on n2 by the chain: phase 2 prefers the node caching it
+    assert "y" in sch["n2"]
+
+
+def test_mru_paper_never_evicts_params_a_ready_task_needs():
+    from distributed_llm_scheduler_amd.core import MRUPaperScheduler
+    tasks = [Task("r", 0.1, 0.1, [], {"p1"}), Task("big", 0.1, 0.1, [], {"q1", "q2"})]
+    for cls, expect in ((MRUScheduler, True), (MRUPaperScheduler, False)):
+        s = cls([Node("n", 1.5)])
+        for t in tasks:
+            s.add_task(t.clone())
+        node = s.nodes["n"]
+        for p in ("p1", "p2"):
+            node.cached_params.add(p)
+            node.available_memory -= 0.5
+            s.param_locations[p].add("n")
+        # big needs 1.1 GB, 0.5 free: both cached params must go; p1 is needed by ready task r
+        assert s.evict_params_for_task(node, s.tasks["big"]) is expect
+        assert ("p1" in node.cached_params) is (not expect)
+
+
+@pytest.mark.parametrize("name", ["Greedy_chain", "MRU_paper"])
+def test_paper_variants_on_llm_dags(name):
+    from distributed_llm_scheduler_amd.eval.simulation import ImprovedSchedulerEvaluator
+    g = DAGGenerator()
+    tasks = g.generate_llm_dag(8, attention_heads=4)
+    ev = ImprovedSchedulerEvaluator(ALL_SCHEDULERS)
+    for regime, floor in ((1.0, 0.85), (0.8, 0.5)):
+        nodes = ev.create_nodes_with_memory_regime(ev.calculate_total_memory_needed(tasks), regime, 2)
+        s, sch = run(ALL_SCHEDULERS[name], tasks, nodes)
+        assert len(s.completed_tasks) + len(s.failed_tasks) + len(s.orphaned_tasks) == len(tasks)
+        assert len(s.completed_tasks) >= floor * len(tasks), (regime, len(s.completed_tasks))
