@@ -6,6 +6,7 @@ lowering are pure functions of their arguments.
 """
 from __future__ import annotations
 
+import json
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -33,6 +34,7 @@ class Plan:
     world: int
     cap_gb: float
     stats: Dict = field(default_factory=dict)
+    args: Dict = field(default_factory=dict)  # plan() arguments (checkpoint / replan)
 
     @property
     def completed(self) -> int:
@@ -46,7 +48,7 @@ class Plan:
 def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: float = 288.0, replicas: int = 1,
          batch: int = 1, seq: int = 512, cost_model: str = "bytes", fuse: bool = True,
          node_speeds: Optional[Sequence[float]] = None, link_bw_gbps: float = 153.0,
-         placement: str = "scheduler", tp: int = 1) -> Plan:
+         placement: str = "scheduler", tp: int = 1, resume: Optional[str] = None) -> Plan:
     """Build the DAG of ``replicas`` requests of ``model``, place it on ``world`` GPUs with
     ``scheduler`` under a per-GPU cap of ``cap_gb`` and lower it to per-rank programs.
 
@@ -59,7 +61,14 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         shard-sum / residual / embedding / head nodes on GPU 0 (tensor parallelism).
     The fixed placements still go through the scheduler's memory accounting (tasks that
     do not fit fail exactly as in the policies).
+
+    ``resume``: path of a placement saved by :func:`save_plan` — the saved decision (task
+    order per GPU and the LOAD/EVICT trace) is reused instead of re-running the policy; the
+    DAG is rebuilt from the saved arguments, which must match this call's.
     """
+    args = dict(model=model, world=world, scheduler=scheduler, cap_gb=cap_gb, replicas=replicas, batch=batch,
+                seq=seq, cost_model=cost_model, fuse=fuse, node_speeds=list(node_speeds) if node_speeds else None,
+                link_bw_gbps=link_bw_gbps, placement=placement, tp=tp)
     tasks, groups, cfg = registry.build(model, batch=batch, seq=seq, replicas=replicas, cost_model=cost_model, tp=tp)
     param_bytes = {pid: group_layout(g)[0] for pid, g in groups.items()}
     nodes = [Node(f"gpu{r}", cap_gb, (node_speeds[r] if node_speeds else 1.0), device=r) for r in range(world)]
@@ -73,7 +82,9 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     sched = cls([n.fresh() for n in nodes], **kw)
     for t in tasks:
         sched.add_task(t.clone())
-    if placement == "scheduler":
+    if resume is not None:
+        sched, schedule = _resume(resume, args, sched)
+    elif placement == "scheduler":
         schedule = sched.schedule()
     elif placement in ("replica", "pipeline", "tensor"):
         schedule = _fixed_schedule(tasks, world, sched, placement, cfg)
@@ -84,10 +95,72 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     caps = {r: int(cap_gb * 1e9) for r in range(world)}
     programs = build_programs(tasks, place, order, world, param_bytes, caps, events=sched.events,
                               node_rank=node_rank, fuse=fuse)
-    p = Plan(model, tasks, groups, cfg, cls.name if placement == "scheduler" else placement, sched, schedule, place, order, node_rank, programs, param_bytes,
-             world, cap_gb)
+    name = cls.name if placement == "scheduler" else placement
+    p = Plan(model, tasks, groups, cfg, name, sched, schedule, place, order, node_rank, programs, param_bytes,
+             world, cap_gb, args=args)
     p.stats = plan_stats(p)
     return p
+
+
+_PLAN_FORMAT = "dlsched-plan/1"
+
+
+def save_plan(p: Plan, path: str) -> None:
+    """Checkpoint a placement: the plan() arguments, the per-GPU task order and the
+    scheduler's action trace (RUN / LOAD / EVICT / FAIL). Resume with ``plan(resume=path)``."""
+    s = p.scheduler
+    doc = {"format": _PLAN_FORMAT, "args": p.args, "scheduler": p.scheduler_name, "schedule": p.schedule,
+           "events": [list(e) for e in s.events], "failed": sorted(s.failed_tasks),
+           "stats": {k: v for k, v in p.stats.items() if isinstance(v, (int, float, list))}}
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
+class _ResumedSchedule:
+    """Scheduler-shaped view of a saved decision (what build_programs / Plan consume)."""
+
+    def __init__(self, sched, doc):
+        self.tasks = sched.tasks
+        self.nodes = sched.nodes
+        self.events = [tuple(e) for e in doc["events"]]
+        self.failed_tasks = set(doc.get("failed", []))
+        self.completed_tasks = set()
+        self.orphaned_tasks = set()
+        for _, act, node, item in self.events:
+            if act == "RUN":
+                if item not in self.tasks:
+                    raise ValueError(f"saved placement runs unknown task {item!r}")
+                self.tasks[item].assigned_node = node
+                self.completed_tasks.add(item)
+        self.orphaned_tasks = set(self.tasks) - self.completed_tasks - self.failed_tasks
+
+
+def _resume(path: str, args: Dict, sched):
+    with open(path) as f:
+        doc = json.load(f)
+    if doc.get("format") != _PLAN_FORMAT:
+        raise ValueError(f"{path}: not a saved plan")
+    saved = dict(doc["args"])
+    mismatch = {k: (saved.get(k), v) for k, v in args.items() if k not in ("fuse",) and saved.get(k) != v}
+    if mismatch:
+        raise ValueError(f"saved plan was made with different arguments: {mismatch}")
+    return _ResumedSchedule(sched, doc), {k: list(v) for k, v in doc["schedule"].items()}
+
+
+def replan(p: Plan, lost_ranks: Sequence[int], **overrides) -> Plan:
+    """Device loss: re-place the whole DAG on the surviving GPUs (ranks renumbered densely,
+    speeds kept). The SURVEY §5 "device-loss injection -> re-plan onto survivors" path; the
+    executor side is :func:`make_executor` on the new plan's programs."""
+    lost = set(lost_ranks)
+    keep = [r for r in range(p.world) if r not in lost]
+    if not keep:
+        raise RuntimeError("no surviving devices")
+    a = dict(p.args)
+    a.update(world=len(keep))
+    if a.get("node_speeds"):
+        a["node_speeds"] = [a["node_speeds"][r] for r in keep]
+    a.update(overrides)
+    return plan(**a)
 
 
 def _layer_of(tid: str, n_layer: int) -> int:

@@ -200,3 +200,31 @@ def test_tensor_parallel_two_ranks(model):
     assert res[1]["shards"] > 0 and res[1]["sends"] > 0 and res[1]["recvs"] > 0
     errs = [e for r in res for e in r["errs"]]
     assert len(errs) == 1 and errs[0][0] < 0.03 * errs[0][1]
+
+
+def test_plan_checkpoint_resume(tmp_path):
+    p = runtime.plan("tiny-gpt2", world=2, scheduler="MRU_spec", seq=16, replicas=2, cap_gb=0.01)
+    path = str(tmp_path / "plan.json")
+    runtime.save_plan(p, path)
+    q = runtime.plan("tiny-gpt2", world=2, scheduler="MRU_spec", seq=16, replicas=2, cap_gb=0.01, resume=path)
+    assert q.placement == p.placement and q.order == p.order
+    assert [i.__dict__ for i in q.programs[0].instrs] == [i.__dict__ for i in p.programs[0].instrs]
+    with pytest.raises(ValueError):
+        runtime.plan("tiny-gpt2", world=2, scheduler="MRU_spec", seq=32, replicas=2, cap_gb=0.01, resume=path)
+    # a resumed single-rank plan still executes to the reference
+    p1 = runtime.plan("tiny-gpt2", world=1, seq=16)
+    runtime.save_plan(p1, path)
+    q1 = runtime.plan("tiny-gpt2", world=1, seq=16, resume=path)
+    store = runtime.make_store(q1)
+    ex = runtime.make_executor(q1, 0, "cpu", store)
+    ex.step()
+    err, scale = _ref_check(q1, ex, store)
+    assert err < 0.02 * scale
+
+
+def test_replan_after_device_loss():
+    p = runtime.plan("tiny-gpt2", world=3, seq=16, replicas=3, node_speeds=[1.0, 1.2, 0.8])
+    q = runtime.replan(p, [1])
+    assert q.world == 2 and q.args["node_speeds"] == [1.0, 0.8]
+    assert q.completed == q.total
+    assert set(q.placement.values()) <= {0, 1}
