@@ -57,12 +57,13 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
 
 
 FOLD_MAX_K = 1024  # fold a preceding norm into the GEMM only up to this K (see DAGExecutor._gemm)
+GUARD_BYTES, GUARD_VALUE = 4096, 0xA5  # debug-mode canary after each arena slab
 
 
 class DAGExecutor:
     def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
                  model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True,
-                 trace: bool = False):
+                 trace: bool = False, debug: bool = False):
         self.tasks = {t.id: t for t in tasks}
         self.prog = program
         self.store = store
@@ -73,6 +74,8 @@ class DAGExecutor:
         self.use_graph = use_graph and self.gpu and not program.has_comm
         self.seed = seed
         self.trace = trace  # roctx range per instruction (eager steps; a graph replay is one range)
+        self.debug = debug  # canary guards after every arena + non-finite check of outputs, per step
+        self._local_consumed = None
         self.dtype = torch.bfloat16
         self._graph = None
         self._views: Dict[str, torch.Tensor] = {}     # activation views (output task -> tensor)
@@ -95,8 +98,14 @@ class DAGExecutor:
     def _setup(self) -> None:
         p = self.prog
         dev = self.device
-        self.act_slab = torch.empty(max(p.act_arena_bytes, 256), dtype=torch.uint8, device=dev)
-        self.param_slab = torch.empty(max(p.param_arena_bytes, 256), dtype=torch.uint8, device=dev)
+        g = GUARD_BYTES if self.debug else 0
+        self._act_full = torch.empty(max(p.act_arena_bytes, 256) + g, dtype=torch.uint8, device=dev)
+        self._param_full = torch.empty(max(p.param_arena_bytes, 256) + g, dtype=torch.uint8, device=dev)
+        self.act_slab = self._act_full[:self._act_full.numel() - g]
+        self.param_slab = self._param_full[:self._param_full.numel() - g]
+        if g:
+            self._act_full[-g:].fill_(GUARD_VALUE)
+            self._param_full[-g:].fill_(GUARD_VALUE)
         for tid, off in p.act_offset.items():
             t = self.tasks[tid]
             shape = tuple(t.op.out_shape) if t.op is not None and t.op.out_shape else (p.act_bytes[tid] // 2,)
@@ -112,7 +121,10 @@ class DAGExecutor:
         for ins in p.instrs:
             if ins.op == "run":
                 ws = max(ws, self._workspace_bytes(ins))
-        self.ws_slab = torch.empty(max(ws, 256), dtype=torch.uint8, device=dev)
+        self._ws_full = torch.empty(max(ws, 256) + g, dtype=torch.uint8, device=dev)
+        self.ws_slab = self._ws_full[:self._ws_full.numel() - g]
+        if g:
+            self._ws_full[-g:].fill_(GUARD_VALUE)
         # external inputs (token ids per request replica)
         for ins in p.instrs:
             if ins.op != "run":
@@ -493,8 +505,40 @@ class DAGExecutor:
                     el = lambda a: (a - t_begin) * 1e3  # noqa: E731
                 stats.events = [(n, c, el(a), el(b)) for n, c, a, b in ev]
                 stats.timeline = [(n, a, b) for n, c, a, b in stats.events if c == "kernel"]
+        if self.debug:
+            self.check_guards()
         self.last = stats
         return stats
+
+    def check_guards(self) -> None:
+        """Debug mode: every arena's trailing canary is intact and the rank's outputs are
+        finite (a kernel writing past its planned region or producing NaN fails loudly)."""
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+        for name, full in (("activation", self._act_full), ("parameter", self._param_full),
+                           ("workspace", self._ws_full)):
+            tail = full[-GUARD_BYTES:]
+            if not bool((tail == GUARD_VALUE).all()):
+                raise RuntimeError(f"rank {self.prog.rank}: {name} arena guard overwritten (out-of-bounds write)")
+        for ins in self.prog.instrs:
+            if ins.op == "run" and not self._consumed_locally(ins.task):
+                v = self._views[ins.task]
+                if not bool(torch.isfinite(v.float()).all()):
+                    raise RuntimeError(f"rank {self.prog.rank}: non-finite values in output of {ins.task}")
+
+    def _consumed_locally(self, tid: str) -> bool:
+        """True if ``tid`` is read by a later group on this rank or sent away (its buffer may
+        legitimately be reused afterwards, so only final outputs are checked)."""
+        if self._local_consumed is None:
+            used = set()
+            for ins in self.prog.instrs:
+                if ins.op == "run":
+                    for t in ins.group:
+                        used.update(self.tasks[t].dependencies)
+                elif ins.op == "send":
+                    used.add(ins.task)
+            self._local_consumed = used
+        return tid in self._local_consumed
 
     def capture(self) -> bool:
         """Capture the steady-state step into a hipGraph (comm-free programs only)."""

@@ -224,8 +224,16 @@ def make_store(p: Plan, seed: int = 0, device_init: bool = False) -> ParamStore:
 
 
 def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None, pg=None, use_graph: bool = True,
-                  trace: bool = False):
+                  trace: bool = False, debug: bool = False):
+    """``debug=True``: validate every rank's program first (parallel/validate.py) and run the
+    executor with arena canaries and output finiteness checks."""
     from .executor import DAGExecutor
 
+    if debug:
+        from .validate import check_plan
+
+        errs = check_plan(p)
+        if errs:
+            raise RuntimeError("invalid plan:\n  " + "\n  ".join(errs[:20]))
     return DAGExecutor(p.tasks, p.programs[rank], store or make_store(p), device, model_cfg=p.cfg,
-                       use_graph=use_graph, pg=pg, trace=trace)
+                       use_graph=use_graph, pg=pg, trace=trace, debug=debug)

@@ -1,0 +1,91 @@
+"""Static program validation (dataflow, residency, p2p pairing, deadlock, arena overlap)."""
+import copy
+
+import pytest
+
+from distributed_llm_scheduler_amd.parallel import runtime
+from distributed_llm_scheduler_amd.parallel.program import Instr
+from distributed_llm_scheduler_amd.parallel.validate import check_plan, validate_programs
+
+CASES = [
+    dict(model="gpt2", world=4, scheduler="MRU_spec", cost_model="reference", cap_gb=8),
+    dict(model="gpt2", world=8, replicas=8),
+    dict(model="llama3-8b", world=8, placement="pipeline", replicas=8),
+    dict(model="mixtral-8x7b", world=8),
+    dict(model="tiny-gpt2", world=2, tp=2, placement="tensor", seq=16),
+    dict(model="gpt2-medium", world=2, cap_gb=0.3),
+    dict(model="tiny-mixtral", world=3, scheduler="MRU_spec", seq=16, cap_gb=0.0002),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(f"{k}={v}" for k, v in c.items()))
+def test_lowered_programs_are_valid(case):
+    p = runtime.plan(**case)
+    assert p.completed == p.total
+    assert check_plan(p) == []
+
+
+@pytest.mark.parametrize("sched", ["DFS", "Greedy", "Critical", "MRU_spec", "EFT", "MRU_paper", "Greedy_chain"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_every_policy_lowers_validly(sched, world):
+    p = runtime.plan("tiny-llama", world=world, scheduler=sched, seq=16, replicas=2, cap_gb=0.0005)
+    assert check_plan(p) == []
+
+
+def _plan2():
+    return runtime.plan("tiny-gpt2", world=2, seq=16, placement="pipeline")
+
+
+def test_detects_missing_parameter_load():
+    p = _plan2()
+    progs = copy.deepcopy(p.programs)
+    i = next(k for k, ins in enumerate(progs[0].instrs) if ins.op == "load")
+    del progs[0].instrs[i]
+    assert any("not resident" in e or "offset" in e for e in validate_programs(p.tasks, progs, p.param_bytes))
+
+
+def test_detects_use_before_produce():
+    p = _plan2()
+    progs = copy.deepcopy(p.programs)
+    runs = [k for k, ins in enumerate(progs[1].instrs) if ins.op == "run"]
+    a, b = runs[0], runs[1]
+    progs[1].instrs[a], progs[1].instrs[b] = progs[1].instrs[b], progs[1].instrs[a]
+    assert any("not available" in e for e in validate_programs(p.tasks, progs, p.param_bytes))
+
+
+def test_detects_unpaired_and_deadlocking_p2p():
+    p = _plan2()
+    progs = copy.deepcopy(p.programs)
+    s = next(k for k, ins in enumerate(progs[0].instrs) if ins.op == "send")
+    snd = progs[0].instrs.pop(s)
+    errs = validate_programs(p.tasks, progs, p.param_bytes)
+    assert any("p2p" in e or "not available" in e for e in errs)
+    # a receive posted before a send both ranks wait on -> deadlock
+    progs = copy.deepcopy(p.programs)
+    progs[0].instrs.insert(0, Instr("recv", task=snd.task, peer=1))
+    progs[1].instrs.append(Instr("send", task=snd.task, peer=0))
+    errs = validate_programs(p.tasks, progs, p.param_bytes)
+    assert errs
+
+
+def test_detects_activation_overlap():
+    p = runtime.plan("tiny-gpt2", world=1, seq=16, fuse=False)
+    progs = copy.deepcopy(p.programs)
+    pr = progs[0]
+    runs = [ins.task for ins in pr.instrs if ins.op == "run"]
+    pr.act_offset[runs[2]] = pr.act_offset[runs[1]]  # clobber a live input
+    assert any("overwrites live activation" in e for e in validate_programs(p.tasks, progs, p.param_bytes))
+
+
+def test_debug_executor_guards_and_validation():
+    p = runtime.plan("tiny-llama", world=1, seq=16)
+    ex = runtime.make_executor(p, 0, "cpu", debug=True)
+    ex.step()  # guards intact, outputs finite
+    ex._act_full[-1] = 0  # simulate an out-of-bounds write past the activation arena
+    with pytest.raises(RuntimeError, match="guard"):
+        ex.step()
+    bad = runtime.plan("tiny-gpt2", world=2, seq=16, placement="pipeline")
+    i = next(k for k, ins in enumerate(bad.programs[0].instrs) if ins.op == "load")
+    del bad.programs[0].instrs[i]
+    with pytest.raises(RuntimeError, match="invalid plan"):
+        runtime.make_executor(bad, 0, "cpu", debug=True)
