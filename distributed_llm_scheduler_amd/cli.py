@@ -9,6 +9,8 @@ Commands (defaults reproduce the reference's settings where one exists, SURVEY Â
             measured step makespan; ``--trace`` writes a Chrome trace, ``--gantt`` a PNG
   simulate  the reference evaluation sweep (raw_results.csv + 2x2 figure)
   extract   the reference GPT-2 DAG (test_gpt2.py semantics) to JSON (test_gpt2.py also pickles it)
+  elastic   run with device-loss injection: a worker dies, the DAG is re-planned onto the
+            surviving devices and the step is re-executed
   models    list the model presets
 
 Common options: --model, --devices (ignored under torchrun: WORLD_SIZE wins), --scheduler,
@@ -158,6 +160,17 @@ def cmd_extract(a) -> int:
     return 0
 
 
+def cmd_elastic(a) -> int:
+    from .parallel.elastic import run_elastic
+
+    out = run_elastic(world=a.devices, steps=a.steps, fail_rank=a.fail_rank, fail_step=a.fail_step,
+                      device=a.device, model=a.model, scheduler=a.scheduler, cap_gb=a.hbm_cap_gb,
+                      replicas=a.replicas, batch=a.batch, seq=a.seq, cost_model=a.cost_model, placement=a.placement,
+                      tp=a.tp)
+    print(json.dumps(out))
+    return 0
+
+
 def cmd_models(a) -> int:
     from .models.config import PRESETS
 
@@ -201,6 +214,13 @@ def main(argv: Optional[List[str]] = None) -> int:
     e.add_argument("--seq", type=int, default=512)
     e.add_argument("--cost-model", choices=["bytes", "reference"], default="reference")
     e.set_defaults(fn=cmd_extract)
+    el = sub.add_parser("elastic", help="run with device-loss injection and re-planning (one process per device)")
+    _common(el)
+    el.add_argument("--device", default="cpu", choices=["cpu", "cuda"])
+    el.add_argument("--steps", type=int, default=2)
+    el.add_argument("--fail-rank", type=int, default=None)
+    el.add_argument("--fail-step", type=int, default=1)
+    el.set_defaults(fn=cmd_elastic)
     m = sub.add_parser("models", help="list model presets")
     m.set_defaults(fn=cmd_models)
     a = ap.parse_args(argv)
