@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -83,13 +84,16 @@ def bench_attn(quick):
         q, k, v = qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:]
         o = torch.empty(B * S, nh * D, device=DEV, dtype=torch.bfloat16)
         ours = timeit(lambda: ops.attention(q, k, v, B, S, nh, nkv, D, True, out=o))
+        sc = 1.0 / math.sqrt(D)
+        var = {f"v{vv}": round(timeit(lambda: ops.ext().attention(q, k, v, B, S, nh, nkv, D, True, sc, o, vv)), 2)
+               for vv in (1, 2, 3, 4)}
         qh = q.reshape(B, S, nh, D).transpose(1, 2).contiguous()
         kh = k.reshape(B, S, nkv, D).transpose(1, 2).repeat_interleave(nh // nkv, 1).contiguous()
         vh = v.reshape(B, S, nkv, D).transpose(1, 2).repeat_interleave(nh // nkv, 1).contiguous()
         ref = timeit(lambda: F.scaled_dot_product_attention(qh, kh, vh, is_causal=True))
         flops = 2.0 * 2 * B * nh * S * S * D / 2
         print(json.dumps({"kind": "attn", "case": label, "ours_us": round(ours, 2), "torch_sdpa_us": round(ref, 2),
-                          "ours_tflops": round(flops / ours / 1e6, 1)}), flush=True)
+                          "ours_tflops": round(flops / ours / 1e6, 1), **var}), flush=True)
 
 
 def bench_norm(quick):
@@ -102,9 +106,15 @@ def bench_norm(quick):
         fused = timeit(lambda: ops.layernorm(x, w, b, residual=r, out=y))
         ref = timeit(lambda: F.layer_norm(x, (H,), w, b))
         gb = 2 * M * H * 2 / 1e9
+        rms = timeit(lambda: ops.rmsnorm(x, w, out=y))
         print(json.dumps({"kind": "layernorm", "M": M, "H": H, "ours_us": round(ours, 2),
-                          "ours_add_ln_us": round(fused, 2), "torch_us": round(ref, 2),
+                          "ours_add_ln_us": round(fused, 2), "ours_rms_us": round(rms, 2), "torch_us": round(ref, 2),
                           "ours_GBps": round(gb / ours * 1e6, 1)}), flush=True)
+    S, nh, nkv, D = 512, 32, 8, 128
+    qkv = torch.randn(S, (nh + 2 * nkv) * D, device=DEV).bfloat16()
+    cos, sin = ops.rope_tables(S, D, 500000.0, DEV)
+    t = timeit(lambda: ops.rope_(qkv, S, nh, nkv, D, nh * D, cos, sin))
+    print(json.dumps({"kind": "rope", "M": S, "heads": nh + nkv, "D": D, "ours_us": round(t, 2)}), flush=True)
 
 
 if __name__ == "__main__":

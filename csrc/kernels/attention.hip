@@ -22,12 +22,16 @@ namespace {
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int D, int NW_>
+template <int D, int NW_, int ST_ = 2>
 struct AttnCfg {
   static constexpr int NW = NW_;                 // waves per block (16 queries each)
+  static constexpr int ST = ST_;                 // K/V stages (ST-1 tiles in flight)
   static constexpr int QB = 16 * NW;             // queries per block
   static constexpr int KT = 64;                  // keys per tile
   static constexpr int RB = D * 2;               // bytes per K/V row
@@ -43,14 +47,14 @@ struct AttnCfg {
 
 __device__ __forceinline__ int swz(int row, int ch_mask) { return row & ch_mask; }
 
-template <int D, int NW>
+template <int D, int NW, int ST>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ Q, int ldq,
                                                        const bf16* __restrict__ Kp, int ldk,
                                                        const bf16* __restrict__ Vp, int ldv, bf16* __restrict__ O,
                                                        int ldo, int S, int n_head, int n_kv_head, float scale_log2,
                                                        int causal, int n_qtiles) {
-  using C = AttnCfg<D, NW>;
-  __shared__ __attribute__((aligned(16))) char smem[2 * C::BUF_BYTES];
+  using C = AttnCfg<D, NW, ST>;
+  __shared__ __attribute__((aligned(16))) char smem[ST * C::BUF_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int qt = causal ? (n_qtiles - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heaviest first
@@ -72,7 +76,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   const int kv_end = causal ? min(S, qt * C::QB + C::QB) : S;
   const int ntiles = (kv_end + C::KT - 1) / C::KT;
   auto issue = [&](int t) {
-    char* buf = smem + (t & 1) * C::BUF_BYTES;
+    char* buf = smem + (t % ST) * C::BUF_BYTES;
 #pragma unroll
     for (int j = 0; j < C::PW; ++j) {
       const int ins = wave * C::PW + j;            // 0 .. 2*INSTR-1
@@ -95,12 +99,16 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   float m_run = -INFINITY, l_run = 0.f;  // for query q0 + li (replicated over the 4 lane groups)
   const int my_q = q0 + li;
 
-  issue(0);
+#pragma unroll
+  for (int p = 0; p < ST - 1; ++p)
+    if (p < ntiles) issue(p);
   for (int t = 0; t < ntiles; ++t) {
-    wait_vm0();
+    // tile t has landed once at most min(ST-2, tiles issued after t) tiles are in flight
+    if (ST == 3 && t + 1 < ntiles) wait_vm<C::PW>();
+    else wait_vm<0>();
     raw_barrier();
-    if (t + 1 < ntiles) issue(t + 1);
-    const char* kb = smem + (t & 1) * C::BUF_BYTES;
+    if (t + ST - 1 < ntiles) issue(t + ST - 1);  // into the buffer everyone finished in t-1
+    const char* kb = smem + (t % ST) * C::BUF_BYTES;
     const char* vb = kb + C::TILE_BYTES;
     const int key0 = t * C::KT;
 
@@ -185,25 +193,33 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 
 }  // namespace
 
-template <int D, int NW>
+template <int D, int NW, int ST>
 static void launch_attn(const AttnArgs& a, hipStream_t s) {
   const int nq = (a.S + 16 * NW - 1) / (16 * NW);
   dim3 grid(nq, a.n_head, a.B), block(64 * NW);
   const float sl2 = a.scale * 1.4426950408889634f;
-  hipLaunchKernelGGL((attn_fwd_kernel<D, NW>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NW, ST>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
                      static_cast<const bf16*>(a.k), a.ldk, static_cast<const bf16*>(a.v), a.ldv,
                      static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq);
 }
 
-void launch_attention_fwd(const AttnArgs& a, hipStream_t s) {
-  // small grids (few heads x short sequences) use 32-query blocks to fill more CUs
-  const long blocks64 = (long)((a.S + 63) / 64) * a.n_head * a.B;
-  const bool small = blocks64 < 512;
-  if (a.D == 64) {
-    if (small) launch_attn<64, 2>(a, s);
-    else launch_attn<64, 4>(a, s);
-  } else {
-    if (small) launch_attn<128, 2>(a, s);
-    else launch_attn<128, 4>(a, s);
+template <int D>
+static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
+  switch (v) {
+    case 1: launch_attn<D, 2, 2>(a, s); break;
+    case 2: launch_attn<D, 4, 2>(a, s); break;
+    case 3: launch_attn<D, 2, 3>(a, s); break;
+    case 4: launch_attn<D, 4, 3>(a, s); break;
+    default: {
+      // small grids (few heads x short sequences) use 32-query blocks to fill more CUs
+      const long blocks64 = (long)((a.S + 63) / 64) * a.n_head * a.B;
+      if (blocks64 < 512) launch_attn<D, 2, 2>(a, s);
+      else launch_attn<D, 4, 2>(a, s);
+    }
   }
+}
+
+void launch_attention_fwd(const AttnArgs& a, hipStream_t s) {
+  if (a.D == 64) launch_variant<64>(a, a.variant, s);
+  else launch_variant<128>(a, a.variant, s);
 }

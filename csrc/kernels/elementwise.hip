@@ -75,24 +75,38 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
 // Rotary embedding (rotate-half convention), in place on the q heads (columns
 // [0, n_head*D)) and k heads (columns [k_col, k_col + n_kv*D)) of each token row.
 // cos/sin tables [S][D/2] fp32 are precomputed on the host (no on-device trig).
+// RoPE (rotate-half) in place on the q and k column ranges of the fused qkv activation:
+// one thread per (token, head, 8 consecutive rotary pairs) -> 16-B loads of both halves and
+// 32-B loads of the cos/sin rows (tables are [S][D/2] fp32).
 __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, int ld, int M, int S, int n_head,
                                                    int n_kv, int D, int k_col, const float* __restrict__ cos_t,
                                                    const float* __restrict__ sin_t) {
-  const int half = D / 2;
+  const int half = D / 2, hv = half / 8;
   const int heads = n_head + n_kv;
-  const int64_t total = (int64_t)M * heads * half;
+  const int64_t total = (int64_t)M * heads * hv;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int j = (int)(i % half);
-    const int64_t t = i / half;
+    const int j = (int)(i % hv) * 8;
+    const int64_t t = i / hv;
     const int hh = (int)(t % heads);
     const int m = (int)(t / heads);
     const int pos = m % S;
     const int col = hh < n_head ? hh * D : k_col + (hh - n_head) * D;
     bf16* base = qkv + (size_t)m * ld + col;
-    const float c = cos_t[pos * half + j], s = sin_t[pos * half + j];
-    const float x1 = bf2f(base[j]), x2 = bf2f(base[j + half]);
-    base[j] = f2bf(x1 * c - x2 * s);
-    base[j + half] = f2bf(x2 * c + x1 * s);
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + j);
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(base + j + half);
+    const f32x4* cp = reinterpret_cast<const f32x4*>(cos_t + (size_t)pos * half + j);
+    const f32x4* sp = reinterpret_cast<const f32x4*>(sin_t + (size_t)pos * half + j);
+    const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+    bf16x8 oa, ob;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float c = e < 4 ? c0[e] : c1[e - 4], sn = e < 4 ? s0[e] : s1[e - 4];
+      const float x1 = bf2f(a[e]), x2 = bf2f(b[e]);
+      oa[e] = f2bf(x1 * c - x2 * sn);
+      ob[e] = f2bf(x2 * c + x1 * sn);
+    }
+    *reinterpret_cast<bf16x8*>(base + j) = oa;
+    *reinterpret_cast<bf16x8*>(base + j + half) = ob;
   }
 }
 
@@ -122,7 +136,7 @@ void launch_embedding(const int32_t* tokens, const void* wte, const void* wpe, v
 
 void launch_rope(void* qkv, int ld, int M, int S, int n_head, int n_kv_head, int D, int k_col, const float* cos_t,
                  const float* sin_t, hipStream_t s) {
-  const int64_t total = (int64_t)M * (n_head + n_kv_head) * (D / 2);
-  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(total / 8 + 1)), dim3(256), 0, s, (bf16*)qkv, ld, M, S, n_head,
+  const int64_t total = (int64_t)M * (n_head + n_kv_head) * (D / 16);
+  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(total)), dim3(256), 0, s, (bf16*)qkv, ld, M, S, n_head,
                      n_kv_head, D, k_col, cos_t, sin_t);
 }

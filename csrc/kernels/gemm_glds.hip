@@ -39,39 +39,95 @@ __device__ __forceinline__ void wait_tiles(int ahead) {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0>
+// BXS = extra weight (B) stages: 0 -> A and W tiles share STAGES buffers and travel
+// together; 1 -> A keeps STAGES buffers (it is L2-resident: short latency) while the COLD
+// weight stream gets STAGES + 1, i.e. one more tile of HBM latency covered inside the same
+// 160 KiB of LDS (e.g. 256x256: 2 x 32 KiB A + 3 x 32 KiB W).
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_, BXS = BXS_;
   static constexpr int BK = 64, CH = 8;
   static constexpr int NW = WM * WN, T = 64 * NW;
   static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
   static constexpr int ROWS = BM + BN, INSTR = ROWS / 8, PW = INSTR / NW;
   static constexpr int STAGE = ROWS * CH;  // bf16x8 units
+  // split staging (BXS > 0): separate A / W rings
+  static constexpr int SA = STAGES, SB = STAGES + BXS;
+  static constexpr int PWA = BM / 8 / NW, PWB = BN / 8 / NW;
+  static constexpr int A_STAGE = BM * CH, B_STAGE = BN * CH;
+  static constexpr int LDS_UNITS = BXS ? SA * A_STAGE + SB * B_STAGE : STAGES * STAGE;
   static_assert(INSTR % NW == 0, "stage rows must split evenly over waves");
+  static_assert(!BXS || ((BM / 8) % NW == 0 && (BN / 8) % NW == 0), "split rings: rows must split over waves");
   static_assert(FM >= 1 && FN >= 1, "wave tile too small");
   static_assert(PW * (STAGES - 2) <= 63, "vmcnt range");
   static_assert(STAGES >= 2 && STAGES <= 8, "stages");
+  static_assert(LDS_UNITS * 16 <= 163840, "LDS budget");
 };
 
-// One output tile (tm, tn) over K-slice ks. Everything from here to the end of the epilogue
-// is per tile; the kernel below maps blocks to tiles (or loops over a device-side row range).
-template <class C>
-__device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
-                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
-                                          const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
-                                          float* __restrict__ part, int M, int Mmax, int N, int K, int act,
-                                          float alpha, int ks, int kslice, int tm, int tn,
-                                          const float* __restrict__ ln_colsum, int ln_mode, float ln_eps) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / C::WN, wn = wave % C::WN;
-  const int m0 = tm * C::BM, n0 = tn * C::BN;
-  if (m0 >= M) return;  // whole block idle (uniform: before any barrier)
-  const int kbeg = ks * kslice;
-  const int nk = kslice / C::BK;
+// split rings: wait until at most a*PWA + b*PWB DMA instructions are outstanding, with
+// a in [0, AMAX] and b in {a, a + 1} (see the issue order in glds_tile)
+template <int PWA, int PWB, int A>
+__device__ __forceinline__ void wait_ab(int a, int b) {
+  if constexpr (A == 0) {
+    if (b >= 1) wait_vm<PWB>();
+    else wait_vm<0>();
+  } else {
+    if (a >= A) {
+      if (b > A) wait_vm<A * PWA + (A + 1) * PWB>();
+      else wait_vm<A * PWA + A * PWB>();
+    } else {
+      wait_ab<PWA, PWB, A - 1>(a, b);
+    }
+  }
+}
 
-  // per-lane DMA source rows (fixed over the K loop): instruction j of this wave covers
-  // stage rows 8*(wave*PW + j) .. +7; lane -> row +lane/8, LDS chunk position lane%8,
-  // global chunk (lane%8) ^ (row & 7). Rows past M/N are clamped (results discarded).
+// MFMAs of one staged K-tile: A rows at sA[row * CH], W rows at sB[row * CH] (both XOR
+// swizzled by row & 7, see the DMA source addresses).
+template <class C>
+__device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int lane, int wm, int wn, bool ln_acc,
+                                         f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM], float (&st_q)[C::FM]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const int chunk = kk * 4 + (lane >> 4);
+    bf16x8 af[C::FM], bw[C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const int row = wm * C::WTM + i * 16 + (lane & 15);
+      af[i] = sA[row * C::CH + (chunk ^ (row & 7))];
+    }
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+      const int row = wn * C::WTN + j * 16 + (lane & 15);
+      bw[j] = sB[row * C::CH + (chunk ^ (row & 7))];
+    }
+    if (ln_acc) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = bf2f(af[i][e]);
+          st_s[i] += x;
+          st_q[i] += x * x;
+        }
+    }
+    // swapped operands: acc = (W A^T) tile, i.e. C^T — lane holds 4 consecutive output
+    // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
+    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[j], af[i], acc[i][j]);
+    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+// Joint rings (BXS == 0): A and W rows of a K-tile share one stage and one DMA batch.
+template <class C>
+__device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restrict__ A, int lda,
+                                               const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
+                                               int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
+                                               f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
+                                               float (&st_q)[C::FM]) {
   const bf16* src[C::PW];
 #pragma unroll
   for (int j = 0; j < C::PW; ++j) {
@@ -94,6 +150,95 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
                                        16, 0, 0);
     }
   };
+#pragma unroll
+  for (int s = 0; s < C::STAGES - 1; ++s)
+    if (s < nk) issue(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(C::STAGES - 2, nk - 1 - kt);  // tiles issued after kt, still allowed in flight
+    wait_tiles<C::PW, C::STAGES - 2>(ahead);
+    raw_barrier();
+    if (kt + C::STAGES - 1 < nk) issue(kt + C::STAGES - 1);
+    const bf16x8* st = smem + (kt % C::STAGES) * C::STAGE;
+    mma_tile<C>(st, st + C::BM * C::CH, lane, wm, wn, ln_acc, acc, st_s, st_q);
+  }
+}
+
+// Split rings (BXS > 0): issue order B0 [A0 B1] [A1 B2] ... — iteration t issues
+// A(t + SA - 1) then B(t + SB - 1). Waiting for A(t) then leaves a = min(SA-2, nk-1-t)
+// later A tiles and b = min(a + 1, nk-1-t) later W tiles in flight (B(t) precedes A(t)).
+template <class C>
+__device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restrict__ A, int lda,
+                                               const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
+                                               int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
+                                               f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
+                                               float (&st_q)[C::FM]) {
+  static_assert(C::SB == C::SA + 1, "split rings: W ring is one deeper than A");
+  const bf16* srcA[C::PWA];
+  const bf16* srcB[C::PWB];
+#pragma unroll
+  for (int j = 0; j < C::PWA; ++j) {
+    const int row = 8 * (wave * C::PWA + j) + (lane >> 3);
+    const int gm = min(m0 + row, M - 1);
+    srcA[j] = A + (size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < C::PWB; ++j) {
+    const int row = 8 * (wave * C::PWB + j) + (lane >> 3);
+    const int gn = min(n0 + row, N - 1);
+    srcB[j] = W + (size_t)gn * ldw + kbeg + ((lane & 7) ^ (row & 7)) * 8;
+  }
+  bf16x8* ringA = smem;
+  bf16x8* ringB = smem + C::SA * C::A_STAGE;
+  auto issueA = [&](int kt) {
+    bf16x8* st = ringA + (kt % C::SA) * C::A_STAGE;
+#pragma unroll
+    for (int j = 0; j < C::PWA; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * C::BK),
+                                       (__attribute__((address_space(3))) void*)(st + (wave * C::PWA + j) * 64), 16,
+                                       0, 0);
+  };
+  auto issueB = [&](int kt) {
+    bf16x8* st = ringB + (kt % C::SB) * C::B_STAGE;
+#pragma unroll
+    for (int j = 0; j < C::PWB; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + kt * C::BK),
+                                       (__attribute__((address_space(3))) void*)(st + (wave * C::PWB + j) * 64), 16,
+                                       0, 0);
+  };
+  constexpr int DA = C::SA - 1;
+  issueB(0);
+#pragma unroll
+  for (int s = 0; s < DA; ++s) {
+    if (s < nk) issueA(s);
+    if (s + 1 < nk) issueB(s + 1);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int a = min(DA - 1, nk - 1 - kt);
+    const int b = min(a + 1, nk - 1 - kt);
+    wait_ab<C::PWA, C::PWB, DA - 1>(a, b);
+    raw_barrier();
+    if (kt + DA < nk) issueA(kt + DA);
+    if (kt + DA + 1 < nk) issueB(kt + DA + 1);
+    mma_tile<C>(ringA + (kt % C::SA) * C::A_STAGE, ringB + (kt % C::SB) * C::B_STAGE, lane, wm, wn, ln_acc, acc,
+                st_s, st_q);
+  }
+}
+
+// One output tile (tm, tn) over K-slice ks. Everything from here to the end of the epilogue
+// is per tile; the kernel below maps blocks to tiles (or loops over a device-side row range).
+template <class C>
+__device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
+                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
+                                          const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
+                                          float* __restrict__ part, int M, int Mmax, int N, int K, int act,
+                                          float alpha, int ks, int kslice, int tm, int tn,
+                                          const float* __restrict__ ln_colsum, int ln_mode, float ln_eps) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int m0 = tm * C::BM, n0 = tn * C::BN;
+  if (m0 >= M) return;  // whole block idle (uniform: before any barrier)
+  const int kbeg = ks * kslice;
+  const int nk = kslice / C::BK;
 
   f32x4 acc[C::FM][C::FN];
 #pragma unroll
@@ -106,51 +251,10 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   float st_s[C::FM], st_q[C::FM];
 #pragma unroll
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
-
-#pragma unroll
-  for (int s = 0; s < C::STAGES - 1; ++s)
-    if (s < nk) issue(s);
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(C::STAGES - 2, nk - 1 - kt);  // tiles issued after kt, still allowed in flight
-    wait_tiles<C::PW, C::STAGES - 2>(ahead);
-    raw_barrier();
-    if (kt + C::STAGES - 1 < nk) issue(kt + C::STAGES - 1);
-    const bf16x8* s = smem + (kt % C::STAGES) * C::STAGE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-      bf16x8 af[C::FM], bw[C::FN];
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int row = wm * C::WTM + i * 16 + (lane & 15);
-        af[i] = s[row * C::CH + (chunk ^ (row & 7))];
-      }
-#pragma unroll
-      for (int j = 0; j < C::FN; ++j) {
-        const int row = C::BM + wn * C::WTN + j * 16 + (lane & 15);
-        bw[j] = s[row * C::CH + (chunk ^ (row & 7))];
-      }
-      if (ln_acc) {
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float x = bf2f(af[i][e]);
-            st_s[i] += x;
-            st_q[i] += x * x;
-          }
-      }
-      // swapped operands: acc = (W A^T) tile, i.e. C^T — lane holds 4 consecutive output
-      // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
-      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[j], af[i], acc[i][j]);
-      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
-    }
-  }
+  if constexpr (C::BXS > 0)
+    mainloop_split<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc, st_s, st_q);
+  else
+    mainloop_joint<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc, st_s, st_q);
 
   // epilogue: lane (g = lane>>4, r = lane&15) of fragment (i, j) holds C[row][col..col+3]
   // with row = m0 + wm*WTM + 16i + r, col = n0 + wn*WTN + 16j + 4g
@@ -320,7 +424,9 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   }
 }
 
-template <class C>
+// LN / RANGED are compile-time switches: a kernel instance carries only the epilogue and
+// tile walk it needs (the folded-norm statistics and the row-range loop cost registers).
+template <class C, int LN, int RANGED>
 __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
                                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
                                                          int ldc, const bf16* __restrict__ bias,
@@ -329,14 +435,14 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
                                                          float alpha, int tiles_m, int tiles_n, int splitk,
                                                          int kslice, const float* __restrict__ ln_colsum,
                                                          int ln_mode, float ln_eps, const int* __restrict__ rows) {
-  __shared__ bf16x8 smem[C::STAGES * C::STAGE];
+  __shared__ bf16x8 smem[C::LDS_UNITS];
   const int ntile = tiles_m * tiles_n;
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
   const int ks = bid / ntile, tile = bid % ntile;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
-  if (rows == nullptr) {
+  if constexpr (!RANGED) {
     glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn,
-                 ln_colsum, ln_mode, ln_eps);
+                 ln_colsum, LN ? ln_mode : 0, ln_eps);
     return;
   }
   // device-side row range (MoE expert): the host launched ONE tile row (tiles_m == 1) — no
@@ -349,7 +455,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   for (int t = 0; t * C::BM < Mr; ++t) {
     if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
     glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, Mr, M, N, K, act, alpha, ks, kslice, t, tn,
-                 ln_colsum, ln_mode, ln_eps);
+                 ln_colsum, 0, ln_eps);
   }
 }
 
@@ -418,13 +524,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 template <class C>
 void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
             float ln_eps, const int* rows) {
-  static_assert(2 * C::BM * sizeof(float) <= C::STAGES * C::STAGE * 16, "LN stats must fit the staging LDS");
+  static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
   const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;
   dim3 grid(tiles_m * tiles_n * splitk), block(C::T);
-  hipLaunchKernelGGL((gemm_glds_kernel<C>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, a.ldw,
-                     (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act,
-                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows);
+#define DLS_K(LN_, RG_)                                                                                           \
+  hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
+                     a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
+                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows)
+  if (rows) DLS_K(0, 1);
+  else if (ln_mode != 0) {
+    if constexpr (C::BM * C::BN <= 256 * 128) DLS_K(1, 0);  // 256x256 tiles have no registers left for it
+  } else DLS_K(0, 0);
+#undef DLS_K
   if (splitk > 1) {
     const int64_t nvec = (int64_t)a.M * (a.N / 8);
     const int g = (int)std::min<int64_t>(2048, (nvec + 255) / 256);
@@ -445,13 +557,19 @@ using C8 = Cfg<256, 256, 2, 4, 2>;     // 8 waves, 128x64 per wave, 2 x 64 KiB s
 using C9 = Cfg<256, 256, 2, 4, 2, 1>;  // same with s_setprio(1) around the MFMA cluster (T5)
 using C10 = Cfg<256, 128, 4, 2, 3, 1>; // C0 with s_setprio
 using C11 = Cfg<128, 128, 2, 2, 4, 1>; // C7 with s_setprio
+// split rings: the cold weight stream one tile deeper than the L2-resident activations
+using C12 = Cfg<256, 256, 2, 4, 2, 0, 1>;  // 2 x 32 KiB A + 3 x 32 KiB W = 160 KiB
+using C13 = Cfg<256, 256, 2, 4, 2, 1, 1>;
+using C14 = Cfg<256, 128, 4, 2, 3, 0, 1>;  // 3 x 32 KiB A + 4 x 16 KiB W = 160 KiB
+using C15 = Cfg<128, 128, 2, 2, 3, 0, 1>;  // 3 x 16 KiB A + 4 x 16 KiB W
 
 struct Shape {
   int bm, bn;
 };
-constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64}, {64, 64},  {64, 128}, {64, 64},
-                             {128, 64},  {128, 128}, {256, 256}, {256, 256}, {256, 128}, {128, 128}};
-constexpr int kNumCfg = 12;
+constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64, 128},  {64, 64},
+                             {128, 64},  {128, 128}, {256, 256}, {256, 256}, {256, 128}, {128, 128},
+                             {256, 256}, {256, 256}, {256, 128}, {128, 128}};
+constexpr int kNumCfg = 16;
 
 }  // namespace
 
@@ -487,7 +605,10 @@ size_t gemm_glds_workspace_bytes(int M, int N, int splitk) { return splitk > 1 ?
 void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s, const float* ln_colsum,
                       int ln_mode, float ln_eps, const int* rows) {
   float* ws = static_cast<float*>(workspace);
-  if (ln_mode != 0) splitk = 1;  // row statistics need the whole K range in one block
+  if (ln_mode != 0) {
+    splitk = 1;  // row statistics need the whole K range in one block
+    if (kShapes[cfg < kNumCfg ? cfg : 3].bm * kShapes[cfg < kNumCfg ? cfg : 3].bn > 256 * 128) cfg = 0;
+  }
 #define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows)
   switch (cfg) {
     case 0: DLS_L(C0); break;
@@ -501,6 +622,10 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
     case 9: DLS_L(C9); break;
     case 10: DLS_L(C10); break;
     case 11: DLS_L(C11); break;
+    case 12: DLS_L(C12); break;
+    case 13: DLS_L(C13); break;
+    case 14: DLS_L(C14); break;
+    case 15: DLS_L(C15); break;
     default: DLS_L(C3); break;
   }
 #undef DLS_L

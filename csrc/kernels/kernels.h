@@ -46,6 +46,7 @@ struct AttnArgs {
   int B, S, n_head, n_kv_head, D;
   float scale;
   int causal;
+  int variant = 0;  // 0 auto; 1..4 = (waves, K/V stages) (2,2) (4,2) (2,3) (4,3) — benchmarks/tuning
 };
 void launch_attention_fwd(const AttnArgs& a, hipStream_t s);
 

@@ -123,7 +123,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
 
 at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
                      int64_t n_head, int64_t n_kv_head, int64_t head_dim, bool causal, double scale,
-                     const c10::optional<at::Tensor>& out) {
+                     const c10::optional<at::Tensor>& out, int64_t variant) {
   for (auto* p : {&q, &k, &v}) {
     check_bf16(*p, "qkv");
     check_rows(*p, "qkv");
@@ -138,7 +138,7 @@ at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor&
   check_rows(o, "out");
   AttnArgs a{q.data_ptr(), (int)q.stride(0), k.data_ptr(), (int)k.stride(0), v.data_ptr(), (int)v.stride(0),
              o.data_ptr(), (int)o.stride(0), (int)B, (int)S, (int)n_head, (int)n_kv_head, (int)head_dim,
-             (float)scale, causal ? 1 : 0};
+             (float)scale, causal ? 1 : 0, (int)variant};
   launch_attention_fwd(a, cur_stream());
   return o;
 }
@@ -235,6 +235,9 @@ void rope_(at::Tensor& qkv, int64_t S, int64_t n_head, int64_t n_kv_head, int64_
                   sin_t.is_contiguous() && cos_t.numel() >= S * head_dim / 2,
               "cos/sin tables must be contiguous fp32 [S][D/2]");
   TORCH_CHECK(k_col + n_kv_head * head_dim <= qkv.size(1) && n_head * head_dim <= qkv.size(1), "head layout");
+  TORCH_CHECK(head_dim % 16 == 0 && k_col % 8 == 0 && qkv.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 16 == 0,
+              "vectorised RoPE needs head_dim % 16 == 0 and 16-B aligned rows / k columns");
   launch_rope(qkv.data_ptr(), (int)qkv.stride(0), (int)qkv.size(0), (int)S, (int)n_head, (int)n_kv_head,
               (int)head_dim, (int)k_col, cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), cur_stream());
 }
@@ -325,7 +328,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("attention", &attention, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"),
         py::arg("n_head"), py::arg("n_kv_head"), py::arg("head_dim"), py::arg("causal") = true,
-        py::arg("scale") = 0.125, py::arg("out") = py::none());
+        py::arg("scale") = 0.125, py::arg("out") = py::none(), py::arg("variant") = 0);
   m.def("norm", &norm, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5,
         py::arg("residual") = py::none(), py::arg("rms") = false, py::arg("out") = py::none(),
         py::arg("sum_out") = py::none());

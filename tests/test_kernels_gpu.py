@@ -43,7 +43,8 @@ def test_gemm_identity_asymmetric():
 @pytest.mark.parametrize("M,N,K", [(512, 2304, 768), (512, 768, 3072), (512, 3072, 768), (77, 130, 200),
                                    (512, 50257, 768), (1, 64, 64), (1024, 1024, 1024)])
 @pytest.mark.parametrize("config,splitk", [(-1, 0), (100, 1), (103, 1), (0, 1), (1, 1), (2, 1), (3, 1), (4, 1),
-                                           (3, 2), (3, 4), (2, 3), (8, 1), (9, 1), (10, 1), (11, 1), (8, 2)])
+                                           (3, 2), (3, 4), (2, 3), (8, 1), (9, 1), (10, 1), (11, 1), (8, 2),
+                                           (12, 1), (13, 1), (14, 1), (15, 1), (12, 2), (14, 4)])
 def test_gemm_shapes(M, N, K, config, splitk):
     x = _rand(M, K, seed=1)
     w = _rand(N, K, scale=0.05, seed=2)
@@ -76,10 +77,11 @@ def test_gemm_epilogue(act):
 @pytest.mark.parametrize("B,S,nh,nkv,D,causal", [(1, 512, 12, 12, 64, True), (2, 200, 4, 4, 64, True),
                                                   (1, 256, 8, 2, 128, True), (1, 130, 4, 4, 64, False),
                                                   (1, 64, 32, 8, 128, True)])
-def test_attention(B, S, nh, nkv, D, causal):
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_attention(B, S, nh, nkv, D, causal, variant):
     qkv = _rand(B * S, (nh + 2 * nkv) * D, seed=7)
     q, k, v = qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:]
-    o = ops.attention(q, k, v, B, S, nh, nkv, D, causal=causal)
+    o = ops.ext().attention(q, k, v, B, S, nh, nkv, D, causal, 1.0 / math.sqrt(D), None, variant)
     ref = ops.ref_attention(q.cpu(), k.cpu(), v.cpu(), B, S, nh, nkv, D, causal=causal)
     _close(o.cpu(), ref, 2e-2)
 
@@ -95,7 +97,7 @@ def test_attention_spike_forces_rescale():
     _close(o.cpu(), ref, 3e-2)
 
 
-@pytest.mark.parametrize("H", [768, 1024, 4096, 64])
+@pytest.mark.parametrize("H", [64, 768, 1024, 2048, 4096, 5120, 8192])
 def test_layernorm_and_residual(H):
     x, r = _rand(300, H, seed=9), _rand(300, H, seed=10)
     w, b = (1 + 0.1 * _rand(H, seed=11).float()).to(torch.bfloat16), _rand(H, scale=0.1, seed=12)
@@ -107,9 +109,15 @@ def test_layernorm_and_residual(H):
     _close(y2.cpu(), ops.ref_layernorm(s_ref, w.cpu(), b.cpu()), 2e-2)
 
 
-def test_rmsnorm():
-    x, w = _rand(100, 4096, seed=13), (1 + 0.1 * _rand(4096, seed=14).float()).to(torch.bfloat16)
+@pytest.mark.parametrize("M,H", [(100, 4096), (301, 4096), (7, 768), (513, 8192), (3, 2048)])
+def test_rmsnorm(M, H):
+    x, w = _rand(M, H, seed=13), (1 + 0.1 * _rand(H, seed=14).float()).to(torch.bfloat16)
     _close(ops.rmsnorm(x, w).cpu(), ops.ref_rmsnorm(x.cpu(), w.cpu()), 2e-2)
+    r = _rand(M, H, seed=15)
+    y, s = ops.rmsnorm(x, w, residual=r)
+    s_ref = (x.cpu().float() + r.cpu().float()).to(torch.bfloat16)
+    assert torch.equal(s.cpu(), s_ref)
+    _close(y.cpu(), ops.ref_rmsnorm(s_ref, w.cpu()), 2e-2)
 
 
 def test_elementwise():
@@ -130,8 +138,9 @@ def test_embedding():
     _close(y.cpu(), ref, 1e-2)
 
 
-def test_rope():
-    S, nh, nkv, D = 64, 4, 2, 128
+@pytest.mark.parametrize("D", [64, 128])
+def test_rope(D):
+    S, nh, nkv = 64, 4, 2
     qkv = _rand(2 * S, (nh + 2 * nkv) * D, seed=20)
     cos, sin = ops.rope_tables(S, D, 10000.0, DEV)
     ref = ops.ref_rope_(qkv.cpu().clone(), S, nh, nkv, D, nh * D, cos.cpu(), sin.cpu())
@@ -163,7 +172,8 @@ def test_moe_pipeline():
 
 
 @pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
-@pytest.mark.parametrize("M,N,K,cfg", [(512, 2304, 768, -1), (300, 1024, 4096, 0), (512, 3072, 768, 2)])
+@pytest.mark.parametrize("M,N,K,cfg", [(512, 2304, 768, -1), (300, 1024, 4096, 0), (512, 3072, 768, 2),
+                                       (512, 1024, 1024, 8), (256, 512, 768, 14)])
 def test_gemm_with_folded_norm(mode, M, N, K, cfg):
     x = _rand(M, K, scale=2.0, seed=40) + 0.5  # non-zero mean rows exercise the mean correction
     w = _rand(N, K, scale=0.03, seed=41)
@@ -179,6 +189,8 @@ def test_gemm_with_folded_norm(mode, M, N, K, cfg):
     wd, cs, bd = ops.derive_norm_gemm(w, nw, nb, bias)
     y = ops.linear_norm(x, wd, cs, bd, mode, act="gelu", residual=res)
     _close(y.cpu(), ref, 3e-2)
+    y2 = ops.ext().gemm(x, wd, bd, res, 1, 1.0, None, cfg, 1, cs, 1 if mode == "layernorm" else 2, 1e-5)
+    _close(y2.cpu(), ref, 3e-2)
 
 
 def _ref_swiglu(x, w13, bias=None):
@@ -189,7 +201,8 @@ def _ref_swiglu(x, w13, bias=None):
     return torch.nn.functional.silu(y[:, :F]) * y[:, F:]
 
 
-@pytest.mark.parametrize("config,splitk", [(-1, 0), (0, 1), (3, 1), (3, 4), (8, 1), (7, 2), (2, 1)])
+@pytest.mark.parametrize("config,splitk", [(-1, 0), (0, 1), (3, 1), (3, 4), (8, 1), (7, 2), (2, 1), (12, 1),
+                                           (14, 2), (15, 1)])
 @pytest.mark.parametrize("M,F,K", [(512, 1024, 768), (200, 512, 1024), (64, 96, 128)])
 def test_gemm_swiglu_epilogue(M, F, K, config, splitk):
     if K % (64 * max(splitk, 1)):
@@ -209,7 +222,7 @@ def test_gemm_swiglu_epilogue(M, F, K, config, splitk):
 
 
 @pytest.mark.parametrize("act", [None, "swiglu"])
-@pytest.mark.parametrize("config,splitk", [(-1, 0), (3, 1), (7, 1), (3, 4), (0, 2)])
+@pytest.mark.parametrize("config,splitk", [(-1, 0), (3, 1), (7, 1), (3, 4), (0, 2), (12, 1), (15, 2)])
 @pytest.mark.parametrize("r0,r1", [(100, 229), (0, 512), (300, 300), (448, 512)])
 def test_gemm_row_range(act, config, splitk, r0, r1):
     M, N, K = 512, 1024, 1024
