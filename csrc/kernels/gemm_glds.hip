@@ -86,26 +86,33 @@ __device__ __forceinline__ void wait_ab(int a, int b) {
 template <class C>
 __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int lane, int wm, int wn, bool ln_acc,
                                          f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM], float (&st_q)[C::FM]) {
+  // All fragments of the K-tile (both 32-deep halves) are requested before the first MFMA:
+  // the second half's ds_reads then complete under the first half's MFMAs instead of
+  // behind an lgkmcnt(0) (the compiler counts lgkmcnt per consumer).
+  bf16x8 af[2][C::FM], bw[2][C::FN];
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     const int chunk = kk * 4 + (lane >> 4);
-    bf16x8 af[C::FM], bw[C::FN];
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      const int row = wm * C::WTM + i * 16 + (lane & 15);
-      af[i] = sA[row * C::CH + (chunk ^ (row & 7))];
-    }
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
       const int row = wn * C::WTN + j * 16 + (lane & 15);
-      bw[j] = sB[row * C::CH + (chunk ^ (row & 7))];
+      bw[kk][j] = sB[row * C::CH + (chunk ^ (row & 7))];
     }
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const int row = wm * C::WTM + i * 16 + (lane & 15);
+      af[kk][i] = sA[row * C::CH + (chunk ^ (row & 7))];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep every ds_read ahead of the MFMAs (counted lgkmcnt waits)
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
     if (ln_acc) {
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float x = bf2f(af[i][e]);
+          const float x = bf2f(af[kk][i][e]);
           st_s[i] += x;
           st_q[i] += x * x;
         }
@@ -116,7 +123,7 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
 #pragma unroll
     for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[j], af[i], acc[i][j]);
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[kk][j], af[kk][i], acc[i][j]);
     if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
   }
 }
