@@ -441,7 +441,8 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
                                                          float* __restrict__ part, int M, int N, int K, int act,
                                                          float alpha, int tiles_m, int tiles_n, int splitk,
                                                          int kslice, const float* __restrict__ ln_colsum,
-                                                         int ln_mode, float ln_eps, const int* __restrict__ rows) {
+                                                         int ln_mode, float ln_eps, const int* __restrict__ rows,
+                                                         int compact_rows) {
   __shared__ bf16x8 smem[C::LDS_UNITS];
   const int ntile = tiles_m * tiles_n;
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
@@ -454,9 +455,9 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   }
   // device-side row range (MoE expert): the host launched ONE tile row (tiles_m == 1) — no
   // idle blocks holding CUs — and each block walks the range's M tiles of its column panel
-  const int r0 = rows[0], Mr = rows[1] - r0;
+  const int r0 = rows[0], Mr = compact_rows ? min(rows[1] - r0, compact_rows) : rows[1] - r0;
   A += (size_t)r0 * lda;
-  Cp += (size_t)r0 * ldc;
+  if (!compact_rows) Cp += (size_t)r0 * ldc;
   if (R) R += (size_t)r0 * ldr;
   if (part) part += (size_t)r0 * N;
   for (int t = 0; t * C::BM < Mr; ++t) {
@@ -473,12 +474,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                             bf16* __restrict__ C, int ldc,
                                                             const bf16* __restrict__ bias,
                                                             const bf16* __restrict__ R, int ldr, int act,
-                                                            float alpha, const int* __restrict__ rows) {
+                                                            float alpha, const int* __restrict__ rows,
+                                                            int compact_rows) {
   const size_t slab = (size_t)M * N;
   int r0 = 0, nrows = M;
   if (rows != nullptr) {
     r0 = rows[0];
     nrows = rows[1] - r0;
+    if (compact_rows) nrows = min(nrows, compact_rows);
   }
   const bool sw = act == ACT_SWIGLU;
   const int NO = sw ? N / 2 : N;
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         o[e] = f2bf(x);
       }
     }
-    *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + c) = o;
+    *reinterpret_cast<bf16x8*>(C + (size_t)(compact_rows ? m - r0 : m) * ldc + c) = o;
   }
 }
 
@@ -538,7 +541,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
 #define DLS_K(LN_, RG_)                                                                                           \
   hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
                      a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
-                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows)
+                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows)
   if (rows) DLS_K(0, 1);
   else if (ln_mode != 0) {
     if constexpr (C::BM * C::BN <= 256 * 128) DLS_K(1, 0);  // 256x256 tiles have no registers left for it
@@ -548,7 +551,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     const int64_t nvec = (int64_t)a.M * (a.N / 8);
     const int g = (int)std::min<int64_t>(2048, (nvec + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, ws, splitk, a.M, a.N, (bf16*)a.C, a.ldc,
-                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows);
+                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows, a.compact_rows);
   }
 }
 

@@ -21,6 +21,8 @@ struct GemmArgs {
   int act;       // DlsAct
   float alpha;
   int config;    // -1 = auto
+  int compact_rows = 0;  // > 0 with a device row range [r0, r1): write output rows 0..r1-r0-1 (not r0..),
+                         // and at most compact_rows of them (the output's row capacity)
 };
 
 int gemm_pick_config(int M, int N, int K);
@@ -76,3 +78,9 @@ void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const fl
 // X [rows][K] sorted by expert, offsets [E+1], W [E][N][K] -> Y [rows][N]
 void launch_grouped_gemm(const void* X, const int32_t* offsets, const void* W, void* Y, int E, int N, int K,
                          int max_rows, int act, hipStream_t s);
+
+// y[m] = r[m] + sum_j w[m,j] * expert_{idx[m,j]}[slot[m,j] - off[idx[m,j]]] over compact per-expert
+// outputs whose base addresses are the device array eo_ptrs[E]; topk <= 8
+void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t* idx, const int32_t* slot_of,
+                               const int32_t* off, const float* w, const void* r, void* y, int M, int topk, int H,
+                               int E, hipStream_t s);

@@ -124,7 +124,60 @@ __global__ __launch_bounds__(256) void combine_kernel(const bf16* __restrict__ e
   }
 }
 
+// y[m] = r[m] + sum_j w[m,j] * E_{e}[slot[m,j] - off[e]],  e = idx[m,j]
+// Expert outputs are COMPACT: expert e's node wrote its routed rows (expert-sorted order)
+// to rows 0..count_e-1 of its own [M][H] buffer, wherever that buffer lives (a local arena
+// view or an xGMI receive buffer). One wave per token row, 16-B chunks per lane.
+__global__ __launch_bounds__(256) void gather_combine_kernel(const unsigned long long* __restrict__ eo_ptrs,
+                                                             const int32_t* __restrict__ idx,
+                                                             const int32_t* __restrict__ slot_of,
+                                                             const int32_t* __restrict__ off,
+                                                             const float* __restrict__ w, const bf16* __restrict__ r,
+                                                             bf16* __restrict__ y, int M, int topk, int H, int E) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const bf16x8* src[8];
+  float g[8];
+  const int kk = topk < 8 ? topk : 8;
+  for (int j = 0; j < kk; ++j) {
+    const int e = idx[m * topk + j];
+    const int row = slot_of[m * topk + j] - off[e];
+    src[j] = (e >= 0 && e < E) ? reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(eo_ptrs[e]) +
+                                                                   (size_t)row * H)
+                               : nullptr;
+    g[j] = w[m * topk + j];
+  }
+  bf16x8* yo = reinterpret_cast<bf16x8*>(y + (size_t)m * H);
+  const bf16x8* ro = r ? reinterpret_cast<const bf16x8*>(r + (size_t)m * H) : nullptr;
+  for (int c = lane; c < H / 8; c += 64) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ro) {
+      const bf16x8 v = ro[c];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = bf2f(v[e]);
+    }
+    for (int j = 0; j < kk; ++j) {
+      if (!src[j]) continue;
+      const bf16x8 v = src[j][c];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += g[j] * bf2f(v[e]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
+    yo[c] = o;
+  }
+}
+
 }  // namespace
+
+void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t* idx, const int32_t* slot_of,
+                               const int32_t* off, const float* w, const void* r, void* y, int M, int topk, int H,
+                               int E, hipStream_t s) {
+  hipLaunchKernelGGL(gather_combine_kernel, dim3((M + 3) / 4), dim3(256), 0, s, eo_ptrs, idx, slot_of, off, w,
+                     (const bf16*)r, (bf16*)y, M, topk, H, E);
+}
 
 void launch_moe_router(const void* logits, int M, int E, int topk, int32_t* topk_idx, float* topk_w,
                        hipStream_t s) {

@@ -39,7 +39,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                 const c10::optional<at::Tensor>& residual, int64_t act, double alpha,
                 const c10::optional<at::Tensor>& out, int64_t config, int64_t splitk,
                 const c10::optional<at::Tensor>& ln_colsum, int64_t ln_mode, double ln_eps,
-                const c10::optional<at::Tensor>& rows) {
+                const c10::optional<at::Tensor>& rows, bool compact_rows) {
   check_bf16(a_in, "A");
   check_bf16(w, "W");
   at::Tensor a = as2d(a_in);
@@ -56,7 +56,8 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   if (out.has_value()) {
     c = as2d(*out);
     check_bf16(c, "out");
-    TORCH_CHECK(c.size(0) == M && c.size(1) == NO && c.stride(1) == 1, "out must be [M][N_out]");
+    TORCH_CHECK((c.size(0) == M || (compact_rows && c.size(0) <= M)) && c.size(1) == NO && c.stride(1) == 1,
+                "out must be [M][N_out] (or fewer rows with compact_rows)");
   } else {
     c = at::empty({M, NO}, a.options());
   }
@@ -85,7 +86,9 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   }
   if (M == 0 || N == 0) return c;
   GemmArgs g{a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0), c.data_ptr(), (int)c.stride(0),
-             bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1};
+             bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1,
+             (compact_rows && rows.has_value()) ? (int)c.size(0) : 0};
+  TORCH_CHECK(!compact_rows || (rows.has_value() && !residual.has_value()), "compact_rows needs rows and no residual");
   const bool glds_ok = (K % 64 == 0);
   const float* csp = nullptr;
   if (ln_mode != 0) {
@@ -310,6 +313,36 @@ at::Tensor grouped_gemm(const at::Tensor& X, const at::Tensor& offsets, const at
   return Y;
 }
 
+// experts: list of E compact [rows][H] bf16 outputs; ptrs: int64 [E] device tensor holding
+// their addresses (built once by the caller and cached — hipGraph-safe)
+at::Tensor moe_gather_combine(const std::vector<at::Tensor>& experts, const at::Tensor& ptrs, const at::Tensor& idx,
+                              const at::Tensor& slot_of, const at::Tensor& offsets, const at::Tensor& w,
+                              const c10::optional<at::Tensor>& residual, at::Tensor& out) {
+  const int64_t E = (int64_t)experts.size();
+  TORCH_CHECK(E > 0 && ptrs.scalar_type() == at::kLong && ptrs.numel() == E && ptrs.is_cuda(), "ptrs: int64 [E]");
+  const int64_t M = out.size(0), H = out.size(1), k = idx.size(1);
+  check_bf16(out, "out");
+  TORCH_CHECK(out.is_contiguous() && H % 8 == 0 && k <= 8, "out contiguous [M][H], H % 8 == 0, top-k <= 8");
+  for (const auto& t : experts) {
+    check_bf16(t, "expert output");
+    TORCH_CHECK(t.is_contiguous() && t.size(-1) == H && t.numel() >= M * H, "expert outputs must be [>=M][H]");
+  }
+  TORCH_CHECK(idx.scalar_type() == at::kInt && idx.numel() == M * k && slot_of.scalar_type() == at::kInt &&
+                  slot_of.numel() == M * k && offsets.scalar_type() == at::kInt && offsets.numel() == E + 1 &&
+                  w.scalar_type() == at::kFloat && w.numel() == M * k,
+              "routing tensors: idx/slot int32 [M][k], offsets int32 [E+1], w fp32 [M][k]");
+  const void* rp = nullptr;
+  if (residual.has_value()) {
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->is_contiguous() && residual->numel() == M * H, "residual [M][H]");
+    rp = residual->data_ptr();
+  }
+  launch_moe_gather_combine(reinterpret_cast<const unsigned long long*>(ptrs.data_ptr<int64_t>()),
+                            idx.data_ptr<int32_t>(), slot_of.data_ptr<int32_t>(), offsets.data_ptr<int32_t>(),
+                            w.data_ptr<float>(), rp, out.data_ptr(), (int)M, (int)k, (int)H, (int)E, cur_stream());
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -317,7 +350,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),
         py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1,
         py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5,
-        py::arg("rows") = py::none());
+        py::arg("rows") = py::none(), py::arg("compact_rows") = false);
   m.attr("REGSTAGE") = kRegStage;
   m.def("gemm_pick_config", &gemm_pick_config);
   m.def("gemm_glds_num_configs", &gemm_glds_num_configs);
@@ -339,6 +372,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none());
   m.def("rope_", &rope_);
   m.def("moe_router", &moe_router);
+  m.def("moe_gather_combine", &moe_gather_combine);
   m.def("moe_align", &moe_align);
   m.def("moe_permute", &moe_permute);
   m.def("moe_combine", &moe_combine, py::arg("expert_out"), py::arg("slot_of"), py::arg("weights"),

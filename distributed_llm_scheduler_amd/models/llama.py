@@ -116,9 +116,13 @@ def build_llama_dag(cfg: "ModelConfig | str" = "llama3-8b", batch: int = 1, seq:
                            {"expert": e, "n_experts": E, "top_k": K, "ffn": F}, shape),
                     6.0 * rows * H * F, extra=M * K * (H + 3 * F) * dtype_bytes)
                 experts.append(f"layer_{i}_expert_{e}")
-            add(f"layer_{i}_output", 0.01, experts + [f"layer_{i}_attn_residual"], [],
-                OpSpec("moe_combine", [tid(x) for x in experts] + [tid(f"layer_{i}_attn_residual")], {}, {}, shape),
-                1.0 * M * H * (E + 1))
+            # combine = residual + gate-weighted gather of the experts' compact outputs; the
+            # router edge carries the (tiny) logits so routing is known wherever this runs
+            add(f"layer_{i}_output", 0.01, experts + [f"layer_{i}_router", f"layer_{i}_attn_residual"], [],
+                OpSpec("moe_combine", [tid(x) for x in experts] + [tid(f"layer_{i}_router"),
+                                                                   tid(f"layer_{i}_attn_residual")],
+                       {}, {"n_experts": E, "top_k": K}, shape),
+                1.0 * M * H * (K + 1))
         else:
             add(f"layer_{i}_mlp", 0.16, [f"layer_{i}_ffn_norm"],
                 [f"layer_{i}_ffn_gate_up_weights", f"layer_{i}_ffn_down_weights"],

@@ -163,27 +163,34 @@ def ref_rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t):
 
 # --------------------------------------------------------------------- dispatchers
 
-def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=None, rows_hint=None):
+def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=None, rows_hint=None,
+           compact=False):
     """``act(alpha * x @ w^T + bias) + residual`` — one MFMA GEMM kernel with the whole
     epilogue fused on GPU. ``act="swiglu"`` takes a gate/up-interleaved weight
     (:func:`interleave_gate_up`) and returns the N/2-wide ``silu(gate) * up``. ``rows``
     (int32[2] tensor on x's device) restricts the GEMM to rows [rows[0], rows[1]) of x and
     ``out`` without a host sync (MoE experts); ``rows_hint`` is the expected row count used
-    to pick the tuned kernel config."""
+    to pick the tuned kernel config; ``compact`` writes the range to rows 0..r1-r0-1 of ``out``
+    (at most ``out.shape[0]`` rows)."""
     a = ACT[act] if not isinstance(act, int) else act
     n_out = w.shape[0] // 2 if a == SWIGLU else w.shape[0]
     if _gpu(x):
         shp = x.shape[:-1] + (n_out,)
         M = x.numel() // x.shape[-1]
         cfg, sk = tuning.lookup(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
-        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows)
+        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact))
         return y.view(shp) if out is None else out
     if rows is not None:
         r0, r1 = (int(v) for v in rows.tolist())
         if out is None:
             out = torch.zeros(x.shape[:-1] + (n_out,), dtype=x.dtype)
         res = residual[r0:r1] if residual is not None else None
-        out[r0:r1] = ref_linear(x[r0:r1], w, bias, act, res, alpha)
+        o2 = out.reshape(-1, out.shape[-1])
+        if compact:
+            n = min(r1 - r0, o2.shape[0])
+            o2[:n] = ref_linear(x[r0:r0 + n], w, bias, act, None, alpha)
+        else:
+            o2[r0:r1] = ref_linear(x[r0:r1], w, bias, act, res, alpha)
         return out
     y = ref_linear(x, w, bias, act, residual, alpha)
     if out is not None:
@@ -353,6 +360,32 @@ def moe_combine(expert_out, slot_of, weights, slot_range=None, out=None):
     g = torch.where(keep[..., None], g, torch.zeros_like(g))  # rows outside the range are never read
     y = (g * weights.float()[..., None]).sum(1).to(expert_out.dtype)
     return out.copy_(y) if out is not None else y
+
+
+def moe_gather_combine(experts, idx, slot_of, offsets, gate, residual=None, out=None, ptrs=None):
+    """``out[m] = residual[m] + sum_j gate[m,j] * experts[e][slot[m,j] - offsets[e]]``, e = idx[m,j],
+    over COMPACT per-expert outputs (expert e's routed rows at rows 0..count_e-1 of its
+    buffer). ``ptrs``: cached int64 device tensor of the expert buffers' addresses (GPU)."""
+    M, k = idx.shape
+    if _gpu(out):
+        if ptrs is None:
+            ptrs = torch.tensor([t.data_ptr() for t in experts], dtype=torch.int64, device=out.device)
+        o2 = out.view(M, -1)
+        return ext().moe_gather_combine([t.reshape(-1, o2.shape[1]) for t in experts], ptrs, idx, slot_of,
+                                        offsets, gate.contiguous(), None if residual is None else
+                                        residual.reshape(M, -1), o2)
+    H = out.shape[-1]
+    acc = residual.reshape(M, H).float().clone() if residual is not None else torch.zeros(M, H)
+    off = offsets.long()
+    for j in range(k):
+        e = idx[:, j].long()
+        row = slot_of.reshape(M, k)[:, j].long() - off[e]
+        for ee in range(len(experts)):
+            sel = (e == ee).nonzero().flatten()
+            if sel.numel():
+                acc[sel] += gate.reshape(M, k)[sel, j, None].float() * experts[ee].reshape(-1, H)[row[sel]].float()
+    out.view(M, H).copy_(acc.to(out.dtype))
+    return out
 
 
 def moe_expert(h, router_logits, w_gate_up, w_down, expert, n_experts, top_k, out=None):

@@ -85,7 +85,8 @@ class DAGExecutor:
         self._valid: List[Tuple[int, int, str]] = []  # param arena regions holding data
         self._inputs: Dict[str, torch.Tensor] = {}
         self._scratch_bufs: Dict[str, torch.Tensor] = {}
-        self._moe_memo: Dict[tuple, tuple] = {}
+        self._moe_memo: Dict[tuple, object] = {}
+        self._moe_ptrs: Dict[tuple, torch.Tensor] = {}
         self._pending_sends: List[Tuple[int, int, object]] = []
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
@@ -307,37 +308,59 @@ class DAGExecutor:
             self._scratch_bufs[tag] = buf
         return buf[:n].view(shape)
 
-    def _moe_routing(self, h_name: str, r_name: str, E: int, top_k: int):
-        """Routing of one MoE layer on this rank, computed ONCE per step and shared by every
-        expert node placed here: top-k gates, expert-sorted token rows (permuted copy of the
-        normalised hidden states), slot map and per-expert row offsets — all on device."""
-        key = (h_name, r_name)
+    def _moe_route(self, r_name: str, E: int, top_k: int):
+        """Routing of one MoE layer on this rank from its router logits, computed ONCE per step
+        and shared by every expert (and the combine) placed here: top-k experts and gates,
+        the expert-sorted order (src rows, slot of each (token, k), per-expert offsets)."""
+        key = ("route", r_name)
         r = self._moe_memo.get(key)
         if r is None:
-            h = self._flat(self._x(h_name))
             idx, gate = ops.moe_router(self._flat(self._x(r_name)), top_k)
             src, slot, off = ops.moe_align(idx, E)
-            xp = ops.moe_permute(h, src)
-            r = (xp, gate, slot, off)
+            r = (idx, gate, src, slot, off)
             self._moe_memo[key] = r
         return r
 
+    def _moe_permuted(self, h_name: str, r_name: str, E: int, top_k: int):
+        key = ("perm", h_name, r_name)
+        xp = self._moe_memo.get(key)
+        if xp is None:
+            src = self._moe_route(r_name, E, top_k)[2]
+            xp = ops.moe_permute(self._flat(self._x(h_name)), src)
+            self._moe_memo[key] = xp
+        return xp
+
     def _moe_expert(self, t: Task, out: torch.Tensor) -> None:
-        """One expert node: its routed rows (a device-side range of the permuted rows) run
-        gate_up GEMM with the SwiGLU epilogue and the down GEMM, then are gate-weighted into
-        this node's [M, H] output (zero for tokens not routed here)."""
+        """One expert node: its routed rows (a device-side range of the expert-sorted rows) run
+        the gate_up GEMM with the SwiGLU epilogue and the down GEMM, which writes them
+        COMPACTLY to rows 0..count-1 of this node's [M, H] output (the layer's combine node
+        gathers them by slot; no per-expert zero-filled [M, H] pass)."""
         a, W = t.op.attrs, t.op.weights
         E, K, e = a["n_experts"], a["top_k"], a["expert"]
-        xp, gate, slot, off = self._moe_routing(t.op.inputs[0], t.op.inputs[1], E, K)
+        off = self._moe_route(t.op.inputs[1], E, K)[4]
+        xp = self._moe_permuted(t.op.inputs[0], t.op.inputs[1], E, K)
         rows = off[e:e + 2]
         R, F = xp.shape[0], a["ffn"]
         hint = max(1, R // E)
         hbuf = self._scratch("moe_h", (R, F))
-        ybuf = self._scratch("moe_y", (R, xp.shape[1]))
         W13, _, _ = self._prep(W["w_gate_up"], None, None, interleave=True)
         ops.linear(xp, W13, act="swiglu", out=hbuf, rows=rows, rows_hint=hint)
-        ops.linear(hbuf, self._w(W["w_down"]), out=ybuf, rows=rows, rows_hint=hint)
-        ops.moe_combine(ybuf, slot, gate, rows, out)
+        ops.linear(hbuf, self._w(W["w_down"]), out=out, rows=rows, rows_hint=hint, compact=True)
+
+    def _moe_combine(self, t: Task, out: torch.Tensor) -> None:
+        """residual + gate-weighted gather of the compact expert outputs (inputs: expert
+        nodes..., router, residual)."""
+        a = t.op.attrs
+        ins_ = t.op.inputs
+        experts, r_name, res_name = ins_[:-2], ins_[-2], ins_[-1]
+        idx, gate, _, slot, off = self._moe_route(r_name, a["n_experts"], a["top_k"])
+        bufs = [self._x(x) for x in experts]
+        key = ("ptrs", t.id)
+        ptrs = self._moe_ptrs.get(key)
+        if ptrs is None and self.gpu:
+            ptrs = torch.tensor([b.data_ptr() for b in bufs], dtype=torch.int64, device=self.device)
+            self._moe_ptrs[key] = ptrs
+        ops.moe_gather_combine(bufs, idx, slot, off, gate, residual=self._x(res_name), out=out, ptrs=ptrs)
 
     def _run_group(self, ins) -> None:
         grp = [self.tasks[t] for t in ins.group]
@@ -397,8 +420,10 @@ class DAGExecutor:
             ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out))
         elif k == "moe_expert":
             self._moe_expert(head, self._flat(out))
-        elif k in ("moe_combine", "sum"):
-            # sum of partial outputs (expert contributions + residual, or TP shard partials)
+        elif k == "moe_combine":
+            self._moe_combine(head, self._flat(out))
+        elif k == "sum":
+            # tensor-parallel shard partials
             ins_ = head.op.inputs
             acc = self._x(ins_[-1])
             for name in ins_[:-1]:

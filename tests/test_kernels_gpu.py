@@ -255,3 +255,46 @@ def test_folded_norm_with_swiglu(mode):
     bi = ops.interleave_gate_up(bd) if nb is not None else None
     y = ops.linear_norm(x, wi, csi, bi, mode, act="swiglu")
     _close(y.cpu(), ref, 3e-2)
+
+
+@pytest.mark.parametrize("config,splitk", [(-1, 0), (7, 1), (15, 4), (3, 2)])
+def test_gemm_row_range_compact(config, splitk):
+    M, N, K, cap = 512, 512, 1024, 200
+    x = _rand(M, K, seed=80)
+    w = _rand(N, K, scale=0.05, seed=81)
+    out = torch.full((cap, N), 7.0, dtype=torch.bfloat16, device=DEV)
+    rows = torch.tensor([130, 290], dtype=torch.int32, device=DEV)  # 160 rows -> out rows 0..159
+    ops.ext().gemm(x, w, None, None, 0, 1.0, out, config, splitk, None, 0, 1e-5, rows, True)
+    torch.cuda.synchronize()
+    o = out.cpu().float()
+    _close(o[:160], ops.ref_linear(x[130:290].cpu(), w.cpu()).float(), 2e-2)
+    assert (o[160:] == 7.0).all()
+    over = torch.tensor([0, 400], dtype=torch.int32, device=DEV)  # more rows than the output holds: clamped
+    ops.ext().gemm(x, w, None, None, 0, 1.0, out, config, splitk, None, 0, 1e-5, over, True)
+    torch.cuda.synchronize()
+    _close(out.cpu().float(), ops.ref_linear(x[:cap].cpu(), w.cpu()).float(), 2e-2)
+
+
+def test_moe_gather_combine():
+    M, E, k, H = 300, 8, 2, 256
+    g = torch.Generator().manual_seed(90)
+    logits = torch.randn(M, E, generator=g).to(torch.bfloat16)
+    idx, gate = ops.moe_router(logits, k)
+    src, slot, off = ops.moe_align(idx, E)
+    counts = (off[1:] - off[:-1]).tolist()
+    experts = [(torch.randn(M, H, generator=g) * (1 + e)).to(torch.bfloat16) for e in range(E)]
+    res = torch.randn(M, H, generator=g).to(torch.bfloat16)
+    ref = ops.moe_gather_combine(experts, idx, slot, off, gate, residual=res, out=torch.empty(M, H, dtype=torch.bfloat16))
+    # explicit fp32 recomputation
+    exp = res.float().clone()
+    for m in range(M):
+        for j in range(k):
+            e = int(idx[m, j])
+            exp[m] += float(gate[m, j]) * experts[e][int(slot[m * k + j]) - int(off[e])].float()
+    _close(ref.float(), exp, 1e-2)
+    assert all(c <= M for c in counts)
+    out = torch.empty(M, H, dtype=torch.bfloat16, device=DEV)
+    y = ops.moe_gather_combine([t.to(DEV) for t in experts], idx.to(DEV), slot.to(DEV), off.to(DEV), gate.to(DEV),
+                               residual=res.to(DEV), out=out)
+    torch.cuda.synchronize()
+    _close(y.cpu().float(), exp, 1e-2)
