@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--init", default="auto", choices=["auto", "host", "device"],
                     help="weight init: device RNG straight into HBM, or host master copy (auto: device "
                          "unless the program re-loads evicted groups, whose cost must be a real copy)")
+    ap.add_argument("--refine-tuning", action="store_true",
+                    help="before timing, pick GEMM configs by whole-step hipGraph time (persists ops/gemm_tuning.json)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-fuse", action="store_true")
     ap.add_argument("--profile", action="store_true", help="also print a measured per-kernel timeline")
@@ -98,6 +100,8 @@ def main():
         ex.step()
     sync()
     captured = ex.capture() if not args.no_graph else False
+    if captured and args.refine_tuning:
+        log(f"[bench] rank {rank}: in-DAG GEMM refinement: {ex.refine_tuning()}")
     if captured:
         ex.step()
     sync()

@@ -21,6 +21,8 @@ import torch
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
 _lock = threading.Lock()
 _table: Optional[Dict[str, Tuple[int, int]]] = None
+_cands: Dict[str, list] = {}     # key -> runner-up (cfg, splitk) by microbenchmark time (for in-DAG refinement)
+_refined: Dict[str, bool] = {}   # key -> chosen by whole-step timing inside a DAG
 REGSTAGE = 100  # config ids >= 100 select the register-staged kernel (csrc ops_binding kRegStage)
 
 
@@ -41,7 +43,10 @@ def table() -> Dict[str, Tuple[int, int]]:
             if os.path.exists(_PATH):
                 try:
                     with open(_PATH) as f:
-                        _table = {k: tuple(v) for k, v in json.load(f).get("gemm", {}).items()}
+                        doc = json.load(f)
+                    _table = {k: tuple(v) for k, v in doc.get("gemm", {}).items()}
+                    _cands.update({k: [tuple(c) for c in v] for k, v in doc.get("candidates", {}).items()})
+                    _refined.update(doc.get("refined", {}))
                 except (OSError, ValueError):
                     _table = {}
         return _table
@@ -62,8 +67,9 @@ def lookup(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
 def _save() -> None:
     try:
         with open(_PATH, "w") as f:
-            json.dump({"device": "MI355X (gfx950)", "gemm": {k: list(v) for k, v in sorted(table().items())}}, f,
-                      indent=1)
+            json.dump({"device": "MI355X (gfx950)", "gemm": {k: list(v) for k, v in sorted(table().items())},
+                       "candidates": {k: [list(c) for c in v] for k, v in sorted(_cands.items())},
+                       "refined": dict(sorted(_refined.items()))}, f, indent=1)
     except OSError:
         pass
 
@@ -139,9 +145,30 @@ def tune(M: int, N: int, K: int, device=None, cold: bool = True, save: bool = Tr
     del ws
     if best is not None:
         table()[_key(M, N, K, tg)] = (best[0], best[1])
+        _cands[_key(M, N, K, tg)] = [c for c, _ in sorted(results.items(), key=lambda kv: kv[1])[:4]]
         if save:
             _save()
     return best, results
+
+
+def set_choice(M: int, N: int, K: int, tg: str, choice: Tuple[int, int]) -> None:
+    table()[_key(M, N, K, tg)] = tuple(choice)
+
+
+def runner_ups(M: int, N: int, K: int, tg: str = "", n: int = 3) -> list:
+    return list(_cands.get(_key(M, N, K, tg), []))[:n]
+
+
+def mark_refined(M: int, N: int, K: int, tg: str = "") -> None:
+    _refined[_key(M, N, K, tg)] = True
+
+
+def is_refined(M: int, N: int, K: int, tg: str = "") -> bool:
+    return bool(_refined.get(_key(M, N, K, tg)))
+
+
+def save() -> None:
+    _save()
 
 
 def ensure_tuned(shapes: Iterable[tuple], device=None) -> None:
