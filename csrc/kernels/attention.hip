@@ -47,6 +47,25 @@ struct AttnCfg {
 
 __device__ __forceinline__ int swz(int row, int ch_mask) { return row & ch_mask; }
 
+// Cross-lane reduction steps on the VALU (v_permlane16/32_swap, CDNA4) instead of
+// ds_bpermute: with the same value in both operands the two results are x[l] and x[l ^ 16]
+// (resp. ^ 32) in some order, so their max / sum is one butterfly step.
+template <bool MAX, int DIST>
+__device__ __forceinline__ float xlane(float x) {
+  const unsigned u = __float_as_uint(x);
+  float a, b;
+  if constexpr (DIST == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+  }
+  return MAX ? fmaxf(a, b) : a + b;
+}
+
 template <int D, int NW, int ST>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ Q, int ldq,
                                                        const bf16* __restrict__ Kp, int ldk,
@@ -75,21 +94,35 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   // LDS-DMA source pointers: instruction j of this wave -> operand (K or V) rows
   const int kv_end = causal ? min(S, qt * C::QB + C::QB) : S;
   const int ntiles = (kv_end + C::KT - 1) / C::KT;
+  // per-lane DMA sources, computed once: instruction j of this wave covers operand op's
+  // rows r0..r0+ROWS_PER_INSTR-1 of every tile; a tile only moves the base by KT rows.
+  // Rows past S (the last tile) are clamped to S-1 (their scores are masked to -inf).
+  const bf16* dsrc[C::PW];
+  int drow[C::PW], doff[C::PW];
+  size_t dstep[C::PW];
+#pragma unroll
+  for (int j = 0; j < C::PW; ++j) {
+    const int ins = wave * C::PW + j;            // 0 .. 2*INSTR-1
+    const int op = ins / C::INSTR;               // 0 = K, 1 = V
+    const int r0 = (ins % C::INSTR) * C::ROWS_PER_INSTR;
+    const int row = r0 + lane / C::CH;
+    const int gch = (lane % C::CH) ^ swz(row, C::CH - 1);
+    const int ld = op == 0 ? ldk : ldv;
+    dsrc[j] = (op == 0 ? Kp : Vp) + tok0 * ld + kvh * D + gch * 8;
+    dstep[j] = (size_t)ld;
+    drow[j] = row;
+    doff[j] = op * C::TILE_BYTES + r0 * C::RB;
+  }
+  const bool tail_clamp = (S % C::KT) != 0;
   auto issue = [&](int t) {
     char* buf = smem + (t % ST) * C::BUF_BYTES;
+    const bool clamp = tail_clamp && (t + 1) * C::KT > S;
 #pragma unroll
     for (int j = 0; j < C::PW; ++j) {
-      const int ins = wave * C::PW + j;            // 0 .. 2*INSTR-1
-      const int op = ins / C::INSTR;               // 0 = K, 1 = V
-      const int r0 = (ins % C::INSTR) * C::ROWS_PER_INSTR;
-      const int row = r0 + lane / C::CH;
-      const int pos = lane % C::CH;
-      const int key = min(t * C::KT + row, S - 1);
-      const int gch = pos ^ swz(row, C::CH - 1);
-      const bf16* base = op == 0 ? (Kp + (tok0 + key) * ldk) : (Vp + (tok0 + key) * ldv);
-      __builtin_amdgcn_global_load_lds((const void*)(base + kvh * D + gch * 8),
-                                       (__attribute__((address_space(3))) void*)(buf + op * C::TILE_BYTES + r0 * C::RB),
-                                       16, 0, 0);
+      int key = t * C::KT + drow[j];
+      if (clamp) key = min(key, S - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(dsrc[j] + (size_t)key * dstep[j]),
+                                       (__attribute__((address_space(3))) void*)(buf + doff[j]), 16, 0, 0);
     }
   };
 
@@ -125,35 +158,41 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
         s[n] = mfma16x16x32(kf, qf[ks], s[n]);
       }
     }
-    // ---- online softmax for query my_q; scores s[n][i] <-> key key0 + 16n + 4g + i
-    const bool diag = causal && (key0 + C::KT > qt * C::QB);
-    float mx = -INFINITY;
+    // ---- online softmax for query my_q; scores s[n][i] <-> key key0 + 16n + 4g + i.
+    // Raw scores are kept; the scale is folded into the exponent: p = 2^(s*c - m*c).
+    // Masks only on the wave's diagonal tile and the ragged last tile (wave-uniform branch).
+    const bool masked = (key0 + C::KT > S) || (causal && key0 + C::KT - 1 > q0);
+    if (masked) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+      for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = key0 + 16 * n + 4 * g + i;
-        float v = s[n][i] * scale_log2;
-        if (key >= S || (diag && key > my_q)) v = -INFINITY;
-        s[n][i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_run - m_new);
+        for (int i = 0; i < 4; ++i) {
+          const int key = key0 + 16 * n + 4 * g + i;
+          if (key >= S || (causal && key > my_q)) s[n][i] = -INFINITY;
+        }
+    }
+    float mx = fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3]));
+#pragma unroll
+    for (int n = 1; n < 4; ++n) mx = fmaxf(mx, fmaxf(fmaxf(s[n][0], s[n][1]), fmaxf(s[n][2], s[n][3])));
+    mx = xlane<true, 16>(mx);
+    mx = xlane<true, 32>(mx);
+    // m_new is finite from the first tile on (key 0 is visible to every query); the clamp
+    // only keeps -inf - -inf out of padded rows
+    const float m_new = fmaxf(fmaxf(m_run, mx), -1e30f);
+    const float alpha = __builtin_amdgcn_exp2f((m_run - m_new) * scale_log2);
+    const float mc = m_new * scale_log2;
     float sum = 0.f;
     bf16x8 pf[2];
 #pragma unroll
     for (int n = 0; n < 4; ++n)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float e = (m_new == -INFINITY) ? 0.f : exp2f(s[n][i] - m_new);
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[n][i], scale_log2, -mc));
         sum += e;
         pf[n >> 1][4 * (n & 1) + i] = f2bf(e);
       }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
+    sum = xlane<false, 16>(sum);
+    sum = xlane<false, 32>(sum);
     l_run = l_run * alpha + sum;
     m_run = m_new;
 #pragma unroll
@@ -210,12 +249,10 @@ static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
     case 2: launch_attn<D, 4, 2>(a, s); break;
     case 3: launch_attn<D, 2, 3>(a, s); break;
     case 4: launch_attn<D, 4, 3>(a, s); break;
-    default: {
-      // small grids (few heads x short sequences) use 32-query blocks to fill more CUs
-      const long blocks64 = (long)((a.S + 63) / 64) * a.n_head * a.B;
-      if (blocks64 < 512) launch_attn<D, 2, 2>(a, s);
-      else launch_attn<D, 4, 2>(a, s);
-    }
+    default:
+      // 64-query blocks, 2 K/V stages: fastest on every measured shape (GPT-2 / Llama-3-8B
+      // S=512, batch 8, S=2048) once the softmax stopped being VALU-bound
+      launch_attn<D, 4, 2>(a, s);
   }
 }
 

@@ -43,6 +43,25 @@ __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "me
 // together; 1 -> A keeps STAGES buffers (it is L2-resident: short latency) while the COLD
 // weight stream gets STAGES + 1, i.e. one more tile of HBM latency covered inside the same
 // 160 KiB of LDS (e.g. 256x256: 2 x 32 KiB A + 3 x 32 KiB W).
+// rotate the adjacent column pairs (c, c+1) of v[0..n) that start at output column col
+// (even) of row `row` — see RopeArgs
+template <int NV>
+__device__ __forceinline__ void rope_pairs(float* v, int row, int col, const RopeArgs& rp) {
+  if (col >= rp.cols) return;
+  const int half = rp.D >> 1;
+  const int pos = row % rp.S;
+  const int j0 = (col % rp.D) >> 1;
+  const float* cp = rp.cos + (size_t)pos * half + j0;
+  const float* sp = rp.sin + (size_t)pos * half + j0;
+#pragma unroll
+  for (int p = 0; p < NV / 2; ++p) {
+    const float c = cp[p], sn = sp[p];
+    const float x0 = v[2 * p], x1 = v[2 * p + 1];
+    v[2 * p] = x0 * c - x1 * sn;
+    v[2 * p + 1] = x1 * c + x0 * sn;
+  }
+}
+
 template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_, BXS = BXS_;
@@ -239,7 +258,8 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
                                           const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
                                           float* __restrict__ part, int M, int Mmax, int N, int K, int act,
                                           float alpha, int ks, int kslice, int tm, int tn,
-                                          const float* __restrict__ ln_colsum, int ln_mode, float ln_eps) {
+                                          const float* __restrict__ ln_colsum, int ln_mode, float ln_eps,
+                                          const RopeArgs& rope) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WN, wn = wave % C::WN;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
@@ -408,6 +428,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = apply_act(alpha * acc[i][j][e] + bv[e], act);
       }
+      if (rope.cols) rope_pairs<4>(v, row, col, rope);
       if (full) {
         if (R) {
           const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(R + (size_t)row * ldr + col);
@@ -442,7 +463,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
                                                          float alpha, int tiles_m, int tiles_n, int splitk,
                                                          int kslice, const float* __restrict__ ln_colsum,
                                                          int ln_mode, float ln_eps, const int* __restrict__ rows,
-                                                         int compact_rows) {
+                                                         int compact_rows, RopeArgs rope) {
   __shared__ bf16x8 smem[C::LDS_UNITS];
   const int ntile = tiles_m * tiles_n;
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
@@ -450,7 +471,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   const int tm = tile % tiles_m, tn = tile / tiles_m;
   if constexpr (!RANGED) {
     glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn,
-                 ln_colsum, LN ? ln_mode : 0, ln_eps);
+                 ln_colsum, LN ? ln_mode : 0, ln_eps, rope);
     return;
   }
   // device-side row range (MoE expert): the host launched ONE tile row (tiles_m == 1) — no
@@ -463,7 +484,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   for (int t = 0; t * C::BM < Mr; ++t) {
     if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
     glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, Mr, M, N, K, act, alpha, ks, kslice, t, tn,
-                 ln_colsum, 0, ln_eps);
+                 ln_colsum, 0, ln_eps, rope);
   }
 }
 
@@ -475,7 +496,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                             const bf16* __restrict__ bias,
                                                             const bf16* __restrict__ R, int ldr, int act,
                                                             float alpha, const int* __restrict__ rows,
-                                                            int compact_rows) {
+                                                            int compact_rows, RopeArgs rope) {
   const size_t slab = (size_t)M * N;
   int r0 = 0, nrows = M;
   if (rows != nullptr) {
@@ -520,11 +541,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
       bf16x8 bv = {}, rv = {};
       if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
       if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = apply_act(alpha * v[e] + (bias ? bf2f(bv[e]) : 0.f), act);
+      if (rope.cols) rope_pairs<8>(x, m, c, rope);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float x = apply_act(alpha * v[e] + (bias ? bf2f(bv[e]) : 0.f), act);
-        if (R) x += bf2f(rv[e]);
-        o[e] = f2bf(x);
+        if (R) x[e] += bf2f(rv[e]);
+        o[e] = f2bf(x[e]);
       }
     }
     *reinterpret_cast<bf16x8*>(C + (size_t)(compact_rows ? m - r0 : m) * ldc + c) = o;
@@ -541,7 +565,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
 #define DLS_K(LN_, RG_)                                                                                           \
   hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
                      a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
-                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows)
+                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows, a.rope)
   if (rows) DLS_K(0, 1);
   else if (ln_mode != 0) {
     if constexpr (C::BM * C::BN <= 256 * 128) DLS_K(1, 0);  // 256x256 tiles have no registers left for it
@@ -551,7 +575,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     const int64_t nvec = (int64_t)a.M * (a.N / 8);
     const int g = (int)std::min<int64_t>(2048, (nvec + 255) / 256);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, ws, splitk, a.M, a.N, (bf16*)a.C, a.ldc,
-                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows, a.compact_rows);
+                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows, a.compact_rows, a.rope);
   }
 }
 

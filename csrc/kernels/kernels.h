@@ -7,6 +7,15 @@
 
 constexpr int kActSwiglu = 4;  // == ACT_SWIGLU in common.h (device-side enum)
 
+// RoPE applied in a GEMM epilogue to output columns [0, cols): the q/k rows of the weight are
+// PAIR-INTERLEAVED per head (column 2i <-> d_i, 2i+1 <-> d_{i+D/2}), so a rotary pair is two
+// adjacent columns of one lane; position = row % S; cos/sin tables are fp32 [S][D/2].
+struct RopeArgs {
+  const float* cos = nullptr;
+  const float* sin = nullptr;
+  int S = 1, D = 2, cols = 0;  // cols == 0: off
+};
+
 struct GemmArgs {
   const void* A;  // bf16 [M][lda]
   int lda;
@@ -23,6 +32,7 @@ struct GemmArgs {
   int config;    // -1 = auto
   int compact_rows = 0;  // > 0 with a device row range [r0, r1): write output rows 0..r1-r0-1 (not r0..),
                          // and at most compact_rows of them (the output's row capacity)
+  RopeArgs rope{};
 };
 
 int gemm_pick_config(int M, int N, int K);

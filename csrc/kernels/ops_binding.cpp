@@ -39,7 +39,9 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                 const c10::optional<at::Tensor>& residual, int64_t act, double alpha,
                 const c10::optional<at::Tensor>& out, int64_t config, int64_t splitk,
                 const c10::optional<at::Tensor>& ln_colsum, int64_t ln_mode, double ln_eps,
-                const c10::optional<at::Tensor>& rows, bool compact_rows) {
+                const c10::optional<at::Tensor>& rows, bool compact_rows,
+                const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin, int64_t rope_S,
+                int64_t rope_D, int64_t rope_cols) {
   check_bf16(a_in, "A");
   check_bf16(w, "W");
   at::Tensor a = as2d(a_in);
@@ -89,6 +91,19 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
              bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1,
              (compact_rows && rows.has_value()) ? (int)c.size(0) : 0};
   TORCH_CHECK(!compact_rows || (rows.has_value() && !residual.has_value()), "compact_rows needs rows and no residual");
+  if (rope_cols > 0) {
+    TORCH_CHECK(rope_cos.has_value() && rope_sin.has_value() && rope_cos->scalar_type() == at::kFloat &&
+                    rope_sin->scalar_type() == at::kFloat && rope_cos->is_contiguous() && rope_sin->is_contiguous() &&
+                    rope_cos->is_cuda() && rope_sin->is_cuda() &&
+                    rope_cos->numel() >= rope_S * rope_D / 2 && rope_sin->numel() >= rope_S * rope_D / 2,
+                "RoPE epilogue: cos/sin fp32 [S][D/2]");
+    TORCH_CHECK(rope_D % 4 == 0 && rope_cols % rope_D == 0 && rope_cols <= N && !swiglu && K % 64 == 0 &&
+                    !rows.has_value(),
+                "RoPE epilogue: D % 4 == 0, whole heads, LDS-DMA kernel, no SwiGLU / row range");
+    g.rope = RopeArgs{rope_cos->data_ptr<float>(), rope_sin->data_ptr<float>(), (int)rope_S, (int)rope_D,
+                      (int)rope_cols};
+    if (config >= kRegStage) config = -1;
+  }
   const bool glds_ok = (K % 64 == 0);
   const float* csp = nullptr;
   if (ln_mode != 0) {
@@ -350,7 +365,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),
         py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1,
         py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5,
-        py::arg("rows") = py::none(), py::arg("compact_rows") = false);
+        py::arg("rows") = py::none(), py::arg("compact_rows") = false, py::arg("rope_cos") = py::none(),
+        py::arg("rope_sin") = py::none(), py::arg("rope_S") = 1, py::arg("rope_D") = 2, py::arg("rope_cols") = 0);
   m.attr("REGSTAGE") = kRegStage;
   m.def("gemm_pick_config", &gemm_pick_config);
   m.def("gemm_glds_num_configs", &gemm_glds_num_configs);

@@ -91,10 +91,15 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
               f"-I{os.path.join(CSRC, 'kernels')}"]
 
+    # per-file code-generation options: the attention kernel's accumulators feed VALU softmax
+    # math every tile, so it takes the VGPR form of the MFMAs (no accvgpr read/write shuffles);
+    # the GEMMs keep the default (their accumulators only meet the VALU in the epilogue)
+    per_file = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
     def compile_kernel(src):
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         if force or _newer(obj, [src] + hdrs):
-            _run([hipcc, *common, "-c", src, "-o", obj], verbose)
+            _run([hipcc, *common, *per_file.get(os.path.basename(src), []), "-c", src, "-o", obj], verbose)
         return obj
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

@@ -91,16 +91,44 @@ def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
     return torch.stack([g, u], 1).reshape((F2,) + rest).contiguous()
 
 
+def rope_pair_perm(n_q_heads: int, n_k_heads: int, head_dim: int, total_rows: int) -> torch.Tensor:
+    """Row order making every RoPE pair adjacent within each q / k head: new row 2i of a head
+    is its old row i, new 2i+1 is old i + D/2 (V rows untouched). q.k is invariant under a
+    permutation applied to both, so attention needs nothing else."""
+    half = head_dim // 2
+    within = torch.stack([torch.arange(half), torch.arange(half) + half], 1).reshape(-1)
+    idx = torch.arange(total_rows)
+    for h in range(n_q_heads + n_k_heads):
+        idx[h * head_dim:(h + 1) * head_dim] = h * head_dim + within
+    return idx
+
+
+def _rope_ref_pairs(y: torch.Tensor, rope) -> torch.Tensor:
+    cos_t, sin_t, S, D, cols = rope
+    M = y.shape[0]
+    pos = torch.arange(M) % S
+    c = cos_t.cpu()[pos].float()
+    sn = sin_t.cpu()[pos].float()
+    heads = cols // D
+    v = y[:, :cols].reshape(M, heads, D // 2, 2)
+    x0, x1 = v[..., 0], v[..., 1]
+    cc, ss = c[:, None, :], sn[:, None, :]
+    out = torch.stack([x0 * cc - x1 * ss, x1 * cc + x0 * ss], -1).reshape(M, cols)
+    return torch.cat([out, y[:, cols:]], 1)
+
+
 def _swiglu_interleaved(y: torch.Tensor) -> torch.Tensor:
     F2 = y.shape[-1]
     v = y.reshape(y.shape[:-1] + (F2 // (2 * SWIGLU_BLOCK), 2, SWIGLU_BLOCK))
     return (F.silu(v[..., 0, :]) * v[..., 1, :]).reshape(y.shape[:-1] + (F2 // 2,))
 
 
-def ref_linear(x, w, bias=None, act=None, residual=None, alpha=1.0):
+def ref_linear(x, w, bias=None, act=None, residual=None, alpha=1.0, rope=None):
     y = alpha * (x.float() @ w.float().t())
     if bias is not None:
         y = y + bias.float()
+    if rope is not None:
+        y = _rope_ref_pairs(y.reshape(-1, y.shape[-1]), rope).reshape(y.shape)
     if (ACT[act] if not isinstance(act, int) else act) == SWIGLU:
         y = _swiglu_interleaved(y)
         return (y if residual is None else y + residual.float()).to(x.dtype)
@@ -164,21 +192,24 @@ def ref_rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t):
 # --------------------------------------------------------------------- dispatchers
 
 def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=None, rows_hint=None,
-           compact=False):
+           compact=False, rope=None):
     """``act(alpha * x @ w^T + bias) + residual`` — one MFMA GEMM kernel with the whole
     epilogue fused on GPU. ``act="swiglu"`` takes a gate/up-interleaved weight
     (:func:`interleave_gate_up`) and returns the N/2-wide ``silu(gate) * up``. ``rows``
     (int32[2] tensor on x's device) restricts the GEMM to rows [rows[0], rows[1]) of x and
     ``out`` without a host sync (MoE experts); ``rows_hint`` is the expected row count used
     to pick the tuned kernel config; ``compact`` writes the range to rows 0..r1-r0-1 of ``out``
-    (at most ``out.shape[0]`` rows)."""
+    (at most ``out.shape[0]`` rows). ``rope=(cos, sin, S, D, cols)`` rotates output columns
+    [0, cols) in the epilogue (q/k rows pair-interleaved, :func:`rope_pair_perm`)."""
     a = ACT[act] if not isinstance(act, int) else act
     n_out = w.shape[0] // 2 if a == SWIGLU else w.shape[0]
     if _gpu(x):
         shp = x.shape[:-1] + (n_out,)
         M = x.numel() // x.shape[-1]
         cfg, sk = tuning.lookup(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
-        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact))
+        rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
+        y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact),
+                       rc, rs_, int(rS), int(rD), int(rcols))
         return y.view(shp) if out is None else out
     if rows is not None:
         r0, r1 = (int(v) for v in rows.tolist())
@@ -192,7 +223,7 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
         else:
             o2[r0:r1] = ref_linear(x[r0:r1], w, bias, act, res, alpha)
         return out
-    y = ref_linear(x, w, bias, act, residual, alpha)
+    y = ref_linear(x, w, bias, act, residual, alpha, rope=rope)
     if out is not None:
         out.copy_(y)
         return out
@@ -212,7 +243,7 @@ def derive_norm_gemm(w, ln_w, ln_b=None, bias=None):
     return wd, cs, b.to(w.dtype).contiguous()
 
 
-def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, residual=None, out=None):
+def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, residual=None, out=None, rope=None):
     """``act(W . norm(x) + bias) + residual`` in ONE GEMM on the raw rows ``x`` (GPU), with
     ``(w_derived, colsum, bias_derived)`` from :func:`derive_norm_gemm`. ``mode`` is
     "layernorm" or "rmsnorm"."""
@@ -220,8 +251,9 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
     a = ACT[act] if not isinstance(act, int) else act
     shp = x.shape[:-1] + (w_derived.shape[0] // 2 if a == SWIGLU else w_derived.shape[0],)
     cfg, _ = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
+    rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
     y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, 1, colsum, m,
-                   float(eps))
+                   float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols))
     return y.view(shp) if out is None else out
 
 

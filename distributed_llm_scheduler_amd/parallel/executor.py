@@ -246,11 +246,13 @@ class DAGExecutor:
 
     # --- derived weights, recomputed after every real fill of W (cache keyed by W's address) ---
     def _prep(self, w_name: str, norm: Optional[Task] = None, b_name: Optional[str] = None,
-              interleave: bool = False):
+              interleave: bool = False, rope_perm: Optional[tuple] = None):
         """(W, colsum, bias) for the GEMM on weight ``w_name``, transformed IN PLACE once per
         fill: a preceding norm folded in (W' = W*gain, colsum(W'), bias' = bias + W.beta) and/or
-        the gate/up rows interleaved for the SwiGLU epilogue (every per-row vector with them).
-        W is read by this fused group only, so overwriting it is safe."""
+        the gate/up rows interleaved for the SwiGLU epilogue (every per-row vector with them),
+        and/or the q/k rows of each head pair-interleaved for the RoPE epilogue
+        (``rope_perm = (n_q_heads, n_k_heads, head_dim)``). W is read by this fused group only,
+        so overwriting it is safe."""
         W = self._w(w_name)
         key = (w_name, W.data_ptr())
         d = self._derived_cache.get(key)
@@ -268,22 +270,29 @@ class DAGExecutor:
                 wd = ops.interleave_gate_up(wd)
                 cs = ops.interleave_gate_up(cs) if cs is not None else None
                 bias = ops.interleave_gate_up(bias) if bias is not None else None
+            if rope_perm is not None:
+                perm = ops.rope_pair_perm(*rope_perm, wd.shape[0]).to(wd.device)
+                wd = wd[perm].contiguous()
+                cs = cs[perm].contiguous() if cs is not None else None
+                bias = bias[perm].contiguous() if bias is not None else None
             if wd is not W:
                 W.copy_(wd)
             d = (cs, bias)
             self._derived_cache[key] = d
         return W, d[0], d[1]
 
-    def _gemm(self, x, w_name, b_name, norm: Optional[Task], act=None, residual=None, out=None):
+    def _gemm(self, x, w_name, b_name, norm: Optional[Task], act=None, residual=None, out=None, rope=None,
+              rope_perm=None):
         """One GEMM node, optionally with a preceding norm folded in (GPU, K <= FOLD_MAX_K:
         the in-kernel row statistics cost more than a separate norm pass at larger K and
         force split-K off; measured on MI355X, Llama-3-8B K=4096: 109 vs 45+8 us).
-        ``act="swiglu"``: W is a [gate; up] weight, interleaved on first use."""
+        ``act="swiglu"``: W is a [gate; up] weight, interleaved on first use. ``rope`` /
+        ``rope_perm``: RoPE in the epilogue over pair-interleaved q/k rows."""
         sw = act == "swiglu"
         if norm is not None and self.gpu and x.shape[-1] <= FOLD_MAX_K:
-            W, cs, bd = self._prep(w_name, norm, b_name, interleave=sw)
+            W, cs, bd = self._prep(w_name, norm, b_name, interleave=sw, rope_perm=rope_perm)
             return ops.linear_norm(x, W, cs, bd, norm.op.kind, norm.op.attrs.get("eps", 1e-5), act=act,
-                                   residual=residual, out=out)
+                                   residual=residual, out=out, rope=rope)
         if norm is not None:
             nw = self._w(norm.op.weights["w"])
             xn = self._scratch("norm", x.shape)
@@ -292,11 +301,11 @@ class DAGExecutor:
             else:
                 ops.rmsnorm(x, nw, norm.op.attrs.get("eps", 1e-5), out=xn)
             x = xn
-        if sw:
-            W, _, bias = self._prep(w_name, None, b_name, interleave=True)
+        if sw or rope_perm is not None:
+            W, _, bias = self._prep(w_name, None, b_name, interleave=sw, rope_perm=rope_perm)
         else:
             W, bias = self._w(w_name), (self._w(b_name) if b_name else None)
-        return ops.linear(x, W, bias, act=act, residual=residual, out=out)
+        return ops.linear(x, W, bias, act=act, residual=residual, out=out, rope=rope)
 
     def _scratch(self, tag: str, shape) -> torch.Tensor:
         """Reusable per-rank buffer (allocated on first use, i.e. in an eager warm-up step,
@@ -404,10 +413,13 @@ class DAGExecutor:
             width = (nh + 2 * nkv) * D
             qkv = self._ws(0, (M, width))
             o = self._ws(M * width, (M, nh * D))
-            self._gemm(x, W["w_qkv"], W.get("b_qkv"), norm, out=qkv)
             if a.get("rope"):
+                # RoPE in the QKV GEMM epilogue (q/k rows pair-interleaved at load time)
                 cos, sin = self._rope_tables(S, D, a.get("rope_theta", 10000.0))
-                ops.rope_(qkv, S, nh, nkv, D, nh * D, cos, sin)
+                self._gemm(x, W["w_qkv"], W.get("b_qkv"), norm, out=qkv, rope=(cos, sin, S, D, (nh + nkv) * D),
+                           rope_perm=(nh, nkv, D))
+            else:
+                self._gemm(x, W["w_qkv"], W.get("b_qkv"), norm, out=qkv)
             ops.attention(qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:], B, S, nh, nkv,
                           D, causal=a.get("causal", True), out=o)
             ops.linear(o, self._w(W["w_o"]), self._w(W["b_o"]) if "b_o" in W else None, residual=residual,

@@ -298,3 +298,27 @@ def test_moe_gather_combine():
                                residual=res.to(DEV), out=out)
     torch.cuda.synchronize()
     _close(y.cpu().float(), exp, 1e-2)
+
+
+@pytest.mark.parametrize("config,splitk", [(-1, 0), (3, 1), (0, 2), (3, 4), (8, 1)])
+def test_gemm_rope_epilogue(config, splitk):
+    B, S, nh, nkv, D, H = 2, 128, 4, 2, 128, 512
+    M, width = B * S, (nh + 2 * nkv) * D
+    x = _rand(M, H, seed=95)
+    w = _rand(width, H, scale=0.05, seed=96)
+    b = _rand(width, scale=0.1, seed=97)
+    cos, sin = ops.rope_tables(S, D, 10000.0, DEV)
+    perm = ops.rope_pair_perm(nh, nkv, D, width).to(DEV)
+    rope = (cos, sin, S, D, (nh + nkv) * D)
+    y = ops.ext().gemm(x, w[perm].contiguous(), b[perm].contiguous(), None, 0, 1.0, None, config, splitk, None, 0,
+                       1e-5, None, False, cos, sin, S, D, (nh + nkv) * D)
+    torch.cuda.synchronize()
+    ref = ops.ref_linear(x.cpu(), w[perm].cpu(), b[perm].cpu(), rope=(cos.cpu(), sin.cpu(), S, D, (nh + nkv) * D))
+    _close(y.cpu(), ref.float(), 2e-2)
+    # attention over the pair-interleaved q/k equals attention with standard rotate-half RoPE
+    std = ops.ref_linear(x.cpu(), w.cpu(), b.cpu())
+    ops.ref_rope_(std, S, nh, nkv, D, nh * D, cos.cpu(), sin.cpu())
+    split = lambda t: (t[:, :nh * D], t[:, nh * D:(nh + nkv) * D], t[:, (nh + nkv) * D:])  # noqa: E731
+    o_std = ops.ref_attention(*split(std), B, S, nh, nkv, D, causal=True)
+    o_new = ops.ref_attention(*split(y.cpu()), B, S, nh, nkv, D, causal=True)
+    _close(o_new, o_std.float(), 3e-2)
