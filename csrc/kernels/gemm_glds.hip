@@ -252,14 +252,17 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 
 // One output tile (tm, tn) over K-slice ks. Everything from here to the end of the epilogue
 // is per tile; the kernel below maps blocks to tiles (or loops over a device-side row range).
-template <class C>
+// LN: row statistics of a folded norm accumulated in the main loop (else, with ln_mode set,
+// they come from ep.ext_stats).
+template <class C, int LN>
 __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                           const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
                                           const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
                                           float* __restrict__ part, int M, int Mmax, int N, int K, int act,
                                           float alpha, int ks, int kslice, int tm, int tn,
                                           const float* __restrict__ ln_colsum, int ln_mode, float ln_eps,
-                                          const RopeArgs& rope) {
+                                          const Epi& ep) {
+  const RopeArgs& rope = ep.rope;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WN, wn = wave % C::WN;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
@@ -274,7 +277,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // fused LayerNorm/RMSNorm prologue: row statistics of A accumulated from the A fragments
   // that stream through LDS anyway (waves with wn == 0; full K per block, splitk == 1)
-  const bool ln_acc = ln_mode != 0 && wn == 0;
+  const bool ln_acc = LN && ln_mode != 0 && wn == 0;
   float st_s[C::FM], st_q[C::FM];
 #pragma unroll
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
@@ -288,6 +291,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   const int g4 = (lane >> 4) * 4, r16 = lane & 15;
   float ln_rs[C::FM], ln_mu[C::FM];
   if (ln_mode != 0) {
+    if constexpr (LN) {
     // reduce the 4 lane groups (k-chunks) -> full-row sums, publish per row via LDS
     float* stats = reinterpret_cast<float*>(smem);
     raw_barrier();  // every wave is past its last LDS read of the staging buffers
@@ -320,6 +324,18 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
       } else {
         ln_mu[i] = 0.f;
         ln_rs[i] = rsqrtf(q * inv_k + ln_eps);
+      }
+    }
+      } else {
+      // statistics handed over by the producer of A (fp32 [M][2] = sum, sum of squares)
+      const float inv_k = 1.0f / (float)K;
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int row = min(m0 + wm * C::WTM + i * 16 + r16, M - 1);
+        const float a = ep.ext_stats[2 * row], q = ep.ext_stats[2 * row + 1];
+        const float mu = ln_mode == 1 ? a * inv_k : 0.f;
+        ln_mu[i] = mu;
+        ln_rs[i] = rsqrtf(fmaxf(q * inv_k - mu * mu, 0.f) + ln_eps);
       }
     }
   }
@@ -396,6 +412,9 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     }
     return;
   }
+  float ps1[C::FM], ps2[C::FM];  // per-row partial (sum, sum of squares) of this lane's outputs
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) ps1[i] = ps2[i] = 0.f;
 #pragma unroll
   for (int j = 0; j < C::FN; ++j) {
     const int col = n0 + wn * C::WTN + j * 16 + g4;
@@ -439,14 +458,45 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
         *reinterpret_cast<bf16x4*>(Cp + (size_t)row * ldc + col) = o;
+        if (ep.stats_out) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float y = bf2f(o[e]);
+            ps1[i] += y;
+            ps2[i] += y * y;
+          }
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (col + e >= N) continue;
           float x = v[e];
           if (R) x += bf2f(R[(size_t)row * ldr + col + e]);
-          Cp[(size_t)row * ldc + col + e] = f2bf(x);
+          const bf16 ob = f2bf(x);
+          Cp[(size_t)row * ldc + col + e] = ob;
+          if (ep.stats_out) {
+            const float y = bf2f(ob);
+            ps1[i] += y;
+            ps2[i] += y * y;
+          }
         }
+      }
+    }
+  }
+  if (ep.stats_out) {
+    // the 4 lane groups of a fragment row hold disjoint columns: fold them, then one pair of
+    // atomics per (row, wave) into the caller-zeroed [M][2] buffer
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      float a = ps1[i], q = ps2[i];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      const int row = m0 + wm * C::WTM + i * 16 + r16;
+      if (lane < 16 && row < M) {
+        atomicAdd(ep.stats_out + 2 * row, a);
+        atomicAdd(ep.stats_out + 2 * row + 1, q);
       }
     }
   }
@@ -463,15 +513,15 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
                                                          float alpha, int tiles_m, int tiles_n, int splitk,
                                                          int kslice, const float* __restrict__ ln_colsum,
                                                          int ln_mode, float ln_eps, const int* __restrict__ rows,
-                                                         int compact_rows, RopeArgs rope) {
+                                                         int compact_rows, Epi ep) {
   __shared__ bf16x8 smem[C::LDS_UNITS];
   const int ntile = tiles_m * tiles_n;
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
   const int ks = bid / ntile, tile = bid % ntile;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
   if constexpr (!RANGED) {
-    glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn,
-                 ln_colsum, LN ? ln_mode : 0, ln_eps, rope);
+    glds_tile<C, LN>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn,
+                     ln_colsum, (LN || ep.ext_stats) ? ln_mode : 0, ln_eps, ep);
     return;
   }
   // device-side row range (MoE expert): the host launched ONE tile row (tiles_m == 1) — no
@@ -483,8 +533,42 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   if (part) part += (size_t)r0 * N;
   for (int t = 0; t * C::BM < Mr; ++t) {
     if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
-    glds_tile<C>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, Mr, M, N, K, act, alpha, ks, kslice, t, tn,
-                 ln_colsum, 0, ln_eps, rope);
+    glds_tile<C, 0>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, Mr, M, N, K, act, alpha, ks, kslice, t, tn,
+                    ln_colsum, 0, ln_eps, ep);
+  }
+}
+
+// Epilogue of a split-K GEMM for 8 consecutive columns c..c+7 of row m (non-SwiGLU):
+// norm fold with handed-over row statistics, bias, activation, RoPE, residual.
+struct ReduceNorm {
+  const float* colsum;
+  int mode;  // 0 none, 1 LayerNorm, 2 RMSNorm (statistics from ep.ext_stats)
+  float eps;
+  int K;
+};
+
+__device__ __forceinline__ void reduce_finalize(float (&x)[8], const float (&v)[8], int m, int c,
+                                                const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
+                                                int act, float alpha, const Epi& ep, const ReduceNorm& nm) {
+  bf16x8 bv = {}, rv = {};
+  if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
+  if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
+  float mu = 0.f, rs = 1.f;
+  if (nm.mode != 0) {
+    const float inv_k = 1.0f / (float)nm.K;
+    const float a = ep.ext_stats[2 * m], q = ep.ext_stats[2 * m + 1];
+    mu = nm.mode == 1 ? a * inv_k : 0.f;
+    rs = rsqrtf(fmaxf(q * inv_k - mu * mu, 0.f) + nm.eps);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float z = nm.mode != 0 ? rs * (v[e] - mu * nm.colsum[c + e]) : alpha * v[e];
+    x[e] = apply_act(z + (bias ? bf2f(bv[e]) : 0.f), act);
+  }
+  if (ep.rope.cols) rope_pairs<8>(x, m, c, ep.rope);
+  if (R) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] += bf2f(rv[e]);
   }
 }
 
@@ -496,7 +580,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
                                                             const bf16* __restrict__ bias,
                                                             const bf16* __restrict__ R, int ldr, int act,
                                                             float alpha, const int* __restrict__ rows,
-                                                            int compact_rows, RopeArgs rope) {
+                                                            int compact_rows, Epi ep, ReduceNorm nm) {
   const size_t slab = (size_t)M * N;
   int r0 = 0, nrows = M;
   if (rows != nullptr) {
@@ -538,26 +622,63 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         o[e] = f2bf(silu(g) * up);
       }
     } else {
-      bf16x8 bv = {}, rv = {};
-      if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
-      if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
       float x[8];
+      reduce_finalize(x, v, m, c, bias, R, ldr, act, alpha, ep, nm);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = apply_act(alpha * v[e] + (bias ? bf2f(bv[e]) : 0.f), act);
-      if (rope.cols) rope_pairs<8>(x, m, c, rope);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if (R) x[e] += bf2f(rv[e]);
-        o[e] = f2bf(x[e]);
-      }
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(x[e]);
     }
     *reinterpret_cast<bf16x8*>(C + (size_t)(compact_rows ? m - r0 : m) * ldc + c) = o;
+  }
+}
+
+// Row-per-wave reduce for a producer that must also emit its rows' statistics (sum, sum of
+// squares of the rounded outputs) for the next folded norm: the wave owns the whole row, so
+// the statistics are plain stores — no atomics.
+__global__ __launch_bounds__(256) void splitk_reduce_rows_kernel(const float* __restrict__ P, int splitk, int M,
+                                                                 int N, bf16* __restrict__ C, int ldc,
+                                                                 const bf16* __restrict__ bias,
+                                                                 const bf16* __restrict__ R, int ldr, int act,
+                                                                 float alpha, Epi ep, ReduceNorm nm) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const size_t slab = (size_t)M * N;
+  float s1 = 0.f, s2 = 0.f;
+  for (int c = lane * 8; c < N; c += 512) {
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < splitk; ++s) {
+      const f32x4* p = reinterpret_cast<const f32x4*>(P + s * slab + (size_t)m * N + c);
+      const f32x4 a = p[0], b = p[1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += a[e];
+        v[4 + e] += b[e];
+      }
+    }
+    float x[8];
+    reduce_finalize(x, v, m, c, bias, R, ldr, act, alpha, ep, nm);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = f2bf(x[e]);
+      const float y = bf2f(o[e]);
+      s1 += y;
+      s2 += y * y;
+    }
+    *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + c) = o;
+  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    ep.stats_out[2 * m] = s1;
+    ep.stats_out[2 * m + 1] = s2;
   }
 }
 
 template <class C>
 void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
             float ln_eps, const int* rows) {
+  const Epi ep{a.rope, a.stats_out, a.ext_stats};
   static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
   const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;
@@ -565,17 +686,23 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
 #define DLS_K(LN_, RG_)                                                                                           \
   hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
                      a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
-                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows, a.rope)
+                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows, ep)
   if (rows) DLS_K(0, 1);
-  else if (ln_mode != 0) {
+  else if (ln_mode != 0 && !a.ext_stats) {
     if constexpr (C::BM * C::BN <= 256 * 128) DLS_K(1, 0);  // 256x256 tiles have no registers left for it
   } else DLS_K(0, 0);
 #undef DLS_K
   if (splitk > 1) {
-    const int64_t nvec = (int64_t)a.M * (a.N / 8);
-    const int g = (int)std::min<int64_t>(2048, (nvec + 255) / 256);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, ws, splitk, a.M, a.N, (bf16*)a.C, a.ldc,
-                       (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows, a.compact_rows, a.rope);
+    const ReduceNorm nm{ln_colsum, a.ext_stats ? ln_mode : 0, ln_eps, a.K};
+    if (a.stats_out && !rows && a.act != kActSwiglu) {
+      hipLaunchKernelGGL(splitk_reduce_rows_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, ws, splitk, a.M, a.N,
+                         (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, ep, nm);
+    } else {
+      const int64_t nvec = (int64_t)a.M * (a.N / 8);
+      const int g = (int)std::min<int64_t>(2048, (nvec + 255) / 256);
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(g), dim3(256), 0, s, ws, splitk, a.M, a.N, (bf16*)a.C, a.ldc,
+                         (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows, a.compact_rows, ep, nm);
+    }
   }
 }
 
@@ -639,8 +766,8 @@ size_t gemm_glds_workspace_bytes(int M, int N, int splitk) { return splitk > 1 ?
 void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s, const float* ln_colsum,
                       int ln_mode, float ln_eps, const int* rows) {
   float* ws = static_cast<float*>(workspace);
-  if (ln_mode != 0) {
-    splitk = 1;  // row statistics need the whole K range in one block
+  if (ln_mode != 0 && !a.ext_stats) {
+    splitk = 1;  // in-kernel row statistics need the whole K range in one block
     if (kShapes[cfg < kNumCfg ? cfg : 3].bm * kShapes[cfg < kNumCfg ? cfg : 3].bn > 256 * 128) cfg = 0;
   }
 #define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows)

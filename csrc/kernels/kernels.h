@@ -33,6 +33,20 @@ struct GemmArgs {
   int compact_rows = 0;  // > 0 with a device row range [r0, r1): write output rows 0..r1-r0-1 (not r0..),
                          // and at most compact_rows of them (the output's row capacity)
   RopeArgs rope{};
+  // Row statistics hand-off between a residual-producing GEMM and the next folded norm:
+  // stats_out: fp32 [M][2] (zeroed by the caller) += (sum, sum of squares) of each FINAL
+  //            (bf16-rounded) output row — the producer's epilogue emits them for free;
+  // ext_stats: read them instead of accumulating them in the consumer's main loop (with
+  //            ln_mode 1/2 and ln_colsum: any tile config, split-K allowed).
+  float* stats_out = nullptr;
+  const float* ext_stats = nullptr;
+};
+
+// epilogue extras carried down to the tile code
+struct Epi {
+  RopeArgs rope;
+  float* stats_out;
+  const float* ext_stats;
 };
 
 int gemm_pick_config(int M, int N, int K);

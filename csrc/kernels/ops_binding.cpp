@@ -41,7 +41,8 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                 const c10::optional<at::Tensor>& ln_colsum, int64_t ln_mode, double ln_eps,
                 const c10::optional<at::Tensor>& rows, bool compact_rows,
                 const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin, int64_t rope_S,
-                int64_t rope_D, int64_t rope_cols) {
+                int64_t rope_D, int64_t rope_cols, const c10::optional<at::Tensor>& stats_out,
+                const c10::optional<at::Tensor>& ext_stats) {
   check_bf16(a_in, "A");
   check_bf16(w, "W");
   at::Tensor a = as2d(a_in);
@@ -91,6 +92,20 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
              bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1,
              (compact_rows && rows.has_value()) ? (int)c.size(0) : 0};
   TORCH_CHECK(!compact_rows || (rows.has_value() && !residual.has_value()), "compact_rows needs rows and no residual");
+  auto check_stats = [&](const at::Tensor& t, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == 2 * M, name,
+                " must be a contiguous fp32 [M][2] GPU tensor");
+  };
+  if (stats_out.has_value()) {
+    check_stats(*stats_out, "stats_out");
+    TORCH_CHECK(!swiglu && !rows.has_value(), "row statistics are emitted by plain (non-SwiGLU, full-row) GEMMs");
+    g.stats_out = stats_out->data_ptr<float>();
+  }
+  if (ext_stats.has_value()) {
+    check_stats(*ext_stats, "ext_stats");
+    TORCH_CHECK(ln_mode != 0, "ext_stats needs ln_mode (1 LayerNorm, 2 RMSNorm) and ln_colsum");
+    g.ext_stats = ext_stats->data_ptr<float>();
+  }
   if (rope_cols > 0) {
     TORCH_CHECK(rope_cos.has_value() && rope_sin.has_value() && rope_cos->scalar_type() == at::kFloat &&
                     rope_sin->scalar_type() == at::kFloat && rope_cos->is_contiguous() && rope_sin->is_contiguous() &&
@@ -113,7 +128,8 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                 "fused norm-GEMM needs fp32 ln_colsum [N]");
     csp = ln_colsum->data_ptr<float>();
   }
-  if (ln_mode != 0 || swiglu || rowp) {
+  if (ln_mode != 0 || swiglu || rowp || stats_out.has_value()) {
+    TORCH_CHECK(glds_ok, "this epilogue needs the LDS-DMA kernel (K % 64 == 0)");
     if (config >= kRegStage) config = -1;  // these epilogues live in the LDS-DMA kernel only
   }
   if (config >= kRegStage || !glds_ok) {
@@ -131,7 +147,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   TORCH_CHECK(cfg < gemm_glds_num_configs(), "unknown GEMM config ", cfg);
   const bool split_ok = (N % 8 == 0) && (c.stride(0) % 8 == 0) && (ldr % 8 == 0) && K % (64 * sk) == 0 &&
                         (!swiglu || N % 32 == 0);
-  if (!split_ok || ln_mode != 0) sk = 1;
+  if (!split_ok || (ln_mode != 0 && !ext_stats.has_value())) sk = 1;
   at::Tensor ws;
   if (sk > 1) ws = at::empty({(int64_t)gemm_glds_workspace_bytes((int)M, (int)N, sk) / 4}, a.options().dtype(at::kFloat));
   launch_gemm_glds(g, cfg, sk, sk > 1 ? ws.data_ptr() : nullptr, cur_stream(), csp, (int)ln_mode, (float)ln_eps,
@@ -366,7 +382,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1,
         py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5,
         py::arg("rows") = py::none(), py::arg("compact_rows") = false, py::arg("rope_cos") = py::none(),
-        py::arg("rope_sin") = py::none(), py::arg("rope_S") = 1, py::arg("rope_D") = 2, py::arg("rope_cols") = 0);
+        py::arg("rope_sin") = py::none(), py::arg("rope_S") = 1, py::arg("rope_D") = 2, py::arg("rope_cols") = 0,
+        py::arg("stats_out") = py::none(), py::arg("ext_stats") = py::none());
   m.attr("REGSTAGE") = kRegStage;
   m.def("gemm_pick_config", &gemm_pick_config);
   m.def("gemm_glds_num_configs", &gemm_glds_num_configs);

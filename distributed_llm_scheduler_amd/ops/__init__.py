@@ -192,7 +192,7 @@ def ref_rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t):
 # --------------------------------------------------------------------- dispatchers
 
 def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=None, rows_hint=None,
-           compact=False, rope=None):
+           compact=False, rope=None, stats_out=None):
     """``act(alpha * x @ w^T + bias) + residual`` — one MFMA GEMM kernel with the whole
     epilogue fused on GPU. ``act="swiglu"`` takes a gate/up-interleaved weight
     (:func:`interleave_gate_up`) and returns the N/2-wide ``silu(gate) * up``. ``rows``
@@ -200,7 +200,9 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
     ``out`` without a host sync (MoE experts); ``rows_hint`` is the expected row count used
     to pick the tuned kernel config; ``compact`` writes the range to rows 0..r1-r0-1 of ``out``
     (at most ``out.shape[0]`` rows). ``rope=(cos, sin, S, D, cols)`` rotates output columns
-    [0, cols) in the epilogue (q/k rows pair-interleaved, :func:`rope_pair_perm`)."""
+    [0, cols) in the epilogue (q/k rows pair-interleaved, :func:`rope_pair_perm`). ``stats_out``
+    (GPU, fp32 [M, 2], zeroed by the caller): accumulate each output row's (sum, sum of
+    squares) for the next folded norm (:func:`linear_norm` ``ext_stats``)."""
     a = ACT[act] if not isinstance(act, int) else act
     n_out = w.shape[0] // 2 if a == SWIGLU else w.shape[0]
     if _gpu(x):
@@ -209,7 +211,7 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
         cfg, sk = tuning.lookup(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
         rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
         y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact),
-                       rc, rs_, int(rS), int(rD), int(rcols))
+                       rc, rs_, int(rS), int(rD), int(rcols), stats_out, None)
         return y.view(shp) if out is None else out
     if rows is not None:
         r0, r1 = (int(v) for v in rows.tolist())
@@ -243,17 +245,22 @@ def derive_norm_gemm(w, ln_w, ln_b=None, bias=None):
     return wd, cs, b.to(w.dtype).contiguous()
 
 
-def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, residual=None, out=None, rope=None):
+def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, residual=None, out=None, rope=None,
+                ext_stats=None):
     """``act(W . norm(x) + bias) + residual`` in ONE GEMM on the raw rows ``x`` (GPU), with
     ``(w_derived, colsum, bias_derived)`` from :func:`derive_norm_gemm`. ``mode`` is
-    "layernorm" or "rmsnorm"."""
+    "layernorm" or "rmsnorm". Row statistics are accumulated in the GEMM's main loop, or —
+    with ``ext_stats`` (fp32 [M, 2] sums emitted by x's producer) — read from there, which
+    frees the tile config and split-K choice."""
     m = {"layernorm": 1, "rmsnorm": 2}[mode]
     a = ACT[act] if not isinstance(act, int) else act
     shp = x.shape[:-1] + (w_derived.shape[0] // 2 if a == SWIGLU else w_derived.shape[0],)
-    cfg, _ = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
+    cfg, sk = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
+    if ext_stats is None:
+        sk = 1
     rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
-    y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, 1, colsum, m,
-                   float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols))
+    y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, sk, colsum,
+                   m, float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols), None, ext_stats)
     return y.view(shp) if out is None else out
 
 

@@ -58,6 +58,7 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
 
 FOLD_MAX_K = 1024  # fold a preceding norm into the GEMM only up to this K (see DAGExecutor._gemm)
 GUARD_BYTES, GUARD_VALUE = 4096, 0xA5  # debug-mode canary after each arena slab
+STATS_HANDOFF = True  # producer GEMMs emit row statistics for the next folded norm (GPU)
 
 
 class DAGExecutor:
@@ -86,6 +87,9 @@ class DAGExecutor:
         self._inputs: Dict[str, torch.Tensor] = {}
         self._scratch_bufs: Dict[str, torch.Tensor] = {}
         self._moe_memo: Dict[tuple, object] = {}
+        self._stats_out: Dict[str, torch.Tensor] = {}   # producer output -> fp32 [M, 2] row stats it emits
+        self._ext_stats: Dict[str, torch.Tensor] = {}   # the same buffers, by the tensor a norm reads
+        self._stats_slab: Optional[torch.Tensor] = None
         self._moe_ptrs: Dict[tuple, torch.Tensor] = {}
         self._pending_sends: List[Tuple[int, int, object]] = []
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
@@ -137,6 +141,45 @@ class DAGExecutor:
                         M = math.prod(op.out_shape[:-1])
                         vocab = self.cfg.vocab_size if self.cfg is not None else 50257
                         self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
+        if self.gpu and STATS_HANDOFF:
+            self._plan_stats_handoff()
+
+    def _plan_stats_handoff(self) -> None:
+        """Pair every folded norm with the GEMM that produces its input on this rank: the
+        producer's epilogue emits each output row's (sum, sum of squares) into a small fp32
+        buffer (zeroed once per step), and the consumer GEMM reads them instead of
+        re-deriving them in its main loop — the norm then costs nothing at any K."""
+        producers = {ins.task: ins for ins in self.prog.instrs if ins.op == "run"}
+
+        def emits(ins) -> bool:
+            grp = [self.tasks[t] for t in ins.group]
+            lead_norm = grp[0].op.kind in ("layernorm", "rmsnorm") and len(grp) > 1
+            head = grp[1] if lead_norm else grp[0]
+            if head.op.kind in ("attention", "swiglu_mlp"):
+                return True
+            # a plain GEMM group writes its output with an un-folded, non-SwiGLU GEMM
+            return head.op.kind == "linear" and not lead_norm and head.op.attrs.get("act") != "swiglu"
+
+        need = []
+        for ins in self.prog.instrs:
+            if ins.op != "run":
+                continue
+            grp = [self.tasks[t] for t in ins.group]
+            if len(grp) > 1 and grp[0].op.kind in ("layernorm", "rmsnorm"):
+                src = grp[0].op.inputs[0]
+                pi = producers.get(src)
+                if pi is not None and emits(pi) and src not in need:
+                    need.append(src)
+        if not need:
+            return
+        rows = {t: math.prod(self.tasks[t].op.out_shape[:-1]) for t in need}
+        self._stats_slab = torch.zeros(sum(2 * r for r in rows.values()), dtype=torch.float32, device=self.device)
+        off = 0
+        for t in need:
+            buf = self._stats_slab[off:off + 2 * rows[t]]
+            self._stats_out[t] = buf
+            self._ext_stats[t] = buf
+            off += 2 * rows[t]
 
     def gemm_shapes(self):
         """(M, N, K) of every GEMM this rank's program launches (for autotuning)."""
@@ -282,17 +325,20 @@ class DAGExecutor:
         return W, d[0], d[1]
 
     def _gemm(self, x, w_name, b_name, norm: Optional[Task], act=None, residual=None, out=None, rope=None,
-              rope_perm=None):
+              rope_perm=None, stats_out=None):
         """One GEMM node, optionally with a preceding norm folded in (GPU, K <= FOLD_MAX_K:
         the in-kernel row statistics cost more than a separate norm pass at larger K and
         force split-K off; measured on MI355X, Llama-3-8B K=4096: 109 vs 45+8 us).
         ``act="swiglu"``: W is a [gate; up] weight, interleaved on first use. ``rope`` /
         ``rope_perm``: RoPE in the epilogue over pair-interleaved q/k rows."""
         sw = act == "swiglu"
-        if norm is not None and self.gpu and x.shape[-1] <= FOLD_MAX_K:
+        ext = self._ext_stats.get(norm.op.inputs[0]) if norm is not None else None
+        if norm is not None and self.gpu and (ext is not None or x.shape[-1] <= FOLD_MAX_K):
+            # folded norm: statistics handed over by x's producer (any K, split-K allowed), or
+            # accumulated in this GEMM's main loop (K <= FOLD_MAX_K)
             W, cs, bd = self._prep(w_name, norm, b_name, interleave=sw, rope_perm=rope_perm)
             return ops.linear_norm(x, W, cs, bd, norm.op.kind, norm.op.attrs.get("eps", 1e-5), act=act,
-                                   residual=residual, out=out, rope=rope)
+                                   residual=residual, out=out, rope=rope, ext_stats=ext)
         if norm is not None:
             nw = self._w(norm.op.weights["w"])
             xn = self._scratch("norm", x.shape)
@@ -305,7 +351,7 @@ class DAGExecutor:
             W, _, bias = self._prep(w_name, None, b_name, interleave=sw, rope_perm=rope_perm)
         else:
             W, bias = self._w(w_name), (self._w(b_name) if b_name else None)
-        return ops.linear(x, W, bias, act=act, residual=residual, out=out, rope=rope)
+        return ops.linear(x, W, bias, act=act, residual=residual, out=out, rope=rope, stats_out=stats_out)
 
     def _scratch(self, tag: str, shape) -> torch.Tensor:
         """Reusable per-rank buffer (allocated on first use, i.e. in an eager warm-up step,
@@ -385,6 +431,7 @@ class DAGExecutor:
             other = [d for d in tail.op.inputs if d != prod][0]
             residual = self._flat(self._x(other))
         act = "gelu" if any(t.op.kind == "gelu" for t in grp[1:]) else head.op.attrs.get("act")
+        st_out = self._stats_out.get(tail.id)  # this group's output feeds a folded norm: emit row stats
         a = head.op.attrs
         W = head.op.weights
         src = norm.op.inputs[0] if norm is not None else (head.op.inputs[0] if head.op.inputs else None)
@@ -404,7 +451,7 @@ class DAGExecutor:
             ops.gelu(self._x(src), out=out)
         elif k in ("linear", "lm_head"):
             self._gemm(self._flat(self._x(src)), W["w"], W.get("b"), norm, act=act, residual=residual,
-                       out=self._flat(out))
+                       out=self._flat(out), stats_out=st_out)
         elif k == "attention":
             x = self._flat(self._x(src))
             M = x.shape[0]
@@ -423,13 +470,13 @@ class DAGExecutor:
             ops.attention(qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:], B, S, nh, nkv,
                           D, causal=a.get("causal", True), out=o)
             ops.linear(o, self._w(W["w_o"]), self._w(W["b_o"]) if "b_o" in W else None, residual=residual,
-                       out=self._flat(out))
+                       out=self._flat(out), stats_out=st_out)
         elif k == "swiglu_mlp":
             x = self._flat(self._x(src))
             M, F = x.shape[0], a["ffn"]
             h = self._ws(0, (M, F))
             self._gemm(x, W["w_gate_up"], None, norm, act="swiglu", out=h)  # SwiGLU in the epilogue
-            ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out))
+            ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out), stats_out=st_out)
         elif k == "moe_expert":
             self._moe_expert(head, self._flat(out))
         elif k == "moe_combine":
@@ -459,6 +506,8 @@ class DAGExecutor:
         tr = self.trace
         self._pending_sends = []
         self._moe_memo = {}
+        if self._stats_slab is not None:
+            self._stats_slab.zero_()
         recv_work: Dict[str, Tuple[object, object]] = {}
         for i, ins in enumerate(self.prog.instrs):
             if tr:

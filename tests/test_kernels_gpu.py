@@ -322,3 +322,42 @@ def test_gemm_rope_epilogue(config, splitk):
     o_std = ops.ref_attention(*split(std), B, S, nh, nkv, D, causal=True)
     o_new = ops.ref_attention(*split(y.cpu()), B, S, nh, nkv, D, causal=True)
     _close(o_new, o_std.float(), 3e-2)
+
+
+@pytest.mark.parametrize("config,splitk", [(3, 1), (3, 3), (0, 1), (8, 2), (100, 1)])
+def test_gemm_emits_row_stats(config, splitk):
+    M, N, K = 300, 768, 768
+    x, w = _rand(M, K, seed=100), _rand(N, K, scale=0.05, seed=101)
+    b, r = _rand(N, scale=0.1, seed=102), _rand(M, N, seed=103)
+    st = torch.zeros(M, 2, dtype=torch.float32, device=DEV)
+    y = ops.ext().gemm(x, w, b, r, 0, 1.0, None, config, splitk, None, 0, 1e-5, None, False, None, None, 1, 2, 0,
+                       st, None)
+    torch.cuda.synchronize()
+    yf = y.cpu().float()
+    ref = torch.stack([yf.sum(1), (yf * yf).sum(1)], 1)
+    assert torch.allclose(st.cpu(), ref, rtol=1e-4, atol=1e-2), (st.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
+@pytest.mark.parametrize("config,splitk,act", [(3, 1, 0), (3, 4, 1), (0, 2, 0), (8, 1, 0), (12, 2, 0), (3, 1, 4)])
+def test_gemm_folded_norm_external_stats(mode, config, splitk, act):
+    M, N, K = 256, 1024, 2048
+    x = _rand(M, K, scale=2.0, seed=110) + 0.3
+    w = _rand(N, K, scale=0.03, seed=111)
+    nw = (1 + 0.2 * _rand(K, seed=112).float()).to(torch.bfloat16)
+    nb = _rand(K, scale=0.1, seed=113) if mode == "layernorm" else None
+    xf = x.cpu().float()
+    st = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).to(DEV)
+    xn = ops.ref_layernorm(x.cpu(), nw.cpu(), nb.cpu()) if mode == "layernorm" else ops.ref_rmsnorm(x.cpu(), nw.cpu())
+    wd, cs, bd = ops.derive_norm_gemm(w, nw, nb, None)
+    if act == 4:  # SwiGLU epilogue over the folded, interleaved weight
+        ref = _ref_swiglu(xn, w.cpu())
+        wd, cs = ops.interleave_gate_up(wd), ops.interleave_gate_up(cs)
+        bd = ops.interleave_gate_up(bd) if nb is not None else None
+    else:
+        ref = ops.ref_linear(xn, w.cpu(), act=act).float()
+        bd = bd if nb is not None else None
+    y = ops.ext().gemm(x, wd, bd, None, act, 1.0, None, config, splitk, cs, 1 if mode == "layernorm" else 2, 1e-5,
+                       None, False, None, None, 1, 2, 0, None, st)
+    torch.cuda.synchronize()
+    _close(y.cpu(), ref, 3e-2)
