@@ -431,6 +431,17 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
         for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
       }
     }
+    float csv[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(W') of this fragment's 4 columns (folded norm)
+    if (ln_mode != 0) {
+      if (full && (N % 4 == 0)) {
+        const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_colsum + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csv[e] = c4[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csv[e] = col + e < N ? ln_colsum[col + e] : 0.f;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
       const int row = m0 + wm * C::WTM + i * 16 + r16;
@@ -440,7 +451,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
         // W.LN(x) = rstd * (W' x - mu * colsum(W')) + (bias + W b), W' = W * ln_w (host-derived)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float cs = (col + e < N) ? ln_colsum[col + e] : 0.f;
+          const float cs = csv[e];
           v[e] = apply_act(ln_rs[i] * (acc[i][j][e] - ln_mu[i] * cs) + bv[e], act);
         }
       } else {
@@ -624,8 +635,24 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     } else {
       float x[8];
       reduce_finalize(x, v, m, c, bias, R, ldr, act, alpha, ep, nm);
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(x[e]);
+      for (int e = 0; e < 8; ++e) {
+        o[e] = f2bf(x[e]);
+        const float y = bf2f(o[e]);
+        s1 += y;
+        s2 += y * y;
+      }
+      if (ep.stats_out) {
+        // launched only when a wave's 64 consecutive items share one row (nv % 64 == 0 and
+        // the loop stride is a multiple of 64): one pair of atomics per wave
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if ((threadIdx.x & 63) == 0) {
+          atomicAdd(ep.stats_out + 2 * m, s1);
+          atomicAdd(ep.stats_out + 2 * m + 1, s2);
+        }
+      }
     }
     *reinterpret_cast<bf16x8*>(C + (size_t)(compact_rows ? m - r0 : m) * ldc + c) = o;
   }
@@ -694,7 +721,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
 #undef DLS_K
   if (splitk > 1) {
     const ReduceNorm nm{ln_colsum, a.ext_stats ? ln_mode : 0, ln_eps, a.K};
-    if (a.stats_out && !rows && a.act != kActSwiglu) {
+    if (a.stats_out && !rows && a.act != kActSwiglu && (a.N / 8) % 64 != 0) {  // small rows: a wave per row
       hipLaunchKernelGGL(splitk_reduce_rows_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, ws, splitk, a.M, a.N,
                          (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, ep, nm);
     } else {

@@ -21,6 +21,7 @@ per-GPU Gantt (same layout as the reference's simulated one, visu.py:206-248).
 from __future__ import annotations
 
 import math
+import os
 import time
 import zlib
 from dataclasses import dataclass, field
@@ -58,7 +59,8 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
 
 FOLD_MAX_K = 1024  # fold a preceding norm into the GEMM only up to this K (see DAGExecutor._gemm)
 GUARD_BYTES, GUARD_VALUE = 4096, 0xA5  # debug-mode canary after each arena slab
-STATS_HANDOFF = True  # producer GEMMs emit row statistics for the next folded norm (GPU)
+# producer GEMMs emit row statistics for the next folded norm (GPU); DLS_STATS_HANDOFF=0 disables
+STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
 
 
 class DAGExecutor:
@@ -168,7 +170,12 @@ class DAGExecutor:
             if len(grp) > 1 and grp[0].op.kind in ("layernorm", "rmsnorm"):
                 src = grp[0].op.inputs[0]
                 pi = producers.get(src)
-                if pi is not None and emits(pi) and src not in need:
+                # measured (MI355X, scripts/gpu_ab.sh): a win where the norm would otherwise be
+                # folded with main-loop statistics (K <= FOLD_MAX_K: GPT-2 0.857 -> 0.832 ms);
+                # at K = 4096 the separate norm kernel is cheaper than the split-K reduce
+                # epilogue work (Llama-3-8B 9.89 vs 9.96 ms)
+                width = self.tasks[src].op.out_shape[-1] if src in self.tasks else 0
+                if pi is not None and emits(pi) and src not in need and width <= FOLD_MAX_K:
                     need.append(src)
         if not need:
             return
