@@ -27,6 +27,16 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+// wait until at most `ahead` tiles (PW DMA instructions each) are still in flight
+template <int PW, int A>
+__device__ __forceinline__ void wait_tiles(int ahead) {
+  if constexpr (A <= 0) {
+    wait_vm<0>();
+  } else {
+    if (ahead >= A) wait_vm<PW * A>();
+    else wait_tiles<PW, A - 1>(ahead);
+  }
+}
 
 template <int D, int NW_, int ST_ = 2>
 struct AttnCfg {
@@ -137,8 +147,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     if (p < ntiles) issue(p);
   for (int t = 0; t < ntiles; ++t) {
     // tile t has landed once at most min(ST-2, tiles issued after t) tiles are in flight
-    if (ST == 3 && t + 1 < ntiles) wait_vm<C::PW>();
-    else wait_vm<0>();
+    wait_tiles<C::PW, ST - 2>(min(ST - 2, ntiles - 1 - t));
     raw_barrier();
     if (t + ST - 1 < ntiles) issue(t + ST - 1);  // into the buffer everyone finished in t-1
     const char* kb = smem + (t % ST) * C::BUF_BYTES;
@@ -249,6 +258,10 @@ static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
     case 2: launch_attn<D, 4, 2>(a, s); break;
     case 3: launch_attn<D, 2, 3>(a, s); break;
     case 4: launch_attn<D, 4, 3>(a, s); break;
+    // deep K/V rings: a causal row's whole key range (S=512, D=64) in flight at once
+    case 5: launch_attn<D, 4, 4>(a, s); break;
+    case 6: launch_attn<D, 4, (D == 64 ? 8 : 5)>(a, s); break;
+    case 7: launch_attn<D, 2, (D == 64 ? 8 : 5)>(a, s); break;
     default:
       // 64-query blocks, 2 K/V stages: fastest on every measured shape (GPT-2 / Llama-3-8B
       // S=512, batch 8, S=2048) once the softmax stopped being VALU-bound

@@ -412,26 +412,28 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     }
     return;
   }
-  float ps1[C::FM], ps2[C::FM];  // per-row partial (sum, sum of squares) of this lane's outputs
-#pragma unroll
-  for (int i = 0; i < C::FM; ++i) ps1[i] = ps2[i] = 0.f;
+  // Staged epilogue: each wave writes its finished fragments (bias, activation, folded norm,
+  // RoPE applied; bf16) into a tile image in LDS, then the block stores the tile as whole
+  // 16-B-per-lane row segments (residual add and row statistics on the way out). A lane's
+  // fragment holds only 4 columns (8 B) of 16 different rows, so storing fragments directly
+  // scatters 32-B pieces over 16 rows per instruction — partial lines that measured
+  // ~1.2 TB/s on the 51 MB LM-head output; full rows run at the HBM write rate.
+  constexpr int BNC = C::BN / 8;  // 16-B chunks per tile row; image chunk c of row r sits at c ^ (r & 7)
+  static_assert(BNC >= 8, "staged epilogue swizzle needs BN >= 64");
+  static_assert(C::BM * C::BN * 2 <= C::LDS_UNITS * 16, "output tile image must fit the staging LDS");
+  bf16* img = reinterpret_cast<bf16*>(smem);
+  __syncthreads();  // every wave is done with the staging buffers (and the norm statistics)
 #pragma unroll
   for (int j = 0; j < C::FN; ++j) {
-    const int col = n0 + wn * C::WTN + j * 16 + g4;
-    if (col >= N) continue;
-    const bool full = vec_ok && col + 3 < N;
+    const int cl = wn * C::WTN + j * 16 + g4;  // local column of this lane's 4 values
+    const int col = n0 + cl;
+    const bool full = col + 3 < N;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    float csv[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(W') of the 4 columns (folded norm)
     if (bias) {
-      if (full) {
-        const bf16x4 b4 = *reinterpret_cast<const bf16x4*>(bias + col);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = bf2f(b4[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
-      }
+      for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
     }
-    float csv[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(W') of this fragment's 4 columns (folded norm)
     if (ln_mode != 0) {
       if (full && (N % 4 == 0)) {
         const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_colsum + col);
@@ -444,70 +446,72 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
-      const int row = m0 + wm * C::WTM + i * 16 + r16;
-      if (row >= M) continue;
+      const int rl = wm * C::WTM + i * 16 + r16;
       float v[4];
       if (ln_mode != 0) {
         // W.LN(x) = rstd * (W' x - mu * colsum(W')) + (bias + W b), W' = W * ln_w (host-derived)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float cs = csv[e];
-          v[e] = apply_act(ln_rs[i] * (acc[i][j][e] - ln_mu[i] * cs) + bv[e], act);
-        }
+        for (int e = 0; e < 4; ++e) v[e] = apply_act(ln_rs[i] * (acc[i][j][e] - ln_mu[i] * csv[e]) + bv[e], act);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = apply_act(alpha * acc[i][j][e] + bv[e], act);
       }
-      if (rope.cols) rope_pairs<4>(v, row, col, rope);
-      if (full) {
+      if (rope.cols) rope_pairs<4>(v, m0 + rl, col, rope);
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+      *reinterpret_cast<bf16x4*>(img + rl * C::BN + (((cl >> 3) ^ (rl & 7)) << 3) + (cl & 7)) = o;
+    }
+  }
+  __syncthreads();
+  const bool v16 = ((reinterpret_cast<uintptr_t>(Cp) | ((uintptr_t)ldc * 2)) & 15) == 0 &&
+                   (!R || ((reinterpret_cast<uintptr_t>(R) | ((uintptr_t)ldr * 2)) & 15) == 0);
+  const bf16x8* img8 = reinterpret_cast<const bf16x8*>(img);
+  const int tid_ = threadIdx.x;
+  // consecutive groups of BNC threads own one tile row per pass (C::T % BNC == 0)
+#pragma unroll 2
+  for (int q = tid_; q < C::BM * BNC; q += C::T) {
+    const int rl = q / BNC, cc = q % BNC;
+    const int row = m0 + rl, col = n0 + cc * 8;
+    bf16x8 o = img8[rl * BNC + (cc ^ (rl & 7))];
+    float s1 = 0.f, s2 = 0.f;
+    if (row < M && col < N) {
+      if (v16 && col + 8 <= N) {
         if (R) {
-          const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(R + (size_t)row * ldr + col);
+          const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(R + (size_t)row * ldr + col);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += bf2f(r4[e]);
+          for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(o[e]) + bf2f(r8[e]));
         }
-        bf16x4 o;
+        *reinterpret_cast<bf16x8*>(Cp + (size_t)row * ldc + col) = o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-        *reinterpret_cast<bf16x4*>(Cp + (size_t)row * ldc + col) = o;
-        if (ep.stats_out) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float y = bf2f(o[e]);
-            ps1[i] += y;
-            ps2[i] += y * y;
-          }
+        for (int e = 0; e < 8; ++e) {
+          const float y = bf2f(o[e]);
+          s1 += y;
+          s2 += y * y;
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 8; ++e) {
           if (col + e >= N) continue;
-          float x = v[e];
+          float x = bf2f(o[e]);
           if (R) x += bf2f(R[(size_t)row * ldr + col + e]);
           const bf16 ob = f2bf(x);
           Cp[(size_t)row * ldc + col + e] = ob;
-          if (ep.stats_out) {
-            const float y = bf2f(ob);
-            ps1[i] += y;
-            ps2[i] += y * y;
-          }
+          const float y = bf2f(ob);
+          s1 += y;
+          s2 += y * y;
         }
       }
     }
-  }
-  if (ep.stats_out) {
-    // the 4 lane groups of a fragment row hold disjoint columns: fold them, then one pair of
-    // atomics per (row, wave) into the caller-zeroed [M][2] buffer
+    if (ep.stats_out) {
 #pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      float a = ps1[i], q = ps2[i];
-      a += __shfl_xor(a, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      const int row = m0 + wm * C::WTM + i * 16 + r16;
-      if (lane < 16 && row < M) {
-        atomicAdd(ep.stats_out + 2 * row, a);
-        atomicAdd(ep.stats_out + 2 * row + 1, q);
+      for (int o_ = 1; o_ < BNC; o_ <<= 1) {
+        s1 += __shfl_xor(s1, o_, 64);
+        s2 += __shfl_xor(s2, o_, 64);
+      }
+      if (cc == 0 && row < M) {
+        atomicAdd(ep.stats_out + 2 * row, s1);
+        atomicAdd(ep.stats_out + 2 * row + 1, s2);
       }
     }
   }
