@@ -38,21 +38,28 @@ __device__ __forceinline__ void wait_tiles(int ahead) {
   }
 }
 
-template <int D, int NW_, int ST_ = 2>
+template <int D, int NW_, int ST_ = 2, int KS_ = 1>
 struct AttnCfg {
-  static constexpr int NW = NW_;                 // waves per block (16 queries each)
+  static constexpr int NW = NW_;                 // query waves per block (16 queries each)
+  static constexpr int KS = KS_;                 // key halves per stage: KS wave groups split each stage's keys
+  static constexpr int NWT = NW * KS;            // waves per block
   static constexpr int ST = ST_;                 // K/V stages (ST-1 tiles in flight)
   static constexpr int QB = 16 * NW;             // queries per block
-  static constexpr int KT = 64;                  // keys per tile
+  static constexpr int KT = 64;                  // keys per wave per stage
+  static constexpr int KTS = KT * KS;            // keys per stage
   static constexpr int RB = D * 2;               // bytes per K/V row
   static constexpr int CH = D / 8;               // 16-B chunks per row
   static constexpr int ROWS_PER_INSTR = 1024 / RB;
-  static constexpr int INSTR = KT / ROWS_PER_INSTR;  // per operand per tile
-  static constexpr int PW = 2 * INSTR / NW;           // per wave per tile (K and V)
-  static constexpr int TILE_BYTES = KT * RB;          // one operand
+  static constexpr int INSTR = KTS / ROWS_PER_INSTR;  // per operand per stage
+  static constexpr int PW = 2 * INSTR / NWT;          // per wave per stage (K and V)
+  static constexpr int TILE_BYTES = KTS * RB;         // one operand
   static constexpr int BUF_BYTES = 2 * TILE_BYTES;    // K + V
   static constexpr int NQK = D / 32;                  // k-steps of S^T
   static constexpr int ND = D / 16;                   // output d-subtiles
+  static constexpr int MERGE_BYTES = KS > 1 ? NW * 64 * (ND * 4 + 2) * 4 : 0;
+  static constexpr int SMEM = ST * BUF_BYTES > MERGE_BYTES ? ST * BUF_BYTES : MERGE_BYTES;
+  static_assert(PW * (ST - 2) <= 63 && PW * NWT == 2 * INSTR, "DMA split");
+  static_assert(SMEM <= 163840, "LDS budget");
 };
 
 __device__ __forceinline__ int swz(int row, int ch_mask) { return row & ch_mask; }
@@ -76,34 +83,38 @@ __device__ __forceinline__ float xlane(float x) {
   return MAX ? fmaxf(a, b) : a + b;
 }
 
-template <int D, int NW, int ST>
-__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restrict__ Q, int ldq,
+template <int D, int NW, int ST, int KS>
+__global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __restrict__ Q, int ldq,
                                                        const bf16* __restrict__ Kp, int ldk,
                                                        const bf16* __restrict__ Vp, int ldv, bf16* __restrict__ O,
                                                        int ldo, int S, int n_head, int n_kv_head, float scale_log2,
-                                                       int causal, int n_qtiles) {
-  using C = AttnCfg<D, NW, ST>;
-  __shared__ __attribute__((aligned(16))) char smem[ST * C::BUF_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                                       int causal, int n_qtiles, int Sq, int q_off) {
+  using C = AttnCfg<D, NW, ST, KS>;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave_id = tid >> 6;
+  // KS > 1: wave group hg takes keys [hg*64, hg*64+64) of every stage (the causal row's key
+  // range is walked by KS independent online-softmax chains, merged through LDS at the end)
+  const int wave = wave_id % NW, hg = wave_id / NW;
   const int g = lane >> 4, li = lane & 15;
   const int qt = causal ? (n_qtiles - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heaviest first
   const int h = blockIdx.y, b = blockIdx.z;
   const int kvh = h / (n_head / n_kv_head);
-  const int q0 = qt * C::QB + wave * 16;  // this wave's 16 queries
-  const size_t tok0 = (size_t)b * S;
+  const int q0 = qt * C::QB + wave * 16;  // this wave's 16 queries (local rows of the q chunk)
+  const size_t tok0 = (size_t)b * S;       // first key row of this batch
+  const size_t qtok0 = (size_t)b * Sq;     // first query / output row of this batch
 
   // Q^T as the B operand: lane holds Q[q0 + li][32*ks + 8*g + j]
   bf16x8 qf[C::NQK];
   {
-    const int qrow = min(q0 + li, S - 1);
+    const int qrow = min(q0 + li, Sq - 1);
 #pragma unroll
     for (int ks = 0; ks < C::NQK; ++ks)
-      qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (tok0 + qrow) * ldq + h * D + 32 * ks + 8 * g);
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (qtok0 + qrow) * ldq + h * D + 32 * ks + 8 * g);
   }
 
   // LDS-DMA source pointers: instruction j of this wave -> operand (K or V) rows
-  const int kv_end = causal ? min(S, qt * C::QB + C::QB) : S;
-  const int ntiles = (kv_end + C::KT - 1) / C::KT;
+  const int kv_end = causal ? min(S, q_off + qt * C::QB + C::QB) : S;
+  const int ntiles = (kv_end + C::KTS - 1) / C::KTS;
   // per-lane DMA sources, computed once: instruction j of this wave covers operand op's
   // rows r0..r0+ROWS_PER_INSTR-1 of every tile; a tile only moves the base by KT rows.
   // Rows past S (the last tile) are clamped to S-1 (their scores are masked to -inf).
@@ -112,7 +123,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
   size_t dstep[C::PW];
 #pragma unroll
   for (int j = 0; j < C::PW; ++j) {
-    const int ins = wave * C::PW + j;            // 0 .. 2*INSTR-1
+    const int ins = wave_id * C::PW + j;         // 0 .. 2*INSTR-1
     const int op = ins / C::INSTR;               // 0 = K, 1 = V
     const int r0 = (ins % C::INSTR) * C::ROWS_PER_INSTR;
     const int row = r0 + lane / C::CH;
@@ -123,13 +134,13 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     drow[j] = row;
     doff[j] = op * C::TILE_BYTES + r0 * C::RB;
   }
-  const bool tail_clamp = (S % C::KT) != 0;
+  const bool tail_clamp = (S % C::KTS) != 0;
   auto issue = [&](int t) {
     char* buf = smem + (t % ST) * C::BUF_BYTES;
-    const bool clamp = tail_clamp && (t + 1) * C::KT > S;
+    const bool clamp = tail_clamp && (t + 1) * C::KTS > S;
 #pragma unroll
     for (int j = 0; j < C::PW; ++j) {
-      int key = t * C::KT + drow[j];
+      int key = t * C::KTS + drow[j];
       if (clamp) key = min(key, S - 1);
       __builtin_amdgcn_global_load_lds((const void*)(dsrc[j] + (size_t)key * dstep[j]),
                                        (__attribute__((address_space(3))) void*)(buf + doff[j]), 16, 0, 0);
@@ -140,7 +151,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 #pragma unroll
   for (int i = 0; i < C::ND; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;  // for query q0 + li (replicated over the 4 lane groups)
-  const int my_q = q0 + li;
+  const int my_q = q0 + li;         // local query row
+  const int gq = q_off + my_q;       // its global position (causal mask)
 
 #pragma unroll
   for (int p = 0; p < ST - 1; ++p)
@@ -150,9 +162,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     wait_tiles<C::PW, ST - 2>(min(ST - 2, ntiles - 1 - t));
     raw_barrier();
     if (t + ST - 1 < ntiles) issue(t + ST - 1);  // into the buffer everyone finished in t-1
-    const char* kb = smem + (t % ST) * C::BUF_BYTES;
+    const char* kb = smem + (t % ST) * C::BUF_BYTES + hg * C::KT * C::RB;
     const char* vb = kb + C::TILE_BYTES;
-    const int key0 = t * C::KT;
+    const int key0 = t * C::KTS + hg * C::KT;
 
     // ---- S^T = K Q^T : 4 key-subtiles x 16 queries
     f32x4 s[4];
@@ -170,14 +182,14 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
     // ---- online softmax for query my_q; scores s[n][i] <-> key key0 + 16n + 4g + i.
     // Raw scores are kept; the scale is folded into the exponent: p = 2^(s*c - m*c).
     // Masks only on the wave's diagonal tile and the ragged last tile (wave-uniform branch).
-    const bool masked = (key0 + C::KT > S) || (causal && key0 + C::KT - 1 > q0);
+    const bool masked = (key0 + C::KT > S) || (causal && key0 + C::KT - 1 > q_off + q0);
     if (masked) {
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = key0 + 16 * n + 4 * g + i;
-          if (key >= S || (causal && key > my_q)) s[n][i] = -INFINITY;
+          if (key >= S || (causal && key > gq)) s[n][i] = -INFINITY;
         }
     }
     float mx = fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3]));
@@ -225,10 +237,43 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
       }
     }
   }
+  if constexpr (KS > 1) {
+    // merge the key-half chains: group hg > 0 publishes (o, m, l), group 0 rescales and sums
+    __syncthreads();  // all DMA landed and every wave is done with the K/V buffers
+    float* mg = reinterpret_cast<float*>(smem);
+    constexpr int REC = C::ND * 4 + 2;
+    for (int h2 = 1; h2 < KS; ++h2) {
+      if (hg == h2) {
+        float* r = mg + (wave * 64 + lane) * REC;
+#pragma unroll
+        for (int dn = 0; dn < C::ND; ++dn)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) r[dn * 4 + i] = o[dn][i];
+        r[C::ND * 4] = m_run;
+        r[C::ND * 4 + 1] = l_run;
+      }
+      __syncthreads();
+      if (hg == 0) {
+        const float* r = mg + (wave * 64 + lane) * REC;
+        const float m1 = r[C::ND * 4], l1 = r[C::ND * 4 + 1];
+        const float mm = fmaxf(fmaxf(m_run, m1), -1e30f);
+        const float a0 = __builtin_amdgcn_exp2f((m_run - mm) * scale_log2);
+        const float a1 = __builtin_amdgcn_exp2f((m1 - mm) * scale_log2);
+        l_run = l_run * a0 + l1 * a1;
+        m_run = mm;
+#pragma unroll
+        for (int dn = 0; dn < C::ND; ++dn)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[dn][i] = o[dn][i] * a0 + r[dn * 4 + i] * a1;
+      }
+      if (h2 + 1 < KS) __syncthreads();
+    }
+    if (hg != 0) return;
+  }
   // ---- normalise and store O[q][d]: lane holds d = 16dn + 4g + i for query my_q
-  if (my_q < S) {
+  if (my_q < Sq) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-    bf16* orow = O + (tok0 + my_q) * ldo + h * D;
+    bf16* orow = O + (qtok0 + my_q) * ldo + h * D;
 #pragma unroll
     for (int dn = 0; dn < C::ND; ++dn) {
       bf16x4 v;
@@ -241,14 +286,16 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(const bf16* __restric
 
 }  // namespace
 
-template <int D, int NW, int ST>
+template <int D, int NW, int ST, int KS = 1>
 static void launch_attn(const AttnArgs& a, hipStream_t s) {
-  const int nq = (a.S + 16 * NW - 1) / (16 * NW);
-  dim3 grid(nq, a.n_head, a.B), block(64 * NW);
+  const int Sq = a.Sq > 0 ? a.Sq : a.S;
+  const int nq = (Sq + 16 * NW - 1) / (16 * NW);
+  dim3 grid(nq, a.n_head, a.B), block(64 * NW * KS);
   const float sl2 = a.scale * 1.4426950408889634f;
-  hipLaunchKernelGGL((attn_fwd_kernel<D, NW, ST>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NW, ST, KS>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
                      static_cast<const bf16*>(a.k), a.ldk, static_cast<const bf16*>(a.v), a.ldv,
-                     static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq);
+                     static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq, Sq,
+                     a.Sq > 0 ? a.q_off : 0);
 }
 
 template <int D>
@@ -262,10 +309,22 @@ static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
     case 5: launch_attn<D, 4, 4>(a, s); break;
     case 6: launch_attn<D, 4, (D == 64 ? 8 : 5)>(a, s); break;
     case 7: launch_attn<D, 2, (D == 64 ? 8 : 5)>(a, s); break;
-    default:
-      // 64-query blocks, 2 K/V stages: fastest on every measured shape (GPT-2 / Llama-3-8B
-      // S=512, batch 8, S=2048) once the softmax stopped being VALU-bound
-      launch_attn<D, 4, 2>(a, s);
+    // key-split stages: two online-softmax chains per query group (shorter dependent chain
+    // per wave, two waves per SIMD) merged in LDS
+    case 8: launch_attn<D, 4, 2, 2>(a, s); break;
+    case 9: launch_attn<D, 2, 2, 2>(a, s); break;
+    case 10: launch_attn<D, 2, (D == 64 ? 3 : 2), 2>(a, s); break;
+    case 11: launch_attn<D, 1, (D == 64 ? 4 : 2), 2>(a, s); break;
+    default: {
+      // 64-query blocks, 2 K/V stages fill the chip from ~320 blocks on (batch 8, S=2048);
+      // below that the causal row's dependent chain is the kernel time, so split each stage's
+      // keys over two wave groups (GPT-2 S=512: 96 blocks, 8.2 -> 6.2 us with 32-query blocks;
+      // Llama-3-8B S=512: 256 blocks, 13.1 -> 11.9 us)
+      const long blocks = (long)(((a.Sq > 0 ? a.Sq : a.S) + 63) / 64) * a.n_head * a.B;
+      if (blocks <= 128) launch_attn<D, 2, 2, 2>(a, s);
+      else if (blocks <= 320) launch_attn<D, 4, 2, 2>(a, s);
+      else launch_attn<D, 4, 2>(a, s);
+    }
   }
 }
 

@@ -531,6 +531,19 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
                                                          int compact_rows, Epi ep) {
   __shared__ bf16x8 smem[C::LDS_UNITS];
   const int ntile = tiles_m * tiles_n;
+  if constexpr (RANGED == 2) {
+    // persistent: a resident grid walks the tiles; tile t+1's first K-tiles are issued right
+    // behind tile t's epilogue stores, so the store drain overlaps the next load latency
+    // instead of holding the CU (one block per CU cannot overlap them across blocks)
+    const int total = ntile * splitk;
+    for (int L = blockIdx.x, it = 0; L < total; L += gridDim.x, ++it) {
+      if (it) raw_barrier();  // every wave is done reading the previous tile's output image
+      const int ks = L / ntile, tile = L % ntile;
+      glds_tile<C, LN>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice,
+                       tile % tiles_m, tile / tiles_m, ln_colsum, (LN || ep.ext_stats) ? ln_mode : 0, ln_eps, ep);
+    }
+    return;
+  }
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
   const int ks = bid / ntile, tile = bid % ntile;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
@@ -706,20 +719,46 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows_kernel(const float* __
   }
 }
 
+// resident blocks of a persistent launch: CUs x blocks per CU (occupancy query, cached)
+template <class C, int LN>
+int persistent_grid() {
+  static int g = 0;
+  if (!g) {
+    int dev = 0, cus = 256, per = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gemm_glds_kernel<C, LN, 2>, C::T, 0);
+    g = cus * (per > 0 ? per : 1);
+  }
+  return g;
+}
+
 template <class C>
 void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
-            float ln_eps, const int* rows) {
+            float ln_eps, const int* rows, bool persist) {
   const Epi ep{a.rope, a.stats_out, a.ext_stats};
   static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
   const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;
-  dim3 grid(tiles_m * tiles_n * splitk), block(C::T);
+  const int total = tiles_m * tiles_n * splitk;
+  dim3 grid(total), block(C::T);
 #define DLS_K(LN_, RG_)                                                                                           \
   hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
                      a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
                      a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows, ep)
+  const bool ln_in = ln_mode != 0 && !a.ext_stats;
   if (rows) DLS_K(0, 1);
-  else if (ln_mode != 0 && !a.ext_stats) {
+  else if (persist) {
+    if (ln_in) {
+      if constexpr (C::BM * C::BN <= 256 * 128) {
+        grid = dim3(std::min(total, persistent_grid<C, 1>()));
+        DLS_K(1, 2);
+      }
+    } else {
+      grid = dim3(std::min(total, persistent_grid<C, 0>()));
+      DLS_K(0, 2);
+    }
+  } else if (ln_in) {
     if constexpr (C::BM * C::BN <= 256 * 128) DLS_K(1, 0);  // 256x256 tiles have no registers left for it
   } else DLS_K(0, 0);
 #undef DLS_K
@@ -797,11 +836,13 @@ size_t gemm_glds_workspace_bytes(int M, int N, int splitk) { return splitk > 1 ?
 void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s, const float* ln_colsum,
                       int ln_mode, float ln_eps, const int* rows) {
   float* ws = static_cast<float*>(workspace);
+  const bool persist = cfg >= kGemmPersist && !rows;
+  cfg &= kGemmPersist - 1;
   if (ln_mode != 0 && !a.ext_stats) {
     splitk = 1;  // in-kernel row statistics need the whole K range in one block
     if (kShapes[cfg < kNumCfg ? cfg : 3].bm * kShapes[cfg < kNumCfg ? cfg : 3].bn > 256 * 128) cfg = 0;
   }
-#define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows)
+#define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist)
   switch (cfg) {
     case 0: DLS_L(C0); break;
     case 1: DLS_L(C1); break;

@@ -54,6 +54,9 @@ void launch_gemm_bf16(const GemmArgs& a, hipStream_t s);  // register-staged, an
 
 // LDS-DMA multistage GEMM (K % 64 == 0); split-K partials need workspace_bytes of fp32
 int gemm_glds_num_configs();
+// cfg | kGemmPersist: the same tile config as a persistent launch (a resident grid walks the
+// tiles; one tile's store drain overlaps the next tile's first loads)
+constexpr int kGemmPersist = 32;
 void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk);
 size_t gemm_glds_workspace_bytes(int M, int N, int splitk);
 // ln_mode: 0 none, 1 LayerNorm, 2 RMSNorm folded into the GEMM (A = raw input rows,
@@ -72,7 +75,12 @@ struct AttnArgs {
   int B, S, n_head, n_kv_head, D;
   float scale;
   int causal;
-  int variant = 0;  // 0 auto; 1..4 = (waves, K/V stages) (2,2) (4,2) (2,3) (4,3) — benchmarks/tuning
+  int variant = 0;  // 0 auto; 1..11 fixed (waves, K/V stages, key split) — benchmarks/tuning
+  // Sequence-chunked attention (context parallelism as a DAG): q holds Sq query rows per
+  // batch at global positions q_off .. q_off+Sq-1; k/v hold S key rows per batch (positions
+  // 0 .. S-1). Sq = 0 means Sq = S, q_off = 0 (ordinary self-attention).
+  int Sq = 0;
+  int q_off = 0;
 };
 void launch_attention_fwd(const AttnArgs& a, hipStream_t s);
 

@@ -144,7 +144,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
     if (cfg < 0) cfg = acfg;
     if (sk <= 0) sk = ask;
   }
-  TORCH_CHECK(cfg < gemm_glds_num_configs(), "unknown GEMM config ", cfg);
+  TORCH_CHECK((cfg & (kGemmPersist - 1)) < gemm_glds_num_configs() && cfg < 2 * kGemmPersist, "unknown GEMM config ", cfg);
   const bool split_ok = (N % 8 == 0) && (c.stride(0) % 8 == 0) && (ldr % 8 == 0) && K % (64 * sk) == 0 &&
                         (!swiglu || N % 32 == 0);
   if (!split_ok || (ln_mode != 0 && !ext_stats.has_value())) sk = 1;
@@ -157,22 +157,25 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
 
 at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
                      int64_t n_head, int64_t n_kv_head, int64_t head_dim, bool causal, double scale,
-                     const c10::optional<at::Tensor>& out, int64_t variant) {
+                     const c10::optional<at::Tensor>& out, int64_t variant, int64_t Sq, int64_t q_off) {
+  if (Sq <= 0) Sq = S;
+  TORCH_CHECK(q_off >= 0 && (!causal || q_off + Sq <= S), "query chunk must lie inside the key range");
   for (auto* p : {&q, &k, &v}) {
     check_bf16(*p, "qkv");
     check_rows(*p, "qkv");
-    TORCH_CHECK(p->size(0) == B * S, "q/k/v must have B*S rows");
+    TORCH_CHECK(p->size(0) == B * (p == &q ? Sq : S), "q must have B*Sq rows and k/v B*S rows");
   }
   TORCH_CHECK(head_dim == 64 || head_dim == 128, "head_dim must be 64 or 128");
   TORCH_CHECK(n_head % n_kv_head == 0, "n_head must be a multiple of n_kv_head");
   TORCH_CHECK(q.size(1) >= n_head * head_dim && k.size(1) >= n_kv_head * head_dim &&
                   v.size(1) >= n_kv_head * head_dim,
               "q/k/v column extent too small for the head layout");
-  at::Tensor o = out.has_value() ? as2d(*out) : at::empty({B * S, n_head * head_dim}, q.options());
+  at::Tensor o = out.has_value() ? as2d(*out) : at::empty({B * Sq, n_head * head_dim}, q.options());
   check_rows(o, "out");
+  TORCH_CHECK(o.size(0) == B * Sq && o.size(1) >= n_head * head_dim, "out must be [B*Sq, >= n_head*head_dim]");
   AttnArgs a{q.data_ptr(), (int)q.stride(0), k.data_ptr(), (int)k.stride(0), v.data_ptr(), (int)v.stride(0),
              o.data_ptr(), (int)o.stride(0), (int)B, (int)S, (int)n_head, (int)n_kv_head, (int)head_dim,
-             (float)scale, causal ? 1 : 0, (int)variant};
+             (float)scale, causal ? 1 : 0, (int)variant, (int)Sq, (int)q_off};
   launch_attention_fwd(a, cur_stream());
   return o;
 }
@@ -385,6 +388,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rope_sin") = py::none(), py::arg("rope_S") = 1, py::arg("rope_D") = 2, py::arg("rope_cols") = 0,
         py::arg("stats_out") = py::none(), py::arg("ext_stats") = py::none());
   m.attr("REGSTAGE") = kRegStage;
+  m.attr("PERSIST") = kGemmPersist;
   m.def("gemm_pick_config", &gemm_pick_config);
   m.def("gemm_glds_num_configs", &gemm_glds_num_configs);
   m.def("gemm_glds_pick", [](int M, int N, int K) {
@@ -394,7 +398,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("attention", &attention, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"),
         py::arg("n_head"), py::arg("n_kv_head"), py::arg("head_dim"), py::arg("causal") = true,
-        py::arg("scale") = 0.125, py::arg("out") = py::none(), py::arg("variant") = 0);
+        py::arg("scale") = 0.125, py::arg("out") = py::none(), py::arg("variant") = 0, py::arg("Sq") = 0,
+        py::arg("q_off") = 0);
   m.def("norm", &norm, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5,
         py::arg("residual") = py::none(), py::arg("rms") = false, py::arg("out") = py::none(),
         py::arg("sum_out") = py::none());

@@ -30,9 +30,10 @@ def build_dag(cfg: ModelConfig, batch: int = 1, seq: int = 512, cost_model: str 
 
 
 def build(model: str, batch: int = 1, seq: int = 512, replicas: int = 1, cost_model: str = "bytes",
-          tp: int = 1) -> Tuple[List[Task], Dict[str, ParamGroup], ModelConfig]:
+          tp: int = 1, sp: int = 1) -> Tuple[List[Task], Dict[str, ParamGroup], ModelConfig]:
     """``replicas`` independent requests (task ids prefixed ``r{k}/``) sharing weights;
-    ``tp > 1`` splits every layer into tensor-parallel shards (models/transforms.py)."""
+    ``tp > 1`` splits every layer into tensor-parallel shards, ``sp > 1`` every token-wise
+    node into sequence chunks (models/transforms.py)."""
     cfg = get_config(model)
     tasks: List[Task] = []
     for r in range(replicas):
@@ -41,4 +42,9 @@ def build(model: str, batch: int = 1, seq: int = 512, replicas: int = 1, cost_mo
     if tp > 1:
         from .transforms import tensor_parallel
         tasks, groups = tensor_parallel(tasks, groups, cfg, tp)
+    if sp > 1:
+        if tp > 1:
+            raise ValueError("combine sequence and tensor parallelism through separate DAGs (not both)")
+        from .transforms import sequence_parallel
+        tasks, groups = sequence_parallel(tasks, groups, cfg, sp)
     return tasks, groups, cfg

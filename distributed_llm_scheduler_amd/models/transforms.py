@@ -204,3 +204,79 @@ def tensor_parallel(tasks: List[Task], groups: Dict[str, ParamGroup], cfg: Model
     used = set().union(*[t.params_needed for t in final])
     new_groups = {pid: g for pid, g in new_groups.items() if pid in used}
     return final, new_groups
+
+
+def sequence_parallel(tasks: List[Task], groups: Dict[str, ParamGroup], cfg: ModelConfig, degree: int
+                      ) -> Tuple[List[Task], Dict[str, ParamGroup]]:
+    """Sequence (context) parallelism as a DAG transform: every token-wise node is split into
+    ``degree`` sequence chunks (chunk c = positions [c*S/P, (c+1)*S/P) of every sequence, all
+    batch rows), so a scheduler can place the chunks of one long request on different GPUs.
+
+    Only attention mixes positions. Each attention node becomes, per chunk c,
+
+    * ``...attention.qkv.sp{c}`` (``qkv_proj``) — the QKV projection of chunk c's rows (RoPE at
+      the chunk's absolute positions), and
+    * ``...attention.sp{c}`` (``attn_sp``) — chunk c's queries against the keys/values of
+      chunks 0..c (causal; all chunks otherwise), then the output projection.
+
+    So the K/V of chunk j flow along DAG edges qkv.sp{j} -> attention.sp{c>=j}: placed on
+    different GPUs those edges are RCCL point-to-point transfers — ring attention expressed
+    as DAG edges (SURVEY §2.3 "SP / CP", §5 "Long-context"). Weights are shared, so the
+    transformed DAG is numerically the same model (the chunks' outputs concatenate to it).
+    """
+    P = degree
+    if P <= 1:
+        return tasks, groups
+    owner = {s.name: pid for pid, g in groups.items() for s in g.tensors}
+    ids = {t.id for t in tasks}
+    out: List[Task] = []
+
+    def chunk_id(name: str, c: int) -> str:
+        return f"{name}.sp{c}" if name in ids else name  # external inputs (token ids) stay whole
+
+    for t in tasks:
+        if t.op is None or not t.op.out_shape or len(t.op.out_shape) != 3:
+            raise ValueError(f"sequence_parallel: task {t.id} has no [B, S, X] output")
+        B, S, X = t.op.out_shape
+        if S % P:
+            raise ValueError(f"sequence_parallel: degree {P} must divide the sequence length {S}")
+        Sc = S // P
+        kind = t.op.kind
+        if kind == "attention":
+            a = t.op.attrs
+            nh, nkv, D = a["n_head"], a["n_kv_head"], a["head_dim"]
+            width = (nh + 2 * nkv) * D
+            wq = {k: v for k, v in t.op.weights.items() if k in ("w_qkv", "b_qkv")}
+            wo = {k: v for k, v in t.op.weights.items() if k in ("w_o", "b_o")}
+            pq = {owner[v] for v in wq.values()}
+            po = {owner[v] for v in wo.values()}
+            M = B * Sc
+            qkv_f = 2.0 * M * X * width
+            qkv_ids = []
+            for c in range(P):
+                src = chunk_id(t.op.inputs[0], c)
+                q = Task(f"{t.id}.qkv.sp{c}", t.memory_required / (2 * P), t.compute_time / (2 * P), [src], set(pq),
+                         OpSpec("qkv_proj", [src], dict(wq), dict(a, seq_chunk=(c, P)), (B, Sc, width)),
+                         2 * M * width, qkv_f)
+                out.append(q)
+                qkv_ids.append(q.id)
+            causal = a.get("causal", True)
+            for c in range(P):
+                kv = qkv_ids[:c + 1] if causal else list(qkv_ids)
+                nkeys = len(kv) * Sc
+                core_f = 2.0 * 2 * B * nh * Sc * nkeys * D / (2 if causal else 1) + 2.0 * M * nh * D * X
+                at = Task(f"{t.id}.sp{c}", t.memory_required / (2 * P), t.compute_time * len(kv) / (P * P), kv,
+                          set(po), OpSpec("attn_sp", kv, dict(wo), dict(a, seq_chunk=(c, P)), (B, Sc, X)),
+                          t.out_bytes // P, core_f)
+                out.append(at)
+            continue
+        for c in range(P):
+            op = copy.deepcopy(t.op)
+            op.inputs = [chunk_id(i, c) for i in op.inputs]
+            op.out_shape = (B, Sc, X)
+            if kind == "embedding":
+                op.attrs = dict(op.attrs, seq_chunk=(c, P), tokens_total=B * S)
+            out.append(Task(f"{t.id}.sp{c}", t.memory_required / P, t.compute_time / P,
+                            [chunk_id(d, c) for d in t.dependencies], set(t.params_needed), op, t.out_bytes // P,
+                            t.flops / P))
+    return out, groups

@@ -147,10 +147,13 @@ def ref_rmsnorm(x, w, eps=1e-5):
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(x.dtype)
 
 
-def ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=None):
-    """q [B*S][>=nh*D], k/v [B*S][>=nkv*D] (row views into a packed qkv buffer allowed)."""
+def ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=None, Sq=None, q_off=0):
+    """q [B*Sq][>=nh*D], k/v [B*S][>=nkv*D] (row views into a packed qkv buffer allowed).
+    ``Sq``/``q_off``: the queries are the sequence chunk at positions q_off .. q_off+Sq-1
+    attending keys 0 .. S-1 (causal: key <= query position)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
-    qh = q[:, :n_head * head_dim].float().reshape(B, S, n_head, head_dim).transpose(1, 2)
+    Sq = S if Sq is None else Sq
+    qh = q[:, :n_head * head_dim].float().reshape(B, Sq, n_head, head_dim).transpose(1, 2)
     kh = k[:, :n_kv_head * head_dim].float().reshape(B, S, n_kv_head, head_dim).transpose(1, 2)
     vh = v[:, :n_kv_head * head_dim].float().reshape(B, S, n_kv_head, head_dim).transpose(1, 2)
     rep = n_head // n_kv_head
@@ -159,10 +162,11 @@ def ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale
         vh = vh.repeat_interleave(rep, dim=1)
     s = (qh @ kh.transpose(-1, -2)) * scale
     if causal:
-        mask = torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1)
+        qpos = torch.arange(Sq, device=q.device)[:, None] + q_off
+        mask = torch.arange(S, device=q.device)[None, :] > qpos
         s = s.masked_fill(mask, float("-inf"))
     o = torch.softmax(s, dim=-1) @ vh
-    return o.transpose(1, 2).reshape(B * S, n_head * head_dim).to(q.dtype)
+    return o.transpose(1, 2).reshape(B * Sq, n_head * head_dim).to(q.dtype)
 
 
 def rope_tables(S: int, head_dim: int, theta: float, device="cpu") -> Tuple[torch.Tensor, torch.Tensor]:
@@ -209,6 +213,20 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
         shp = x.shape[:-1] + (n_out,)
         M = x.numel() // x.shape[-1]
         cfg, sk = tuning.lookup(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
+        if cfg == tuning.LIB:
+            if a == 0 and residual is None and rows is None and rope is None and stats_out is None:
+                # a PLAIN GEMM (no fused epilogue) whose tuned choice is the vendor library
+                # (hipBLASLt via torch); every fused-epilogue GEMM stays on the HIP kernels
+                x2 = x.reshape(M, x.shape[-1])
+                o2 = out.view(M, n_out) if out is not None else torch.empty(M, n_out, dtype=x.dtype, device=x.device)
+                if bias is not None:
+                    torch.addmm(bias, x2, w.t(), beta=1.0, alpha=float(alpha), out=o2)
+                else:
+                    torch.mm(x2, w.t(), out=o2)
+                    if alpha != 1.0:
+                        o2.mul_(alpha)
+                return o2.view(shp) if out is None else out
+            cfg, sk = -1, 0
         rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
         y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact),
                        rc, rs_, int(rS), int(rD), int(rcols), stats_out, None)
@@ -256,6 +274,8 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
     a = ACT[act] if not isinstance(act, int) else act
     shp = x.shape[:-1] + (w_derived.shape[0] // 2 if a == SWIGLU else w_derived.shape[0],)
     cfg, sk = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
+    if cfg == tuning.LIB:
+        cfg, sk = -1, 0
     if ext_stats is None:
         sk = 1
     rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
@@ -301,11 +321,14 @@ def rmsnorm(x, w, eps=1e-5, residual=None, out=None, sum_out=None):
     return out.copy_(y) if out is not None else y
 
 
-def attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=None, out=None):
+def attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=None, out=None, Sq=None, q_off=0):
+    """Flash attention (GPU) / fp32 reference (CPU). ``Sq``/``q_off``: a sequence chunk of
+    queries at positions q_off.. against S keys (sequence-parallel attention nodes)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
     if _gpu(q):
-        return ext().attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, float(scale), out)
-    y = ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, scale)
+        return ext().attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, float(scale), out, 0,
+                               int(Sq or 0), int(q_off))
+    y = ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, scale, Sq=Sq, q_off=q_off)
     if out is not None:
         out.copy_(y)
         return out

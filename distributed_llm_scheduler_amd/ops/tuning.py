@@ -24,6 +24,10 @@ _table: Optional[Dict[str, Tuple[int, int]]] = None
 _cands: Dict[str, list] = {}     # key -> runner-up (cfg, splitk) by microbenchmark time (for in-DAG refinement)
 _refined: Dict[str, bool] = {}   # key -> chosen by whole-step timing inside a DAG
 REGSTAGE = 100  # config ids >= 100 select the register-staged kernel (csrc ops_binding kRegStage)
+PERSIST = 32    # config | 32: the same LDS-DMA tile config as a persistent launch (kernels.h kGemmPersist)
+LIB = 200       # the vendor library (hipBLASLt through torch.mm): a candidate for PLAIN GEMMs only —
+                # a GEMM with a fused epilogue (activation, residual, folded norm, RoPE, row
+                # statistics, SwiGLU, row range) always runs on the HIP kernels
 
 
 def _key(M: int, N: int, K: int, tg: str = "") -> str:
@@ -101,7 +105,7 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
 
 
 def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
-    out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1)]
+    out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1), (LIB, 1)]
     for cfg in range(n_cfg):
         for sk in (1, 2, 3, 4, 6, 8):
             if K % 64 or K % (64 * sk) or (sk > 1 and N % 8) or K // (64 * sk) < 2:
@@ -109,6 +113,10 @@ def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
             if sk > 1 and M * N > 2048 * 8192:
                 continue
             out.append((cfg, sk))
+    if M * N >= (8 << 20) and K % 64 == 0:
+        # many more tiles than resident blocks (LM heads): the persistent tile walk of the
+        # 256x128 / 64x64 configs (ops_binding PERSIST = 32)
+        out += [(PERSIST + c, 1) for c in (0, 3, 14) if c < n_cfg]
     return out
 
 
@@ -133,8 +141,11 @@ def tune(M: int, N: int, K: int, device=None, cold: bool = True, save: bool = Tr
     results = {}
     for cfg, sk in candidates(M, N, K, e.gemm_glds_num_configs(), tg):
         try:
-            t = _graph_time(lambda i: e.gemm(x, ws[i % copies], None, None, act, 1.0, out, cfg, sk, None, 0, 1e-5,
-                                             rng))
+            if cfg == LIB:
+                t = _graph_time(lambda i: torch.mm(x, ws[i % copies].t(), out=out))
+            else:
+                t = _graph_time(lambda i: e.gemm(x, ws[i % copies], None, None, act, 1.0, out, cfg, sk, None, 0,
+                                                 1e-5, rng))
         except RuntimeError:
             continue
         results[(cfg, sk)] = t

@@ -44,7 +44,8 @@ def test_gemm_identity_asymmetric():
                                    (512, 50257, 768), (1, 64, 64), (1024, 1024, 1024)])
 @pytest.mark.parametrize("config,splitk", [(-1, 0), (100, 1), (103, 1), (0, 1), (1, 1), (2, 1), (3, 1), (4, 1),
                                            (3, 2), (3, 4), (2, 3), (8, 1), (9, 1), (10, 1), (11, 1), (8, 2),
-                                           (12, 1), (13, 1), (14, 1), (15, 1), (12, 2), (14, 4)])
+                                           (12, 1), (13, 1), (14, 1), (15, 1), (12, 2), (14, 4),
+                                           (32, 1), (35, 1), (35, 4), (40, 1), (46, 1)])  # 32+: persistent
 def test_gemm_shapes(M, N, K, config, splitk):
     x = _rand(M, K, seed=1)
     w = _rand(N, K, scale=0.05, seed=2)
@@ -83,6 +84,20 @@ def test_attention(B, S, nh, nkv, D, causal, variant):
     q, k, v = qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:]
     o = ops.ext().attention(q, k, v, B, S, nh, nkv, D, causal, 1.0 / math.sqrt(D), None, variant)
     ref = ops.ref_attention(q.cpu(), k.cpu(), v.cpu(), B, S, nh, nkv, D, causal=causal)
+    _close(o.cpu(), ref, 2e-2)
+
+
+@pytest.mark.parametrize("B,S,Sq,q_off,nh,nkv,D", [(1, 512, 128, 384, 12, 12, 64), (2, 256, 64, 64, 4, 4, 64),
+                                                    (1, 512, 256, 256, 32, 8, 128), (1, 200, 50, 150, 4, 2, 128),
+                                                    (1, 384, 128, 0, 12, 12, 64)])
+def test_attention_query_chunk(B, S, Sq, q_off, nh, nkv, D):
+    # a sequence chunk's queries (positions q_off..) against every key before them:
+    # the attention node of the sequence-parallel DAG transform
+    kv = _rand(B * S, 2 * nkv * D, seed=71)
+    q = _rand(B * Sq, nh * D, seed=72)
+    k, v = kv[:, :nkv * D], kv[:, nkv * D:]
+    o = ops.attention(q, k, v, B, S, nh, nkv, D, True, Sq=Sq, q_off=q_off)
+    ref = ops.ref_attention(q.cpu(), k.cpu(), v.cpu(), B, S, nh, nkv, D, True, Sq=Sq, q_off=q_off)
     _close(o.cpu(), ref, 2e-2)
 
 
@@ -173,7 +188,8 @@ def test_moe_pipeline():
 
 @pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
 @pytest.mark.parametrize("M,N,K,cfg", [(512, 2304, 768, -1), (300, 1024, 4096, 0), (512, 3072, 768, 2),
-                                       (512, 1024, 1024, 8), (256, 512, 768, 14)])
+                                       (512, 1024, 1024, 8), (256, 512, 768, 14),
+                                       (512, 2304, 768, 35), (512, 3072, 768, 32)])
 def test_gemm_with_folded_norm(mode, M, N, K, cfg):
     x = _rand(M, K, scale=2.0, seed=40) + 0.5  # non-zero mean rows exercise the mean correction
     w = _rand(N, K, scale=0.03, seed=41)
