@@ -47,8 +47,10 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--cap-gb", type=float, default=288.0, help="per-GPU HBM budget for parameters")
-    ap.add_argument("--placement", default="scheduler", choices=["scheduler", "replica", "pipeline", "tensor"])
+    ap.add_argument("--placement", default="scheduler",
+                    choices=["scheduler", "replica", "pipeline", "tensor", "sequence"])
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel shards per layer (DAG transform)")
+    ap.add_argument("--sp", type=int, default=1, help="sequence chunks per request (context-parallel DAG transform)")
     ap.add_argument("--init", default="auto", choices=["auto", "host", "device"],
                     help="weight init: device RNG straight into HBM, or host master copy (auto: device "
                          "unless the program re-loads evicted groups, whose cost must be a real copy)")
@@ -80,7 +82,7 @@ def main():
     t0 = time.time()
     plan = runtime.plan(args.model, world=world, scheduler=args.scheduler, cap_gb=args.cap_gb, replicas=replicas,
                         batch=args.batch, seq=args.seq, cost_model="bytes", fuse=not args.no_fuse,
-                        placement=args.placement, tp=args.tp)
+                        placement=args.placement, tp=args.tp, sp=args.sp)
     log(f"[bench] rank {rank}: planned {plan.stats['tasks_completed']}/{plan.stats['tasks_total']} tasks in "
         f"{(time.time() - t0) * 1e3:.1f} ms; {plan.stats}")
     loads = [i.param for i in plan.programs[rank].instrs if i.op == "load"]
@@ -153,7 +155,8 @@ def main():
             "data": "synthetic",
             "config": {"model": {"gpt2": "gpt2-small"}.get(args.model, args.model), "global_batch": replicas * args.batch, "seq_len": args.seq,
                        "parallelism": f"dag-placement x{world} ({plan.scheduler_name if args.placement == 'scheduler' else args.placement}"
-                                      f"{f', tp{args.tp}' if args.tp > 1 else ''}, {replicas} request DAGs)"},
+                                      f"{f', tp{args.tp}' if args.tp > 1 else ''}{f', sp{args.sp}' if args.sp > 1 else ''}"
+                                      f", {replicas} request DAGs)"},
             "tasks_completed": plan.stats["tasks_completed"],
             "tasks_total": plan.stats["tasks_total"],
             "mem_cap_gb_per_gpu": args.cap_gb,

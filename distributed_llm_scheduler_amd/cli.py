@@ -15,7 +15,7 @@ Commands (defaults reproduce the reference's settings where one exists, SURVEY Â
 
 Common options: --model, --devices (ignored under torchrun: WORLD_SIZE wins), --scheduler,
 --hbm-cap-gb, --cost-model {bytes,reference}, --seq, --batch, --replicas, --placement,
---tp, --seed, --dtype (bf16 only: the kernels compute in bf16 with fp32 accumulation).
+--tp, --sp, --seed, --dtype (bf16 only: the kernels compute in bf16 with fp32 accumulation).
 """
 from __future__ import annotations
 
@@ -38,8 +38,10 @@ def _common(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--replicas", type=int, default=1, help="independent request DAGs (data parallelism)")
-    ap.add_argument("--placement", default="scheduler", choices=["scheduler", "replica", "pipeline", "tensor"])
-    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--placement", default="scheduler",
+                    choices=["scheduler", "replica", "pipeline", "tensor", "sequence"])
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel shards per layer (DAG transform)")
+    ap.add_argument("--sp", type=int, default=1, help="sequence chunks per request (context-parallel DAG transform)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dtype", default="bf16", choices=["bf16"])
     ap.add_argument("--no-fuse", action="store_true")
@@ -50,7 +52,7 @@ def _plan(a, world: int, resume: Optional[str] = None):
 
     return runtime.plan(a.model, world=world, scheduler=a.scheduler, cap_gb=a.hbm_cap_gb, replicas=a.replicas,
                         batch=a.batch, seq=a.seq, cost_model=a.cost_model, fuse=not a.no_fuse,
-                        placement=a.placement, tp=a.tp, resume=resume)
+                        placement=a.placement, tp=a.tp, resume=resume, sp=a.sp)
 
 
 def cmd_plan(a) -> int:
@@ -166,7 +168,7 @@ def cmd_elastic(a) -> int:
     out = run_elastic(world=a.devices, steps=a.steps, fail_rank=a.fail_rank, fail_step=a.fail_step,
                       device=a.device, model=a.model, scheduler=a.scheduler, cap_gb=a.hbm_cap_gb,
                       replicas=a.replicas, batch=a.batch, seq=a.seq, cost_model=a.cost_model, placement=a.placement,
-                      tp=a.tp)
+                      tp=a.tp, sp=a.sp)
     print(json.dumps(out))
     return 0
 

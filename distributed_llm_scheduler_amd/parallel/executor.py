@@ -140,7 +140,8 @@ class DAGExecutor:
                 op = self.tasks[tid].op
                 for name in op.inputs:
                     if name not in self.tasks and name not in self._inputs:
-                        M = math.prod(op.out_shape[:-1])
+                        # a sequence chunk's embedding reads its slice of the whole request
+                        M = op.attrs.get("tokens_total", math.prod(op.out_shape[:-1]))
                         vocab = self.cfg.vocab_size if self.cfg is not None else 50257
                         self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
         if self.gpu and STATS_HANDOFF:
@@ -157,7 +158,7 @@ class DAGExecutor:
             grp = [self.tasks[t] for t in ins.group]
             lead_norm = grp[0].op.kind in ("layernorm", "rmsnorm") and len(grp) > 1
             head = grp[1] if lead_norm else grp[0]
-            if head.op.kind in ("attention", "swiglu_mlp"):
+            if head.op.kind in ("attention", "attn_sp", "swiglu_mlp"):
                 return True
             # a plain GEMM group writes its output with an un-folded, non-SwiGLU GEMM
             return head.op.kind == "linear" and not lead_norm and head.op.attrs.get("act") != "swiglu"
@@ -235,6 +236,11 @@ class DAGExecutor:
         if k == "swiglu_mlp":
             F = a["ffn"]
             return 2 * (M * 2 * F + M * F) + 512
+        if k == "attn_sp":
+            # gathered K/V of the visible chunks + the attention output
+            D = a["head_dim"]
+            keys = M * len(t.op.inputs)
+            return 2 * (keys * 2 * a["n_kv_head"] * D + M * a["n_head"] * D) + 1024
         if k == "moe":
             return 0
         return 0
@@ -444,9 +450,15 @@ class DAGExecutor:
         src = norm.op.inputs[0] if norm is not None else (head.op.inputs[0] if head.op.inputs else None)
         if k == "embedding":
             tok = self._x(head.op.inputs[0])
-            S = head.op.out_shape[1]
-            ops.embedding(tok, self._w(W["wte"]), self._w(W["wpe"]) if "wpe" in W else None, S,
-                          out=self._flat(out))
+            B, S = head.op.out_shape[0], head.op.out_shape[1]
+            wpe = self._w(W["wpe"]) if "wpe" in W else None
+            if "seq_chunk" in a:  # sequence chunk c: its token slice, positions from c*S on
+                c, P = a["seq_chunk"]
+                tok = tok.view(B, S * P)[:, c * S:(c + 1) * S]
+                tok = tok.reshape(-1) if B == 1 else tok.contiguous().view(-1)
+                if wpe is not None:
+                    wpe = wpe[c * S:(c + 1) * S]
+            ops.embedding(tok, self._w(W["wte"]), wpe, S, out=self._flat(out))
         elif k == "layernorm":
             ops.layernorm(self._flat(self._x(src)), self._w(W["w"]), self._w(W["b"]), a.get("eps", 1e-5),
                           out=self._flat(out))
@@ -476,6 +488,38 @@ class DAGExecutor:
                 self._gemm(x, W["w_qkv"], W.get("b_qkv"), norm, out=qkv)
             ops.attention(qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:], B, S, nh, nkv,
                           D, causal=a.get("causal", True), out=o)
+            ops.linear(o, self._w(W["w_o"]), self._w(W["b_o"]) if "b_o" in W else None, residual=residual,
+                       out=self._flat(out), stats_out=st_out)
+        elif k == "qkv_proj":
+            # sequence chunk c's QKV rows (RoPE at its absolute positions c*Sc ..)
+            x = self._flat(self._x(src))
+            B, Sc = head.op.out_shape[0], head.op.out_shape[1]
+            nh, nkv, D = a["n_head"], a["n_kv_head"], a["head_dim"]
+            c, P = a["seq_chunk"]
+            if a.get("rope"):
+                cos, sin = self._rope_tables(Sc * P, D, a.get("rope_theta", 10000.0))
+                self._gemm(x, W["w_qkv"], W.get("b_qkv"), norm, out=self._flat(out),
+                           rope=(cos[c * Sc:], sin[c * Sc:], Sc, D, (nh + nkv) * D), rope_perm=(nh, nkv, D))
+            else:
+                self._gemm(x, W["w_qkv"], W.get("b_qkv"), norm, out=self._flat(out))
+        elif k == "attn_sp":
+            B, Sc = head.op.out_shape[0], head.op.out_shape[1]
+            nh, nkv, D = a["n_head"], a["n_kv_head"], a["head_dim"]
+            c, P = a["seq_chunk"]
+            M = B * Sc
+            chunks = [self._flat(self._x(n)) for n in head.op.inputs]  # qkv of the visible chunks
+            q = chunks[c][:, :nh * D]
+            nkeys = len(chunks) * Sc
+            if len(chunks) == 1:
+                kv = chunks[0][:, nh * D:]
+            else:  # gather the chunks' K/V rows into one [B, keys, 2*nkv*D] block
+                kv = self._ws(0, (B, nkeys, 2 * nkv * D))
+                for j, ch in enumerate(chunks):
+                    kv[:, j * Sc:(j + 1) * Sc].copy_(ch.view(B, Sc, -1)[:, :, nh * D:])
+                kv = kv.view(B * nkeys, 2 * nkv * D)
+            o = self._ws(2 * B * nkeys * 2 * nkv * D // 2 + 256, (M, nh * D))
+            ops.attention(q, kv[:, :nkv * D], kv[:, nkv * D:], B, nkeys, nh, nkv, D,
+                          causal=a.get("causal", True), out=o, Sq=Sc, q_off=c * Sc)
             ops.linear(o, self._w(W["w_o"]), self._w(W["b_o"]) if "b_o" in W else None, residual=residual,
                        out=self._flat(out), stats_out=st_out)
         elif k == "swiglu_mlp":

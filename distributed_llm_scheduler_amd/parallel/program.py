@@ -71,13 +71,13 @@ def _fuse_kind(prev_kind: str, nxt: Task) -> Optional[str]:
     if nxt.op is None:
         return None
     kb = nxt.op.kind
-    if prev_kind in ("layernorm", "rmsnorm") and kb in ("linear", "attention", "swiglu_mlp") \
+    if prev_kind in ("layernorm", "rmsnorm") and kb in ("linear", "attention", "qkv_proj", "swiglu_mlp") \
             and not nxt.op.attrs.get("act"):
         return f"{prev_kind}+{kb}"  # norm folded into the GEMM (in-kernel row stats + derived weights)
     base = prev_kind.split("+", 1)[1] if prev_kind.startswith(("layernorm+", "rmsnorm+")) else prev_kind
     if base == "linear" and kb == "gelu":
         return prev_kind + "+gelu"  # GELU in the GEMM epilogue
-    if base in ("linear", "linear+gelu", "attention", "swiglu_mlp") and kb == "residual":
+    if base in ("linear", "linear+gelu", "attention", "attn_sp", "swiglu_mlp") and kb == "residual":
         return prev_kind + "+residual"  # residual add in the (output-projection) GEMM epilogue
     return None
 

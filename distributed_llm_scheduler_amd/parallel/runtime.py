@@ -48,7 +48,7 @@ class Plan:
 def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: float = 288.0, replicas: int = 1,
          batch: int = 1, seq: int = 512, cost_model: str = "bytes", fuse: bool = True,
          node_speeds: Optional[Sequence[float]] = None, link_bw_gbps: float = 153.0,
-         placement: str = "scheduler", tp: int = 1, resume: Optional[str] = None) -> Plan:
+         placement: str = "scheduler", tp: int = 1, resume: Optional[str] = None, sp: int = 1) -> Plan:
     """Build the DAG of ``replicas`` requests of ``model``, place it on ``world`` GPUs with
     ``scheduler`` under a per-GPU cap of ``cap_gb`` and lower it to per-rank programs.
 
@@ -59,6 +59,8 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         (pipeline parallelism: each block boundary is a cross-GPU p2p edge),
       * ``"tensor"``    — with ``tp > 1``: shard k of every layer on GPU k % world, the
         shard-sum / residual / embedding / head nodes on GPU 0 (tensor parallelism).
+      * ``"sequence"``  — with ``sp > 1``: sequence chunk c of every node on GPU c % world
+        (context parallelism; the K/V edges between chunks are the cross-GPU transfers).
     The fixed placements still go through the scheduler's memory accounting (tasks that
     do not fit fail exactly as in the policies).
 
@@ -69,7 +71,10 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     args = dict(model=model, world=world, scheduler=scheduler, cap_gb=cap_gb, replicas=replicas, batch=batch,
                 seq=seq, cost_model=cost_model, fuse=fuse, node_speeds=list(node_speeds) if node_speeds else None,
                 link_bw_gbps=link_bw_gbps, placement=placement, tp=tp)
-    tasks, groups, cfg = registry.build(model, batch=batch, seq=seq, replicas=replicas, cost_model=cost_model, tp=tp)
+    if sp > 1:
+        args["sp"] = sp
+    tasks, groups, cfg = registry.build(model, batch=batch, seq=seq, replicas=replicas, cost_model=cost_model, tp=tp,
+                                        sp=sp)
     param_bytes = {pid: group_layout(g)[0] for pid, g in groups.items()}
     nodes = [Node(f"gpu{r}", cap_gb, (node_speeds[r] if node_speeds else 1.0), device=r) for r in range(world)]
     node_rank = {n.id: r for r, n in enumerate(nodes)}
@@ -86,7 +91,7 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         sched, schedule = _resume(resume, args, sched)
     elif placement == "scheduler":
         schedule = sched.schedule()
-    elif placement in ("replica", "pipeline", "tensor"):
+    elif placement in ("replica", "pipeline", "tensor", "sequence"):
         schedule = _fixed_schedule(tasks, world, sched, placement, cfg)
     else:
         raise ValueError(f"unknown placement {placement!r}")
@@ -181,9 +186,10 @@ def _fixed_schedule(tasks: Sequence[Task], world: int, sched, mode: str, cfg) ->
         if mode == "replica":
             rep = int(t.id.split("/")[0][1:]) if "/" in t.id else 0
             r = rep % world
-        elif mode == "tensor":
+        elif mode in ("tensor", "sequence"):
+            tag = "tp" if mode == "tensor" else "sp"
             sfx = t.id.rsplit(".", 1)[-1] if "." in t.id.split("/")[-1] else ""
-            r = int(sfx[2:]) % world if sfx.startswith("tp") and sfx[2:].isdigit() else 0
+            r = int(sfx[2:]) % world if sfx.startswith(tag) and sfx[2:].isdigit() else 0
         else:
             layer = min(max(_layer_of(t.id, L), 0), L - 1)
             r = min(layer * world // L, world - 1)
