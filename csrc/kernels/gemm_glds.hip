@@ -62,14 +62,20 @@ __device__ __forceinline__ void rope_pairs(float* v, int row, int col, const Rop
   }
 }
 
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0>
+// KG_ = K groups: KG wave groups of WM x WN waves share each output tile; a stage holds KG
+// consecutive 64-deep K-tiles and group g multiplies tile g of every stage (intra-block
+// split-K: KG x the waves — and DMA issuers — per CU on a skinny grid, no reduce kernel; the
+// groups' accumulators are summed through LDS before the epilogue).
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0, int KG_ = 1>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_, BXS = BXS_;
+  static constexpr int KG = KG_;
   static constexpr int BK = 64, CH = 8;
-  static constexpr int NW = WM * WN, T = 64 * NW;
+  static constexpr int NW = WM * WN, T = 64 * NW * KG;
   static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
   static constexpr int ROWS = BM + BN, INSTR = ROWS / 8, PW = INSTR / NW;
-  static constexpr int STAGE = ROWS * CH;  // bf16x8 units
+  static constexpr int SUB = ROWS * CH;     // one 64-deep K-tile image (bf16x8 units)
+  static constexpr int STAGE = SUB * KG;    // bf16x8 units
   // split staging (BXS > 0): separate A / W rings
   static constexpr int SA = STAGES, SB = STAGES + BXS;
   static constexpr int PWA = BM / 8 / NW, PWB = BN / 8 / NW;
@@ -81,6 +87,8 @@ struct Cfg {
   static_assert(PW * (STAGES - 2) <= 63, "vmcnt range");
   static_assert(STAGES >= 2 && STAGES <= 8, "stages");
   static_assert(LDS_UNITS * 16 <= 163840, "LDS budget");
+  static_assert(KG == 1 || (BXS == 0 && PRIO == 0), "K groups use the joint ring");
+  static_assert(KG == 1 || NW * 64 * FM * FN * 16 <= LDS_UNITS * 16, "K-group reduction must fit the LDS");
 };
 
 // split rings: wait until at most a*PWA + b*PWB DMA instructions are outstanding, with
@@ -151,29 +159,35 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
 template <class C>
 __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
-                                               int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
-                                               f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
+                                               int kbeg, int nk, int lane, int wave, int kgrp, int wm, int wn,
+                                               bool ln_acc, f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
                                                float (&st_q)[C::FM]) {
+  // `wave` is the wave's index in the whole block (all K groups issue DMA); instruction
+  // gi = wave*PW + j loads 8 rows of K-tile gi / INSTR of the stage
   const bf16* src[C::PW];
+  int dst[C::PW];
 #pragma unroll
   for (int j = 0; j < C::PW; ++j) {
-    const int row = 8 * (wave * C::PW + j) + (lane >> 3);
+    const int gi = wave * C::PW + j;
+    const int sub = gi / C::INSTR, r8 = gi % C::INSTR;
+    const int row = 8 * r8 + (lane >> 3);
     const int gch = (lane & 7) ^ (row & 7);
+    const int kofs = kbeg + sub * C::BK + gch * 8;
     if (row < C::BM) {
       const int gm = min(m0 + row, M - 1);
-      src[j] = A + (size_t)gm * lda + kbeg + gch * 8;
+      src[j] = A + (size_t)gm * lda + kofs;
     } else {
       const int gn = min(n0 + row - C::BM, N - 1);
-      src[j] = W + (size_t)gn * ldw + kbeg + gch * 8;
+      src[j] = W + (size_t)gn * ldw + kofs;
     }
+    dst[j] = sub * C::SUB + r8 * 64;
   }
   auto issue = [&](int kt) {
     bf16x8* stage = smem + (kt % C::STAGES) * C::STAGE;
 #pragma unroll
     for (int j = 0; j < C::PW; ++j) {
-      __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(stage + (wave * C::PW + j) * 64),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * (C::BK * C::KG)),
+                                       (__attribute__((address_space(3))) void*)(stage + dst[j]), 16, 0, 0);
     }
   };
 #pragma unroll
@@ -184,7 +198,7 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
     wait_tiles<C::PW, C::STAGES - 2>(ahead);
     raw_barrier();
     if (kt + C::STAGES - 1 < nk) issue(kt + C::STAGES - 1);
-    const bf16x8* st = smem + (kt % C::STAGES) * C::STAGE;
+    const bf16x8* st = smem + (kt % C::STAGES) * C::STAGE + kgrp * C::SUB;
     mma_tile<C>(st, st + C::BM * C::CH, lane, wm, wn, ln_acc, acc, st_s, st_q);
   }
 }
@@ -264,11 +278,12 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
                                           const Epi& ep) {
   const RopeArgs& rope = ep.rope;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int kgrp = wave / C::NW, wq = wave % C::NW;  // K group, wave within the group
+  const int wm = wq / C::WN, wn = wq % C::WN;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
   if (m0 >= M) return;  // whole block idle (uniform: before any barrier)
   const int kbeg = ks * kslice;
-  const int nk = kslice / C::BK;
+  const int nk = kslice / (C::BK * C::KG);
 
   f32x4 acc[C::FM][C::FN];
 #pragma unroll
@@ -284,7 +299,29 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   if constexpr (C::BXS > 0)
     mainloop_split<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc, st_s, st_q);
   else
-    mainloop_joint<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc, st_s, st_q);
+    mainloop_joint<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
+                      st_q);
+  if constexpr (C::KG > 1) {
+    // sum the K groups' accumulators into group 0 (lane-contiguous 16-B records)
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem);
+    for (int g2 = 1; g2 < C::KG; ++g2) {
+      if (kgrp == g2) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) red[((i * C::FN + j) * C::NW + wq) * 64 + lane] = acc[i][j];
+      }
+      __syncthreads();
+      if (kgrp == 0) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) acc[i][j] += red[((i * C::FN + j) * C::NW + wq) * 64 + lane];
+      }
+      __syncthreads();
+    }
+  }
 
   // epilogue: lane (g = lane>>4, r = lane&15) of fragment (i, j) holds C[row][col..col+3]
   // with row = m0 + wm*WTM + 16i + r, col = n0 + wn*WTN + 16j + 4g
@@ -344,6 +381,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   // columns straddle N falls back to scalars.
   const bool vec_ok = (ldc % 4 == 0) && (!R || ldr % 4 == 0);
   if (part != nullptr) {  // split-K: fp32 partial slab, reduced by splitk_reduce_kernel
+    if (kgrp != 0) return;
     float* P = part + (size_t)ks * Mmax * N;
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
@@ -364,6 +402,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     return;
   }
   if (act == ACT_SWIGLU) {
+    if (kgrp != 0) return;
     // fragment pairs (2jj, 2jj+1) hold gate and up for the same 16 output columns
     const int NO = N / 2;
 #pragma unroll
@@ -425,6 +464,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   __syncthreads();  // every wave is done with the staging buffers (and the norm statistics)
 #pragma unroll
   for (int j = 0; j < C::FN; ++j) {
+    if (kgrp != 0) break;  // K group 0 holds the summed tile
     const int cl = wn * C::WTN + j * 16 + g4;  // local column of this lane's 4 values
     const int col = n0 + cl;
     const bool full = col + 3 < N;
@@ -750,7 +790,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
   if (rows) DLS_K(0, 1);
   else if (persist) {
     if (ln_in) {
-      if constexpr (C::BM * C::BN <= 256 * 128) {
+      if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) {
         grid = dim3(std::min(total, persistent_grid<C, 1>()));
         DLS_K(1, 2);
       }
@@ -759,7 +799,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
       DLS_K(0, 2);
     }
   } else if (ln_in) {
-    if constexpr (C::BM * C::BN <= 256 * 128) DLS_K(1, 0);  // 256x256 tiles have no registers left for it
+    if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) DLS_K(1, 0);  // 256x256: no registers left for it
   } else DLS_K(0, 0);
 #undef DLS_K
   if (splitk > 1) {
@@ -793,18 +833,28 @@ using C12 = Cfg<256, 256, 2, 4, 2, 0, 1>;  // 2 x 32 KiB A + 3 x 32 KiB W = 160 
 using C13 = Cfg<256, 256, 2, 4, 2, 1, 1>;
 using C14 = Cfg<256, 128, 4, 2, 3, 0, 1>;  // 3 x 32 KiB A + 4 x 16 KiB W = 160 KiB
 using C15 = Cfg<128, 128, 2, 2, 3, 0, 1>;  // 3 x 16 KiB A + 4 x 16 KiB W
+// two K groups (8 waves, intra-block split-K) for the skinny M = 512 GEMMs
+using C16 = Cfg<64, 64, 2, 2, 3, 0, 0, 2>;   // 3 x 32 KiB stages
+using C17 = Cfg<64, 64, 2, 2, 2, 0, 0, 2>;   // 2 x 32 KiB: two blocks per CU
+using C18 = Cfg<128, 64, 2, 2, 2, 0, 0, 2>;  // 2 x 48 KiB
+using C19 = Cfg<64, 128, 2, 2, 2, 0, 0, 2>;
+using C20 = Cfg<64, 64, 2, 2, 2, 0, 0, 4>;   // four K groups: 16 waves, 2 x 64 KiB stages
+using C21 = Cfg<64, 64, 1, 2, 2, 0, 0, 4>;   // four K groups of 2 waves (64x32 each)
 
 struct Shape {
   int bm, bn;
 };
 constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64, 128},  {64, 64},
                              {128, 64},  {128, 128}, {256, 256}, {256, 256}, {256, 128}, {128, 128},
-                             {256, 256}, {256, 256}, {256, 128}, {128, 128}};
-constexpr int kNumCfg = 16;
+                             {256, 256}, {256, 256}, {256, 128}, {128, 128}, {64, 64},   {64, 64},
+                             {128, 64},  {64, 128},  {64, 64},   {64, 64}};
+constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 256, 256};
+constexpr int kNumCfg = 22;
 
 }  // namespace
 
 int gemm_glds_num_configs() { return kNumCfg; }
+int gemm_glds_kstep(int cfg) { return kKStep[(cfg & (kGemmPersist - 1)) < kNumCfg ? (cfg & (kGemmPersist - 1)) : 3]; }
 
 // Heuristic: largest tile whose grid (times a split-K factor that keeps >= 4 K-tiles per
 // block) reaches ~256 blocks; split-K only when the output grid alone is too small.
@@ -841,6 +891,7 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
   if (ln_mode != 0 && !a.ext_stats) {
     splitk = 1;  // in-kernel row statistics need the whole K range in one block
     if (kShapes[cfg < kNumCfg ? cfg : 3].bm * kShapes[cfg < kNumCfg ? cfg : 3].bn > 256 * 128) cfg = 0;
+    if (cfg < kNumCfg && kKStep[cfg] != 64) cfg = 3;  // K groups: no in-kernel row statistics
   }
 #define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist)
   switch (cfg) {
@@ -859,6 +910,12 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
     case 13: DLS_L(C13); break;
     case 14: DLS_L(C14); break;
     case 15: DLS_L(C15); break;
+    case 16: DLS_L(C16); break;
+    case 17: DLS_L(C17); break;
+    case 18: DLS_L(C18); break;
+    case 19: DLS_L(C19); break;
+    case 20: DLS_L(C20); break;
+    case 21: DLS_L(C21); break;
     default: DLS_L(C3); break;
   }
 #undef DLS_L

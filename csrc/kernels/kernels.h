@@ -54,6 +54,7 @@ void launch_gemm_bf16(const GemmArgs& a, hipStream_t s);  // register-staged, an
 
 // LDS-DMA multistage GEMM (K % 64 == 0); split-K partials need workspace_bytes of fp32
 int gemm_glds_num_configs();
+int gemm_glds_kstep(int cfg);  // K granularity of a config (64, or 128 for two K groups)
 // cfg | kGemmPersist: the same tile config as a persistent launch (a resident grid walks the
 // tiles; one tile's store drain overlaps the next tile's first loads)
 constexpr int kGemmPersist = 32;

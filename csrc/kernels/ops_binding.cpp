@@ -145,7 +145,9 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
     if (sk <= 0) sk = ask;
   }
   TORCH_CHECK((cfg & (kGemmPersist - 1)) < gemm_glds_num_configs() && cfg < 2 * kGemmPersist, "unknown GEMM config ", cfg);
-  const bool split_ok = (N % 8 == 0) && (c.stride(0) % 8 == 0) && (ldr % 8 == 0) && K % (64 * sk) == 0 &&
+  TORCH_CHECK(K % gemm_glds_kstep(cfg) == 0, "GEMM config ", cfg, " needs K % ", gemm_glds_kstep(cfg), " == 0");
+  const bool split_ok = (N % 8 == 0) && (c.stride(0) % 8 == 0) && (ldr % 8 == 0) &&
+                        K % (gemm_glds_kstep(cfg) * sk) == 0 &&
                         (!swiglu || N % 32 == 0);
   if (!split_ok || (ln_mode != 0 && !ext_stats.has_value())) sk = 1;
   at::Tensor ws;
@@ -391,6 +393,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("PERSIST") = kGemmPersist;
   m.def("gemm_pick_config", &gemm_pick_config);
   m.def("gemm_glds_num_configs", &gemm_glds_num_configs);
+  m.def("gemm_glds_kstep", &gemm_glds_kstep);
   m.def("gemm_glds_pick", [](int M, int N, int K) {
     int c, s;
     gemm_glds_pick(M, N, K, &c, &s);

@@ -226,7 +226,7 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
                     if alpha != 1.0:
                         o2.mul_(alpha)
                 return o2.view(shp) if out is None else out
-            cfg, sk = -1, 0
+            cfg, sk = tuning.lookup_fused(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
         rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
         y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact),
                        rc, rs_, int(rS), int(rD), int(rcols), stats_out, None)
@@ -273,9 +273,7 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
     m = {"layernorm": 1, "rmsnorm": 2}[mode]
     a = ACT[act] if not isinstance(act, int) else act
     shp = x.shape[:-1] + (w_derived.shape[0] // 2 if a == SWIGLU else w_derived.shape[0],)
-    cfg, sk = tuning.lookup(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
-    if cfg == tuning.LIB:
-        cfg, sk = -1, 0
+    cfg, sk = tuning.lookup_fused(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
     if ext_stats is None:
         sk = 1
     rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)

@@ -68,6 +68,20 @@ def lookup(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
     return v if v is not None else (-1, 0)
 
 
+def lookup_fused(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
+    """Like :func:`lookup`, for a GEMM with a fused epilogue (which the vendor library cannot
+    run): if the tuned choice is ``LIB``, the fastest HIP-kernel candidate of the same
+    microbenchmark instead of the kernel's heuristic."""
+    cfg, sk = lookup(M, N, K, tg)
+    if cfg != LIB:
+        return cfg, sk
+    table()
+    for c in _cands.get(_key(M, N, K, tg), []):
+        if c[0] != LIB:
+            return tuple(c)
+    return -1, 0
+
+
 def _save() -> None:
     try:
         with open(_PATH, "w") as f:
