@@ -86,7 +86,7 @@ def bench_attn(quick):
         ours = timeit(lambda: ops.attention(q, k, v, B, S, nh, nkv, D, True, out=o))
         sc = 1.0 / math.sqrt(D)
         var = {f"v{vv}": round(timeit(lambda: ops.ext().attention(q, k, v, B, S, nh, nkv, D, True, sc, o, vv)), 2)
-               for vv in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11)}
+               for vv in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13)}
         qh = q.reshape(B, S, nh, D).transpose(1, 2).contiguous()
         kh = k.reshape(B, S, nkv, D).transpose(1, 2).repeat_interleave(nh // nkv, 1).contiguous()
         vh = v.reshape(B, S, nkv, D).transpose(1, 2).repeat_interleave(nh // nkv, 1).contiguous()

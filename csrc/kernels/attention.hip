@@ -315,6 +315,9 @@ static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
     case 9: launch_attn<D, 2, 2, 2>(a, s); break;
     case 10: launch_attn<D, 2, (D == 64 ? 3 : 2), 2>(a, s); break;
     case 11: launch_attn<D, 1, (D == 64 ? 4 : 2), 2>(a, s); break;
+    // four key chains per query group (D = 128: two, the LDS holds no more)
+    case 12: launch_attn<D, 1, 2, (D == 64 ? 4 : 2)>(a, s); break;
+    case 13: launch_attn<D, 2, 2, (D == 64 ? 4 : 2)>(a, s); break;
     default: {
       // 64-query blocks, 2 K/V stages fill the chip from ~320 blocks on (batch 8, S=2048);
       // below that the causal row's dependent chain is the kernel time, so split each stage's

@@ -22,6 +22,8 @@
 
 namespace {
 
+__device__ __forceinline__ int kslice_count(int K, int kslice) { return K / kslice; }
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -323,9 +325,67 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     }
   }
 
+  const int g4 = (lane >> 4) * 4, r16 = lane & 15;
+  if (part != nullptr && ep.tile_sem != nullptr) {
+    // In-launch split-K combine (cdna_hip_programming.md §projection GEMM item 2, sc1 form):
+    // every K slice stores its fp32 tile WRITE-THROUGH (sc1) into its slab, drains, and one
+    // lane draws a ticket from the tile's agent-scope counter; the slice that draws
+    // splitk-1 reads the other slabs with sc1 loads (no L1 copy can be stale), adds them to
+    // its registers and runs the ordinary epilogue. No separate reduce kernel, no spinning.
+    const size_t slab = (size_t)Mmax * N;
+    const int tiles_m = (M + C::BM - 1) / C::BM;
+    int* sem = ep.tile_sem + tm + tn * tiles_m;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(part, 0, (int)(slab * kslice_count(K, kslice) * 4), 0x00020000);
+    if (kgrp == 0) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int row = m0 + wm * C::WTM + i * 16 + r16;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int col = n0 + wn * C::WTN + j * 16 + g4;
+          if (col >= N) continue;  // N % 8 == 0 on split-K launches: a fragment is in or out whole
+          const f32x4 v = acc[i][j];
+          u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+          __builtin_amdgcn_raw_buffer_store_b128(u, rsrc, (int)(((size_t)ks * slab + (size_t)row * N + col) * 4), 0,
+                                                 16);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);  // the block's one LDS array (staging is free now)
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(sem, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == kslice_count(K, kslice) - 1;
+      if (last) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      flag[0] = last;
+    }
+    __syncthreads();
+    const bool last = flag[0] != 0;
+    if (!last) return;  // block-uniform
+    if (kgrp == 0) {
+      const int nsl = kslice_count(K, kslice);
+      for (int s2 = 0; s2 < nsl; ++s2) {
+        if (s2 == ks) continue;
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+          const int row = min(m0 + wm * C::WTM + i * 16 + r16, M - 1);
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) {
+            const int col = min(n0 + wn * C::WTN + j * 16 + g4, N - 4);
+            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(
+                rsrc, (int)(((size_t)s2 * slab + (size_t)row * N + col) * 4), 0, 16);
+            acc[i][j] += f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]),
+                               __uint_as_float(u[3])};
+          }
+        }
+      }
+    }
+    part = nullptr;  // the tile now holds the full sum: ordinary epilogue below
+  }
   // epilogue: lane (g = lane>>4, r = lane&15) of fragment (i, j) holds C[row][col..col+3]
   // with row = m0 + wm*WTM + 16i + r, col = n0 + wn*WTN + 16j + 4g
-  const int g4 = (lane >> 4) * 4, r16 = lane & 15;
   float ln_rs[C::FM], ln_mu[C::FM];
   if (ln_mode != 0) {
     if constexpr (LN) {
@@ -776,7 +836,7 @@ int persistent_grid() {
 template <class C>
 void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
             float ln_eps, const int* rows, bool persist) {
-  const Epi ep{a.rope, a.stats_out, a.ext_stats};
+  const Epi ep{a.rope, a.stats_out, a.ext_stats, (splitk > 1 && !rows) ? a.tile_sem : nullptr};
   static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
   const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;
@@ -802,7 +862,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) DLS_K(1, 0);  // 256x256: no registers left for it
   } else DLS_K(0, 0);
 #undef DLS_K
-  if (splitk > 1) {
+  if (splitk > 1 && !ep.tile_sem) {
     const ReduceNorm nm{ln_colsum, a.ext_stats ? ln_mode : 0, ln_eps, a.K};
     if (a.stats_out && !rows && a.act != kActSwiglu && (a.N / 8) % 64 != 0) {  // small rows: a wave per row
       hipLaunchKernelGGL(splitk_reduce_rows_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, ws, splitk, a.M, a.N,

@@ -40,6 +40,7 @@ struct GemmArgs {
   //            ln_mode 1/2 and ln_colsum: any tile config, split-K allowed).
   float* stats_out = nullptr;
   const float* ext_stats = nullptr;
+  int* tile_sem = nullptr;  // split-K: >= tiles_m*tiles_n zeroed counters -> combine inside the GEMM launch
 };
 
 // epilogue extras carried down to the tile code
@@ -47,6 +48,9 @@ struct Epi {
   RopeArgs rope;
   float* stats_out;
   const float* ext_stats;
+  // in-launch split-K combine: one arrival counter per output tile (zero before the launch,
+  // reset by each tile's last arriver); nullptr -> separate reduce kernel
+  int* tile_sem = nullptr;
 };
 
 int gemm_pick_config(int M, int N, int K);

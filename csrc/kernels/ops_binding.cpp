@@ -5,6 +5,8 @@
 // current HIP stream (so the executor's stream and hipGraph capture apply), and
 // allocates outputs through torch's caching allocator unless the caller passes `out`
 // (the executor passes views into its HBM arena).
+#include <cstdlib>
+
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
@@ -13,6 +15,28 @@
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+// Split-K tile counters for the in-launch combine: one zeroed int32 pool per device (allocated
+// on first use — the executor's eager warm-up step runs before any hipGraph capture), handed
+// out round-robin so kernels in flight on other streams never share a counter; each tile's
+// last arriver resets its counter, so a region is zero again whenever it is reused.
+constexpr int64_t kSemPool = 1 << 20;
+int* split_k_counters(const at::Tensor& like, int64_t n) {
+  static at::Tensor pool[64];
+  static int64_t next[64];
+  const int d = like.get_device();
+  TORCH_CHECK(d >= 0 && d < 64 && n <= kSemPool, "split-K counters");
+  if (!pool[d].defined()) pool[d] = at::zeros({kSemPool}, like.options().dtype(at::kInt));
+  n = (n + 63) / 64 * 64;
+  if (next[d] + n > kSemPool) next[d] = 0;
+  int* p = pool[d].data_ptr<int>() + next[d];
+  next[d] += n;
+  return p;
+}
+const bool kSplitKFixup = [] {
+  const char* e = std::getenv("DLS_SPLITK_FIXUP");
+  return !(e && e[0] == '0');
+}();
 
 void check_bf16(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -151,7 +175,10 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                         (!swiglu || N % 32 == 0);
   if (!split_ok || (ln_mode != 0 && !ext_stats.has_value())) sk = 1;
   at::Tensor ws;
-  if (sk > 1) ws = at::empty({(int64_t)gemm_glds_workspace_bytes((int)M, (int)N, sk) / 4}, a.options().dtype(at::kFloat));
+  if (sk > 1) {
+    ws = at::empty({(int64_t)gemm_glds_workspace_bytes((int)M, (int)N, sk) / 4}, a.options().dtype(at::kFloat));
+    if (kSplitKFixup && !rowp) g.tile_sem = split_k_counters(a, (M + 63) / 64 * ((N + 63) / 64));
+  }
   launch_gemm_glds(g, cfg, sk, sk > 1 ? ws.data_ptr() : nullptr, cur_stream(), csp, (int)ln_mode, (float)ln_eps,
                    rowp);
   return c;

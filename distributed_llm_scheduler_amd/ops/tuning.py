@@ -18,7 +18,8 @@ from typing import Dict, Iterable, Optional, Tuple
 
 import torch
 
-_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning.json")
+_PATH = os.environ.get("DLS_GEMM_TUNING") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "gemm_tuning.json")
 _lock = threading.Lock()
 _table: Optional[Dict[str, Tuple[int, int]]] = None
 _cands: Dict[str, list] = {}     # key -> runner-up (cfg, splitk) by microbenchmark time (for in-DAG refinement)
