@@ -119,11 +119,21 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
     return statistics.median(res)
 
 
+def kstep(cfg: int) -> int:
+    """K granularity of an LDS-DMA config (csrc gemm_glds kKStep): 64, or 128 / 256 for the
+    two / four K-group configs 16-19 / 20-21."""
+    c = cfg % PERSIST if cfg < REGSTAGE else 0
+    return 256 if c in (20, 21) else 128 if 16 <= c <= 19 else 64
+
+
 def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
     out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1), (LIB, 1)]
     for cfg in range(n_cfg):
+        ks = kstep(cfg)
+        if ks > 64 and "r" in tg:
+            continue  # K-group configs are not offered for device-side row ranges (MoE experts)
         for sk in (1, 2, 3, 4, 6, 8):
-            if K % 64 or K % (64 * sk) or (sk > 1 and N % 8) or K // (64 * sk) < 2:
+            if K % 64 or K % (ks * sk) or (sk > 1 and N % 8) or K // (ks * sk) < 2:
                 continue
             if sk > 1 and M * N > 2048 * 8192:
                 continue
