@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--cap-gb", type=float, default=288.0, help="per-GPU HBM budget for parameters")
+    ap.add_argument("--cost-model", default="bytes", choices=["bytes", "reference"],
+                    help="planning cost model: real tensor bytes, or the reference's 0.5 GB per parameter "
+                         "(memory-regime experiments: e.g. gpt2-medium under an 8 GB cap forces evict/reload)")
     ap.add_argument("--placement", default="scheduler",
                     choices=["scheduler", "replica", "pipeline", "tensor", "sequence"])
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel shards per layer (DAG transform)")
@@ -81,7 +84,7 @@ def main():
     replicas = world * args.replicas_per_gpu
     t0 = time.time()
     plan = runtime.plan(args.model, world=world, scheduler=args.scheduler, cap_gb=args.cap_gb, replicas=replicas,
-                        batch=args.batch, seq=args.seq, cost_model="bytes", fuse=not args.no_fuse,
+                        batch=args.batch, seq=args.seq, cost_model=args.cost_model, fuse=not args.no_fuse,
                         placement=args.placement, tp=args.tp, sp=args.sp)
     log(f"[bench] rank {rank}: planned {plan.stats['tasks_completed']}/{plan.stats['tasks_total']} tasks in "
         f"{(time.time() - t0) * 1e3:.1f} ms; {plan.stats}")
@@ -160,6 +163,9 @@ def main():
             "tasks_completed": plan.stats["tasks_completed"],
             "tasks_total": plan.stats["tasks_total"],
             "mem_cap_gb_per_gpu": args.cap_gb,
+            "cost_model": args.cost_model,
+            "param_loads_per_step": sum(1 for i in plan.programs[rank].instrs if i.op == "load"),
+            "param_evictions_per_step": sum(1 for i in plan.programs[rank].instrs if i.op == "evict"),
             "scheduler": plan.scheduler_name,
             "tokens_per_s": round(tokens / (ms_per_step / 1e3), 1),
             "kernels_per_rank": plan.stats["kernels_per_rank"],

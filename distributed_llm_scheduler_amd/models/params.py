@@ -116,6 +116,7 @@ class ParamStore:
         self.device_init = device_init
         self.pin = (torch.cuda.is_available() and not device_init) if pin is None else pin
         self._host: Dict[str, torch.Tensor] = {}
+        self._images: Dict[str, torch.Tensor] = {}
         self._specs: Dict[str, TensorSpec] = {}
         for g in groups.values():
             for sp in g.tensors:
@@ -146,6 +147,24 @@ class ParamStore:
         else:
             out.copy_(self.tensor(name), non_blocking=True)
 
+    def group_image(self, pid: str) -> Optional[torch.Tensor]:
+        """The group as ONE host byte image in its arena layout (pinned), so a refill is a
+        single DMA of the whole group instead of a copy per tensor; ``None`` for
+        device-initialised stores (nothing on the host to copy)."""
+        if self.device_init:
+            return None
+        img = self._images.get(pid)
+        if img is None:
+            total, layout = group_layout(self.groups[pid], torch.tensor([], dtype=self.dtype).element_size())
+            img = torch.zeros(total, dtype=torch.uint8)
+            for spec, off in layout:
+                t = self.tensor(spec.name).contiguous()
+                img[off:off + t.numel() * t.element_size()].copy_(t.view(-1).view(torch.uint8))
+            if self.pin:
+                img = img.pin_memory()
+            self._images[pid] = img
+        return img
+
     def group_tensors(self, pid: str) -> List[Tuple[TensorSpec, torch.Tensor]]:
         return [(s, self.tensor(s.name)) for s in self.groups[pid].tensors]
 
@@ -160,6 +179,8 @@ class ParamStore:
             raise ValueError(f"{name}: expected shape {spec.shape}, got {tuple(value.shape)}")
         t = value.detach().to("cpu", self.dtype).contiguous()
         self._host[name] = t.pin_memory() if self.pin else t
+        self._images = {k: v for k, v in self._images.items()
+                        if all(sp.name != name for sp in self.groups[k].tensors)}
 
 
 GROUP_ALIGN = 256

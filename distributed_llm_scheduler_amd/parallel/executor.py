@@ -5,8 +5,12 @@ One process per GPU (``torch.distributed`` world, backend ``nccl`` = RCCL on ROC
 
 * activations live in ONE preallocated slab per rank at statically planned offsets
   (program.py); parameters in a second slab whose size is the per-GPU memory cap;
-* ``load`` copies a parameter group host(pinned)->HBM on the compute stream unless the
-  arena region still holds it from the previous step (steady-state residency);
+* ``load`` copies a parameter group host(pinned)->HBM unless the arena region still holds it
+  from the previous step (steady-state residency). On GPU the copy runs on a side copy
+  stream, issued as soon as the last kernel that used an overlapping arena region has been
+  enqueued (hipEvent fork), and the compute stream waits for it only at the load's own
+  position — parameter refills overlap the kernels in between (``DLS_PREFETCH=1``; default
+  in order on the compute stream). A refill is ONE DMA of the group's pinned host image;
 * ``recv``/``send`` are RCCL point-to-point ops (``dist.irecv``/``dist.isend``): RCCL runs
   them on its own stream ordered after the producing kernels, and the consumer waits
   stream-side (``work.wait()``), so transfers overlap the next independent kernels; a
@@ -61,6 +65,11 @@ FOLD_MAX_K = 1024  # fold a preceding norm into the GEMM only up to this K (see 
 GUARD_BYTES, GUARD_VALUE = 4096, 0xA5  # debug-mode canary after each arena slab
 # producer GEMMs emit row statistics for the next folded norm (GPU); DLS_STATS_HANDOFF=0 disables
 STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
+# parameter refills on a side copy stream, hoisted to the earliest safe point (GPU). Off by
+# default: measured on MI355X (gpt2-medium, 8 GB reference-cost cap, MRU_spec: 148 group
+# refills = 0.71 GB per step) the step is host-link bound (~37 GB/s) and the extra
+# cross-stream events cost more (20.4 ms) than the overlap returns (19.4 ms in order)
+PREFETCH = os.environ.get("DLS_PREFETCH", "0") == "1"
 
 
 class DAGExecutor:
@@ -146,6 +155,40 @@ class DAGExecutor:
                         self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
         if self.gpu and STATS_HANDOFF:
             self._plan_stats_handoff()
+        self._hoist: Dict[int, List[int]] = {}
+        self._copy_stream = None
+        if self.gpu and PREFETCH and any(i.op == "load" for i in p.instrs):
+            self._plan_prefetch()
+            self._copy_stream = torch.cuda.Stream(self.device)
+
+    def _plan_prefetch(self) -> None:
+        """For every ``load`` at instruction i: the earliest point it may start — right after
+        the last earlier instruction that touches an overlapping arena region (a kernel
+        group using a parameter group resident there, or an earlier load into it). The
+        copy is issued there on the copy stream; the mapping switch stays at i."""
+        region: Dict[str, Tuple[int, int]] = {}
+        touches: List[Tuple[int, List[Tuple[int, int]]]] = []
+        for i, ins in enumerate(self.prog.instrs):
+            if ins.op == "load":
+                off = self.prog.param_offset.get((i, ins.param))
+                if off is None:
+                    continue
+                size = group_layout(self.store.groups[ins.param])[0]
+                j = -1
+                for ti, regs in reversed(touches):
+                    if any(o < off + size and off < o + n for o, n in regs):
+                        j = ti
+                        break
+                self._hoist.setdefault(j, []).append(i)
+                region[ins.param] = (off, size)
+                touches.append((i, [(off, size)]))
+            elif ins.op == "run":
+                used = set()
+                for tid in ins.group:
+                    used |= self.tasks[tid].params_needed
+                regs = [region[q] for q in used if q in region]
+                if regs:
+                    touches.append((i, regs))
 
     def _plan_stats_handoff(self) -> None:
         """Pair every folded norm with the GEMM that produces its input on this rank: the
@@ -251,28 +294,60 @@ class DAGExecutor:
         return self.ws_slab[base:base + 2 * n].view(self.dtype).view(shape)
 
     # ------------------------------------------------------------- parameters
-    def _load(self, instr_index: int, pid: str, stats: StepStats) -> None:
+    def _group_views(self, instr_index: int, pid: str):
         off = self.prog.param_offset.get((instr_index, pid))
         if off is None:
             raise RuntimeError(f"parameter group {pid} did not fit the per-GPU parameter budget")
-        group = self.store.groups[pid]
-        total, layout = group_layout(group)
+        total, layout = group_layout(self.store.groups[pid])
         views = {}
         for spec, sub in layout:
             n = spec.numel
             views[spec.name] = self.param_slab[off + sub:off + sub + 2 * n].view(self.dtype).view(spec.shape)
+        return off, total, layout, views
+
+    def _fill(self, off, total, layout, views, pid, stats: StepStats) -> bool:
+        """Copy the group into its arena region unless the region already holds it."""
+        if (off, total, pid) in self._valid:
+            return False  # region still holds this group (steady-state residency)
+        self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
+        for spec, _ in layout:  # these weights are original again: drop stale folded-norm state
+            self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
+        img = self.store.group_image(pid) if self.gpu else None
+        if img is not None:  # one DMA of the whole group image
+            self.param_slab[off:off + total].copy_(img, non_blocking=True)
+        else:
+            for spec, _ in layout:
+                self.store.fill(spec.name, views[spec.name])
+        self._valid.append((off, total, pid))
+        stats.param_fills += 1
+        stats.bytes_filled += total
+        return True
+
+    def _prefetch(self, i: int, after, stats: StepStats, pending: Dict[int, object], events) -> None:
+        """Issue load i's copy on the copy stream behind the compute-stream event ``after``."""
+        pid = self.prog.instrs[i].param
+        off, total, layout, views = self._group_views(i, pid)
+        if (off, total, pid) in self._valid:
+            pending[i] = None
+            return
+        cs = self._copy_stream
+        cs.wait_event(after)
+        with torch.cuda.stream(cs):
+            t0 = self._mark() if events is not None else None
+            self._fill(off, total, layout, views, pid, stats)
+            done = torch.cuda.Event(enable_timing=events is not None)
+            done.record(cs)
+        if events is not None:
+            events.append((pid, "load", t0, done))
+        pending[i] = done
+
+    def _load(self, instr_index: int, pid: str, stats: StepStats) -> None:
+        off, total, layout, views = self._group_views(instr_index, pid)
         self._params[pid] = views
         self._wflat.update(views)
         if (off, total, pid) in self._valid:
             return  # region still holds this group (steady-state residency)
-        self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
-        for spec, _ in layout:  # these weights are original again: drop stale folded-norm state
-            self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
-        for spec, _ in layout:
-            self.store.fill(spec.name, views[spec.name])
-        self._valid.append((off, total, pid))
-        stats.param_fills += 1
-        stats.bytes_filled += total
+        self._fill(off, total, layout, views, pid, stats)
 
     def _evict(self, pid: str) -> None:
         for name in self._params.pop(pid, {}):
@@ -560,10 +635,24 @@ class DAGExecutor:
         if self._stats_slab is not None:
             self._stats_slab.zero_()
         recv_work: Dict[str, Tuple[object, object]] = {}
+        hoist = self._hoist if self._copy_stream is not None else None
+        pending: Dict[int, object] = {}
+        if hoist and -1 in hoist:
+            ev0 = torch.cuda.Event()
+            ev0.record()
+            for k in hoist[-1]:
+                self._prefetch(k, ev0, stats, pending, events)
         for i, ins in enumerate(self.prog.instrs):
             if tr:
                 Roctx.push(f"{ins.op}:{ins.task or ins.param}")
-            if ins.op == "load":
+            if ins.op == "load" and hoist is not None and i in pending:
+                off, total, layout, views = self._group_views(i, ins.param)
+                self._params[ins.param] = views
+                self._wflat.update(views)
+                done = pending.pop(i)
+                if done is not None:
+                    torch.cuda.current_stream(self.device).wait_event(done)
+            elif ins.op == "load":
                 t0 = self._mark() if events is not None else None
                 fills = stats.param_fills
                 self._load(i, ins.param, stats)
@@ -609,8 +698,16 @@ class DAGExecutor:
                 else:
                     self._run_group(ins)
                 stats.kernels += 1
+            if hoist and i in hoist:  # loads whose region is free from here on
+                ev = torch.cuda.Event()
+                ev.record()
+                for k in hoist[i]:
+                    self._prefetch(k, ev, stats, pending, events)
             if tr:
                 Roctx.pop()
+        for done in pending.values():  # (none in a well-formed program: each load is reached)
+            if done is not None:
+                torch.cuda.current_stream(self.device).wait_event(done)
         for w, _ in recv_work.values():
             w.wait()
         for _, _, w in self._pending_sends:
