@@ -61,6 +61,28 @@ def test_memory_capped_reloads_on_gpu():
     _check(p, ex, store, 0.03)
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_memory_capped_reloads_with_prefetch(monkeypatch, graph):
+    """Refills hoisted onto the side copy stream (DLS_PREFETCH=1) give the same logits."""
+    from distributed_llm_scheduler_amd.parallel import executor as exmod
+    monkeypatch.setattr(exmod, "PREFETCH", True)
+    full = runtime.plan("mini-gpt2", world=1, seq=64)
+    need = sum(runtime.make_store(full).nbytes(g) for g in full.groups) / 1e9
+    p = runtime.plan("mini-gpt2", world=1, seq=64, cap_gb=need * 0.5)
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=graph)
+    assert ex._copy_stream is not None and ex._hoist
+    for _ in range(2):
+        st = ex.step()
+    if graph:
+        assert ex.capture()
+        ex.step()
+    else:
+        assert st.param_fills > 0
+    torch.cuda.synchronize()
+    _check(p, ex, store, 0.03)
+
+
 def test_device_init_fills_hbm():
     p = runtime.plan("mini-llama", world=1, seq=64)
     store = runtime.make_store(p, device_init=True)
