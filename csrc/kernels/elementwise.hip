@@ -1,6 +1,8 @@
 // Memory-bound element-wise kernels: GELU(tanh), residual add, SwiGLU, token+position
 // embedding gather, rotary embedding. All move 16-byte (8 x bf16) vectors per lane and
 // grid-stride over at most 256 CUs x 8 blocks (cdna_hip_programming.md Guideline 11,13).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -50,10 +52,13 @@ __global__ __launch_bounds__(256) void swiglu_kernel(const bf16* __restrict__ gu
 }
 
 // y[m] = wte[tok[m]] + wpe[m % S] (wpe may be null: token embedding only)
+// zbuf (optional): fp32 words zeroed on the way (the step's row-statistics accumulators, so the
+// first node of the step clears them instead of a separate fill kernel)
 __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restrict__ tok,
                                                         const bf16* __restrict__ wte,
                                                         const bf16* __restrict__ wpe, bf16* __restrict__ y, int M,
-                                                        int S, int H) {
+                                                        int S, int H, float* __restrict__ zbuf, int zn) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < zn; i += gridDim.x * 256) zbuf[i] = 0.f;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -129,9 +134,9 @@ void launch_swiglu(const void* gu, void* y, int M, int F, hipStream_t s) {
 }
 
 void launch_embedding(const int32_t* tokens, const void* wte, const void* wpe, void* y, int M, int S, int H,
-                      hipStream_t s) {
+                      hipStream_t s, float* zbuf, int zn) {
   hipLaunchKernelGGL(embedding_kernel, dim3((M + 3) / 4), dim3(256), 0, s, tokens, (const bf16*)wte,
-                     (const bf16*)wpe, (bf16*)y, M, S, H);
+                     (const bf16*)wpe, (bf16*)y, M, S, H, zbuf, zn);
 }
 
 void launch_rope(void* qkv, int ld, int M, int S, int n_head, int n_kv_head, int D, int k_col, const float* cos_t,

@@ -275,7 +275,7 @@ at::Tensor swiglu(const at::Tensor& gu_in, const c10::optional<at::Tensor>& out)
 }
 
 at::Tensor embedding(const at::Tensor& tokens, const at::Tensor& wte, const c10::optional<at::Tensor>& wpe, int64_t S,
-                     const c10::optional<at::Tensor>& out) {
+                     const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& zero) {
   TORCH_CHECK(tokens.is_cuda() && tokens.scalar_type() == at::kInt && tokens.is_contiguous(),
               "tokens must be contiguous int32 on the GPU");
   check_bf16(wte, "wte");
@@ -288,8 +288,16 @@ at::Tensor embedding(const at::Tensor& tokens, const at::Tensor& wte, const c10:
   }
   at::Tensor y = out.has_value() ? as2d(*out) : at::empty({M, H}, wte.options());
   TORCH_CHECK(y.is_contiguous() && y.size(0) == M && y.size(1) == H, "out mismatch");
+  float* zb = nullptr;
+  int zn = 0;
+  if (zero.has_value()) {
+    TORCH_CHECK(zero->is_cuda() && zero->scalar_type() == at::kFloat && zero->is_contiguous(),
+                "zero must be a contiguous fp32 GPU tensor");
+    zb = zero->data_ptr<float>();
+    zn = (int)zero->numel();
+  }
   launch_embedding(tokens.data_ptr<int32_t>(), wte.data_ptr(), wpe.has_value() ? wpe->data_ptr() : nullptr,
-                   y.data_ptr(), (int)M, (int)S, (int)H, cur_stream());
+                   y.data_ptr(), (int)M, (int)S, (int)H, cur_stream(), zb, zn);
   return y;
 }
 
@@ -437,7 +445,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add", &add, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
   m.def("swiglu", &swiglu, py::arg("gate_up"), py::arg("out") = py::none());
   m.def("embedding", &embedding, py::arg("tokens"), py::arg("wte"), py::arg("wpe") = py::none(), py::arg("S") = 1,
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("zero") = py::none());
   m.def("rope_", &rope_);
   m.def("moe_router", &moe_router);
   m.def("moe_gather_combine", &moe_gather_combine);

@@ -356,9 +356,12 @@ def swiglu(gate_up, out=None):
     return out.copy_(y) if out is not None else y
 
 
-def embedding(tokens, wte, wpe=None, S=1, out=None):
+def embedding(tokens, wte, wpe=None, S=1, out=None, zero=None):
+    """``wte[tokens] (+ wpe[pos % S])``; ``zero`` (GPU fp32) is cleared by the same kernel."""
     if _gpu(wte):
-        return ext().embedding(tokens.to(torch.int32).contiguous(), wte, wpe, int(S), out)
+        return ext().embedding(tokens.to(torch.int32).contiguous(), wte, wpe, int(S), out, zero)
+    if zero is not None:
+        zero.zero_()
     t = tokens.reshape(-1).long()
     y = wte.float()[t]
     if wpe is not None:

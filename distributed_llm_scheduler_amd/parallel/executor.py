@@ -72,6 +72,7 @@ STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
 PREFETCH = os.environ.get("DLS_PREFETCH", "0") == "1"
 
 
+
 class DAGExecutor:
     def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
                  model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True,
@@ -155,6 +156,11 @@ class DAGExecutor:
                         self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
         if self.gpu and STATS_HANDOFF:
             self._plan_stats_handoff()
+        self._zero_in_embedding = False
+        if self._stats_slab is not None:
+            runs = [i for i in p.instrs if i.op == "run"]
+            first = self.tasks[runs[0].group[0]] if runs else None
+            self._zero_in_embedding = first is not None and first.op.kind == "embedding"
         self._hoist: Dict[int, List[int]] = {}
         self._copy_stream = None
         if self.gpu and PREFETCH and any(i.op == "load" for i in p.instrs):
@@ -533,7 +539,8 @@ class DAGExecutor:
                 tok = tok.reshape(-1) if B == 1 else tok.contiguous().view(-1)
                 if wpe is not None:
                     wpe = wpe[c * S:(c + 1) * S]
-            ops.embedding(tok, self._w(W["wte"]), wpe, S, out=self._flat(out))
+            zero = self._stats_slab if self._zero_in_embedding else None
+            ops.embedding(tok, self._w(W["wte"]), wpe, S, out=self._flat(out), zero=zero)
         elif k == "layernorm":
             ops.layernorm(self._flat(self._x(src)), self._w(W["w"]), self._w(W["b"]), a.get("eps", 1e-5),
                           out=self._flat(out))
@@ -632,8 +639,9 @@ class DAGExecutor:
         tr = self.trace
         self._pending_sends = []
         self._moe_memo = {}
-        if self._stats_slab is not None:
+        if self._stats_slab is not None and not self._zero_in_embedding:
             self._stats_slab.zero_()
+
         recv_work: Dict[str, Tuple[object, object]] = {}
         hoist = self._hoist if self._copy_stream is not None else None
         pending: Dict[int, object] = {}
