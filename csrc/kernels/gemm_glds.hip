@@ -517,9 +517,14 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   // fragment holds only 4 columns (8 B) of 16 different rows, so storing fragments directly
   // scatters 32-B pieces over 16 rows per instruction — partial lines that measured
   // ~1.2 TB/s on the 51 MB LM-head output; full rows run at the HBM write rate.
-  constexpr int BNC = C::BN / 8;  // 16-B chunks per tile row; image chunk c of row r sits at c ^ (r & 7)
-  static_assert(BNC >= 8, "staged epilogue swizzle needs BN >= 64");
-  static_assert(C::BM * C::BN * 2 <= C::LDS_UNITS * 16, "output tile image must fit the staging LDS");
+  // BNC 16-B chunks per tile row, stored in rows of BNP (power of two >= 8) chunks: image chunk
+  // c of row r sits at c ^ (r & 7), and BNP consecutive lanes own one row in the store pass
+  constexpr int BNC = C::BN / 8;
+  constexpr int BNP = BNC <= 8 ? 8 : BNC <= 16 ? 16 : BNC <= 32 ? 32 : 64;
+  static_assert(C::BN % 8 == 0 && BNC <= 64, "staged epilogue: BN % 8 == 0, BN <= 512");
+  static_assert(C::BM * BNP * 16 <= C::LDS_UNITS * 16, "output tile image must fit the staging LDS");
+  static_assert((C::BM * BNP) % 64 == 0 && ((C::BM * BNP) % C::T == 0 || C::BM * BNP < C::T),
+                "store pass: every wave makes the same number of passes (shuffles stay wave-uniform)");
   bf16* img = reinterpret_cast<bf16*>(smem);
   __syncthreads();  // every wave is done with the staging buffers (and the norm statistics)
 #pragma unroll
@@ -560,7 +565,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
       bf16x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-      *reinterpret_cast<bf16x4*>(img + rl * C::BN + (((cl >> 3) ^ (rl & 7)) << 3) + (cl & 7)) = o;
+      *reinterpret_cast<bf16x4*>(img + rl * BNP * 8 + (((cl >> 3) ^ (rl & 7)) << 3) + (cl & 7)) = o;
     }
   }
   __syncthreads();
@@ -568,14 +573,14 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
                    (!R || ((reinterpret_cast<uintptr_t>(R) | ((uintptr_t)ldr * 2)) & 15) == 0);
   const bf16x8* img8 = reinterpret_cast<const bf16x8*>(img);
   const int tid_ = threadIdx.x;
-  // consecutive groups of BNC threads own one tile row per pass (C::T % BNC == 0)
+  // consecutive groups of BNP threads own one tile row per pass (lanes past BNC idle)
 #pragma unroll 2
-  for (int q = tid_; q < C::BM * BNC; q += C::T) {
-    const int rl = q / BNC, cc = q % BNC;
+  for (int q = tid_; q < C::BM * BNP; q += C::T) {
+    const int rl = q / BNP, cc = q % BNP;
     const int row = m0 + rl, col = n0 + cc * 8;
-    bf16x8 o = img8[rl * BNC + (cc ^ (rl & 7))];
+    bf16x8 o = img8[rl * BNP + (cc ^ (rl & 7))];
     float s1 = 0.f, s2 = 0.f;
-    if (row < M && col < N) {
+    if (cc < BNC && row < M && col < N) {
       if (v16 && col + 8 <= N) {
         if (R) {
           const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(R + (size_t)row * ldr + col);
@@ -605,7 +610,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     }
     if (ep.stats_out) {
 #pragma unroll
-      for (int o_ = 1; o_ < BNC; o_ <<= 1) {
+      for (int o_ = 1; o_ < BNP; o_ <<= 1) {
         s1 += __shfl_xor(s1, o_, 64);
         s2 += __shfl_xor(s2, o_, 64);
       }
@@ -904,6 +909,15 @@ using C18 = Cfg<128, 64, 2, 2, 2, 0, 0, 2>;  // 2 x 48 KiB
 using C19 = Cfg<64, 128, 2, 2, 2, 0, 0, 2>;
 using C20 = Cfg<64, 64, 2, 2, 2, 0, 0, 4>;   // four K groups: 16 waves, 2 x 64 KiB stages
 using C21 = Cfg<64, 64, 1, 2, 2, 0, 0, 4>;   // four K groups of 2 waves (64x32 each)
+// tiles sized so a 512-row GEMM covers the 256 CUs exactly once (per-CU L2->LDS bytes, not
+// MFMA rate, bound these: 512x3072 -> 8x32 tiles of 64x96, 512x2304 -> 16x16 of 32x144,
+// 512x768 -> 16x16 of 32x48)
+using C22 = Cfg<64, 96, 2, 2, 4>;
+using C23 = Cfg<32, 144, 2, 1, 4>;
+using C24 = Cfg<32, 48, 2, 1, 4>;
+using C25 = Cfg<64, 96, 2, 2, 3, 0, 0, 2>;
+using C26 = Cfg<32, 144, 2, 1, 3, 0, 0, 2>;
+using C27 = Cfg<32, 48, 2, 1, 4, 0, 0, 2>;
 
 struct Shape {
   int bm, bn;
@@ -911,9 +925,11 @@ struct Shape {
 constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64, 128},  {64, 64},
                              {128, 64},  {128, 128}, {256, 256}, {256, 256}, {256, 128}, {128, 128},
                              {256, 256}, {256, 256}, {256, 128}, {128, 128}, {64, 64},   {64, 64},
-                             {128, 64},  {64, 128},  {64, 64},   {64, 64}};
-constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 128, 128, 128, 128, 256, 256};
-constexpr int kNumCfg = 22;
+                             {128, 64},  {64, 128},  {64, 64},   {64, 64},   {64, 96},   {32, 144},
+                             {32, 48},   {64, 96},   {32, 144},  {32, 48}};
+constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
+                          64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128};
+constexpr int kNumCfg = 28;
 
 }  // namespace
 
@@ -957,6 +973,9 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
     if (kShapes[cfg < kNumCfg ? cfg : 3].bm * kShapes[cfg < kNumCfg ? cfg : 3].bn > 256 * 128) cfg = 0;
     if (cfg < kNumCfg && kKStep[cfg] != 64) cfg = 3;  // K groups: no in-kernel row statistics
   }
+  // the SwiGLU epilogue pairs 16-column gate/up fragments: wave tiles must be multiples of 32
+  // columns (configs 22-27 have 48- / 144-column wave tiles)
+  if (a.act == kActSwiglu && cfg >= 22 && cfg < kNumCfg) cfg = kKStep[cfg] == 64 ? 3 : 17;
 #define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist)
   switch (cfg) {
     case 0: DLS_L(C0); break;
@@ -980,6 +999,12 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
     case 19: DLS_L(C19); break;
     case 20: DLS_L(C20); break;
     case 21: DLS_L(C21); break;
+    case 22: DLS_L(C22); break;
+    case 23: DLS_L(C23); break;
+    case 24: DLS_L(C24); break;
+    case 25: DLS_L(C25); break;
+    case 26: DLS_L(C26); break;
+    case 27: DLS_L(C27); break;
     default: DLS_L(C3); break;
   }
 #undef DLS_L

@@ -121,9 +121,9 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
 
 def kstep(cfg: int) -> int:
     """K granularity of an LDS-DMA config (csrc gemm_glds kKStep): 64, or 128 / 256 for the
-    two / four K-group configs 16-19 / 20-21."""
+    two / four K-group configs 16-19, 25-27 / 20-21."""
     c = cfg % PERSIST if cfg < REGSTAGE else 0
-    return 256 if c in (20, 21) else 128 if 16 <= c <= 19 else 64
+    return 256 if c in (20, 21) else 128 if (16 <= c <= 19 or 25 <= c <= 27) else 64
 
 
 def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
@@ -132,6 +132,8 @@ def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
         ks = kstep(cfg)
         if ks > 64 and "r" in tg:
             continue  # K-group configs are not offered for device-side row ranges (MoE experts)
+        if cfg >= 22 and "s" in tg:
+            continue  # 48/144-column wave tiles cannot pair SwiGLU gate/up fragments
         for sk in (1, 2, 3, 4, 6, 8):
             if K % 64 or K % (ks * sk) or (sk > 1 and N % 8) or K // (ks * sk) < 2:
                 continue
