@@ -649,6 +649,23 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     }
     return;
   }
+  if constexpr (RANGED == 3) {
+    // grouped MoE experts: block (g, tn) walks expert g's row range [rows[g], rows[g+1]) of
+    // its column panel with expert g's weight; consecutive blocks share an expert (its rows
+    // stay L2-resident while its weight panels stream)
+    const int g = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    const int r0 = rows[g], cnt = rows[g + 1] - r0;
+    const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
+    const bf16* Wg = reinterpret_cast<const bf16*>(ep.grp_w[g]);
+    bf16* Cg = ep.grp_c ? reinterpret_cast<bf16*>(ep.grp_c[g]) : Cp + (size_t)r0 * ldc;
+    const bf16* Ag = A + (size_t)r0 * lda;
+    for (int t = 0; t * C::BM < Mr; ++t) {
+      if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
+      glds_tile<C, 0>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act, alpha, 0, K, t,
+                      tn, ln_colsum, 0, ln_eps, ep);
+    }
+    return;
+  }
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
   const int ks = bid / ntile, tile = bid % ntile;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
@@ -931,6 +948,41 @@ constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64
                           64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128};
 constexpr int kNumCfg = 28;
 
+// call f(Cfg{}) for config id cfg (unknown ids: C3)
+template <class F>
+void with_cfg(int cfg, F&& f) {
+  switch (cfg) {
+    case 0: f(C0{}); break;
+    case 1: f(C1{}); break;
+    case 2: f(C2{}); break;
+    case 4: f(C4{}); break;
+    case 5: f(C5{}); break;
+    case 6: f(C6{}); break;
+    case 7: f(C7{}); break;
+    case 8: f(C8{}); break;
+    case 9: f(C9{}); break;
+    case 10: f(C10{}); break;
+    case 11: f(C11{}); break;
+    case 12: f(C12{}); break;
+    case 13: f(C13{}); break;
+    case 14: f(C14{}); break;
+    case 15: f(C15{}); break;
+    case 16: f(C16{}); break;
+    case 17: f(C17{}); break;
+    case 18: f(C18{}); break;
+    case 19: f(C19{}); break;
+    case 20: f(C20{}); break;
+    case 21: f(C21{}); break;
+    case 22: f(C22{}); break;
+    case 23: f(C23{}); break;
+    case 24: f(C24{}); break;
+    case 25: f(C25{}); break;
+    case 26: f(C26{}); break;
+    case 27: f(C27{}); break;
+    default: f(C3{}); break;
+  }
+}
+
 }  // namespace
 
 int gemm_glds_num_configs() { return kNumCfg; }
@@ -976,36 +1028,19 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
   // the SwiGLU epilogue pairs 16-column gate/up fragments: wave tiles must be multiples of 32
   // columns (configs 22-27 have 48- / 144-column wave tiles)
   if (a.act == kActSwiglu && cfg >= 22 && cfg < kNumCfg) cfg = kKStep[cfg] == 64 ? 3 : 17;
-#define DLS_L(CF) launch<CF>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist)
-  switch (cfg) {
-    case 0: DLS_L(C0); break;
-    case 1: DLS_L(C1); break;
-    case 2: DLS_L(C2); break;
-    case 4: DLS_L(C4); break;
-    case 5: DLS_L(C5); break;
-    case 6: DLS_L(C6); break;
-    case 7: DLS_L(C7); break;
-    case 8: DLS_L(C8); break;
-    case 9: DLS_L(C9); break;
-    case 10: DLS_L(C10); break;
-    case 11: DLS_L(C11); break;
-    case 12: DLS_L(C12); break;
-    case 13: DLS_L(C13); break;
-    case 14: DLS_L(C14); break;
-    case 15: DLS_L(C15); break;
-    case 16: DLS_L(C16); break;
-    case 17: DLS_L(C17); break;
-    case 18: DLS_L(C18); break;
-    case 19: DLS_L(C19); break;
-    case 20: DLS_L(C20); break;
-    case 21: DLS_L(C21); break;
-    case 22: DLS_L(C22); break;
-    case 23: DLS_L(C23); break;
-    case 24: DLS_L(C24); break;
-    case 25: DLS_L(C25); break;
-    case 26: DLS_L(C26); break;
-    case 27: DLS_L(C27); break;
-    default: DLS_L(C3); break;
-  }
-#undef DLS_L
+  with_cfg(cfg, [&](auto c) { launch<decltype(c)>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist); });
+}
+
+void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const int* offsets,
+                              const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s) {
+  cfg &= kGemmPersist - 1;
+  if (a.act == kActSwiglu && cfg >= 22 && cfg < kNumCfg) cfg = kKStep[cfg] == 64 ? 3 : 17;
+  with_cfg(cfg, [&](auto c) {
+    using C = decltype(c);
+    const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs};
+    const int tiles_n = (a.N + C::BN - 1) / C::BN;
+    hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(n_groups * tiles_n), dim3(C::T), 0, s, (const bf16*)a.A,
+                       a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0, nullptr, a.M, a.N, a.K, a.act,
+                       a.alpha, 1, tiles_n, 1, a.K, nullptr, 0, 1e-5f, offsets, a.compact_rows, ep);
+  });
 }

@@ -51,6 +51,10 @@ struct Epi {
   // in-launch split-K combine: one arrival counter per output tile (zero before the launch,
   // reset by each tile's last arriver); nullptr -> separate reduce kernel
   int* tile_sem = nullptr;
+  // grouped launch (every expert of an MoE layer in ONE grid): per-group weight pointers and,
+  // for compact outputs, per-group output pointers (device arrays of E addresses)
+  const unsigned long long* grp_w = nullptr;
+  const unsigned long long* grp_c = nullptr;
 };
 
 int gemm_pick_config(int M, int N, int K);
@@ -71,6 +75,12 @@ size_t gemm_glds_workspace_bytes(int M, int N, int splitk);
 void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s,
                       const float* ln_colsum = nullptr, int ln_mode = 0, float ln_eps = 1e-5f,
                       const int* rows = nullptr);
+// Grouped MoE-expert GEMM: E groups in ONE launch (grid = E x column tiles). Group g multiplies
+// rows [offsets[g], offsets[g+1]) of A by its own weight (w_ptrs[g], [N][K], ldw = a.ldw) and
+// writes them either at the same rows of a.C (c_ptrs == nullptr) or compactly to rows
+// 0..min(count, a.compact_rows)-1 of c_ptrs[g]. No split-K; any LDS-DMA config.
+void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const int* offsets,
+                              const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s);
 
 struct AttnArgs {
   const void* q; int ldq;   // bf16, row = token (b*S + s), head h at column h*D

@@ -384,6 +384,66 @@ at::Tensor grouped_gemm(const at::Tensor& X, const at::Tensor& offsets, const at
   return Y;
 }
 
+// Every expert of an MoE layer in ONE LDS-DMA GEMM launch. x: expert-sorted rows [R][K];
+// weights: E tensors [N][K] (validated here) whose addresses the caller caches in w_ptrs
+// (int64 [E] on the device: hipGraph-safe); offsets int32 [E+1]. Output: `out` [R][N'] at the
+// rows' own positions, or (outs + out_ptrs) E compact outputs, rows 0..min(count, cap)-1 each.
+void gemm_grouped(const at::Tensor& x, const std::vector<at::Tensor>& weights, const at::Tensor& w_ptrs,
+                  const at::Tensor& offsets, int64_t act, const c10::optional<at::Tensor>& out,
+                  const std::vector<at::Tensor>& outs, const c10::optional<at::Tensor>& out_ptrs, int64_t config) {
+  const int64_t E = (int64_t)weights.size();
+  check_bf16(x, "x");
+  check_rows(x, "x");
+  TORCH_CHECK(E > 0, "at least one expert");
+  const int64_t R = x.size(0), K = x.size(1), N = weights[0].size(0);
+  const bool sw = act == kActSwiglu;
+  const int64_t NO = sw ? N / 2 : N;
+  for (const auto& w : weights) {
+    check_bf16(w, "expert weight");
+    TORCH_CHECK(w.is_contiguous() && w.dim() == 2 && w.size(0) == N && w.size(1) == K, "expert weights [N][K]");
+  }
+  TORCH_CHECK(w_ptrs.is_cuda() && w_ptrs.scalar_type() == at::kLong && w_ptrs.numel() == E, "w_ptrs int64 [E]");
+  TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.numel() == E + 1,
+              "offsets int32 [E+1]");
+  const int cfg = (int)(config < 0 ? 3 : config);
+  TORCH_CHECK((cfg & (kGemmPersist - 1)) < gemm_glds_num_configs() && K % gemm_glds_kstep(cfg) == 0,
+              "grouped GEMM: config ", cfg, " needs K % ", gemm_glds_kstep(cfg), " == 0");
+  TORCH_CHECK(!sw || N % 32 == 0, "SwiGLU needs interleaved gate/up rows (N % 32 == 0)");
+  GemmArgs g{};
+  g.A = x.data_ptr();
+  g.lda = (int)x.stride(0);
+  g.ldw = (int)K;
+  g.M = (int)R;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.act = (int)act;
+  g.alpha = 1.0f;
+  const unsigned long long* cp = nullptr;
+  if (out_ptrs.has_value()) {
+    TORCH_CHECK((int64_t)outs.size() == E && out_ptrs->is_cuda() && out_ptrs->scalar_type() == at::kLong &&
+                    out_ptrs->numel() == E,
+                "compact outputs: E tensors + int64 [E] addresses");
+    const int64_t cap = outs[0].size(0);
+    for (const auto& o : outs) {
+      check_bf16(o, "expert output");
+      TORCH_CHECK(o.dim() == 2 && o.is_contiguous() && o.size(1) == NO && o.size(0) == cap,
+                  "expert outputs: E contiguous [cap][N'] tensors");
+    }
+    g.ldc = (int)NO;
+    g.compact_rows = (int)cap;
+    cp = reinterpret_cast<const unsigned long long*>(out_ptrs->data_ptr<int64_t>());
+  } else {
+    TORCH_CHECK(out.has_value(), "grouped GEMM needs `out` or compact outputs");
+    check_bf16(*out, "out");
+    check_rows(*out, "out");
+    TORCH_CHECK(out->size(0) == R && out->size(1) == NO, "out must be [R][N'] (N' = N/2 with SwiGLU)");
+    g.C = out->data_ptr();
+    g.ldc = (int)out->stride(0);
+  }
+  launch_gemm_glds_grouped(g, cfg, (int)E, offsets.data_ptr<int32_t>(),
+                           reinterpret_cast<const unsigned long long*>(w_ptrs.data_ptr<int64_t>()), cp, cur_stream());
+}
+
 // experts: list of E compact [rows][H] bf16 outputs; ptrs: int64 [E] device tensor holding
 // their addresses (built once by the caller and cached — hipGraph-safe)
 at::Tensor moe_gather_combine(const std::vector<at::Tensor>& experts, const at::Tensor& ptrs, const at::Tensor& idx,
@@ -454,4 +514,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_combine", &moe_combine, py::arg("expert_out"), py::arg("slot_of"), py::arg("weights"),
         py::arg("range") = py::none(), py::arg("out") = py::none());
   m.def("grouped_gemm", &grouped_gemm, py::arg("X"), py::arg("offsets"), py::arg("W"), py::arg("act") = 0);
+  m.def("gemm_grouped", &gemm_grouped, py::arg("x"), py::arg("weights"), py::arg("w_ptrs"), py::arg("offsets"),
+        py::arg("act") = 0, py::arg("out") = py::none(), py::arg("outs") = std::vector<at::Tensor>{},
+        py::arg("out_ptrs") = py::none(), py::arg("config") = -1);
 }

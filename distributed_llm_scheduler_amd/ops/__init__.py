@@ -466,6 +466,44 @@ def moe_expert(h, router_logits, w_gate_up, w_down, expert, n_experts, top_k, ou
     return moe_combine(y, slot, gate, rng, out)
 
 
+def gemm_grouped(x, weights, offsets, act=None, out=None, outs=None, w_ptrs=None, out_ptrs=None, rows_hint=None):
+    """Every expert of an MoE layer in ONE GEMM launch (GPU: LDS-DMA kernel, grid = experts x
+    column tiles). Expert e multiplies the expert-sorted rows [offsets[e], offsets[e+1]) of
+    ``x`` by ``weights[e]`` ([N][K]; SwiGLU: gate/up-interleaved, N/2 outputs) and writes them
+    at the same rows of ``out``, or compactly to rows 0.. of ``outs[e]`` (at most its row
+    count). ``w_ptrs`` / ``out_ptrs``: cached int64 device tensors of the tensors' addresses
+    (built here when omitted — pass cached ones inside a hipGraph)."""
+    a = ACT[act] if not isinstance(act, int) else act
+    E = len(weights)
+    N, K = weights[0].shape
+    if _gpu(x):
+        if w_ptrs is None:
+            w_ptrs = torch.tensor([w.data_ptr() for w in weights], dtype=torch.int64, device=x.device)
+        if outs is not None and out_ptrs is None:
+            out_ptrs = torch.tensor([o.data_ptr() for o in outs], dtype=torch.int64, device=x.device)
+        hint = rows_hint or max(1, x.shape[0] // E)
+        # grouped variants ("g"): tuned as GROUPS experts of `hint` rows in one launch; until
+        # tuned, the per-expert row-range choice ("r") stands in
+        cfg, _ = tuning.lookup_fused(hint, N, K, ("s" if a == SWIGLU else "") + "g")
+        if cfg < 0:
+            cfg, _ = tuning.lookup_fused(hint, N, K, tuning.tag(a, True))
+        if cfg >= tuning.REGSTAGE:
+            cfg = -1
+        ext().gemm_grouped(x, list(weights), w_ptrs, offsets, a, out, list(outs) if outs is not None else [],
+                           out_ptrs, cfg)
+        return out if outs is None else outs
+    off = [int(v) for v in offsets.tolist()]
+    for e in range(E):
+        r0, r1 = off[e], off[e + 1]
+        if outs is not None:
+            n = min(r1 - r0, outs[e].shape[0])
+            if n > 0:
+                outs[e][:n] = ref_linear(x[r0:r0 + n], weights[e], act=act)
+        elif r1 > r0:
+            out[r0:r1] = ref_linear(x[r0:r1], weights[e], act=act)
+    return out if outs is None else outs
+
+
 def grouped_gemm(X, offsets, W, act=None):
     """Per-expert ``act(X_e @ W_e^T)`` over expert-sorted rows; W is [E][N][K]."""
     a = ACT[act] if not isinstance(act, int) else act

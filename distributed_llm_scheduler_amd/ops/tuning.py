@@ -130,17 +130,15 @@ def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
     out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1), (LIB, 1)]
     for cfg in range(n_cfg):
         ks = kstep(cfg)
-        if ks > 64 and "r" in tg:
-            continue  # K-group configs are not offered for device-side row ranges (MoE experts)
         if cfg >= 22 and "s" in tg:
             continue  # 48/144-column wave tiles cannot pair SwiGLU gate/up fragments
-        for sk in (1, 2, 3, 4, 6, 8):
+        for sk in ((1,) if "g" in tg else (1, 2, 3, 4, 6, 8)):  # grouped launches: no split-K
             if K % 64 or K % (ks * sk) or (sk > 1 and N % 8) or K // (ks * sk) < 2:
                 continue
             if sk > 1 and M * N > 2048 * 8192:
                 continue
             out.append((cfg, sk))
-    if M * N >= (8 << 20) and K % 64 == 0:
+    if M * N >= (8 << 20) and K % 64 == 0 and not tg:
         # many more tiles than resident blocks (LM heads): the persistent tile walk of the
         # 256x128 / 64x64 configs (ops_binding PERSIST = 32)
         out += [(PERSIST + c, 1) for c in (0, 3, 14) if c < n_cfg]
@@ -157,6 +155,8 @@ def tune(M: int, N: int, K: int, device=None, cold: bool = True, save: bool = Tr
     e = ext()
     dev = device or torch.device("cuda")
     act = 4 if "s" in tg else 0
+    if "g" in tg:
+        return _tune_grouped(e, M, N, K, dev, act, tg, save)
     rows_total = 4 * M if "r" in tg else M
     x = (torch.randn(rows_total, K, device=dev) * 0.5).bfloat16()
     rng = torch.tensor([M, 2 * M], dtype=torch.int32, device=dev) if "r" in tg else None
@@ -180,6 +180,41 @@ def tune(M: int, N: int, K: int, device=None, cold: bool = True, save: bool = Tr
             best = (cfg, sk, t)
         if verbose:
             print(f"  {M}x{N}x{K} cfg={cfg} splitk={sk}: {t:.2f} us")
+    del ws
+    if best is not None:
+        table()[_key(M, N, K, tg)] = (best[0], best[1])
+        _cands[_key(M, N, K, tg)] = [c for c, _ in sorted(results.items(), key=lambda kv: kv[1])[:4]]
+        if save:
+            _save()
+    return best, results
+
+
+GROUPS = 8  # experts per grouped microbenchmark launch (Mixtral-8x7B)
+
+
+def _tune_grouped(e, M: int, N: int, K: int, dev, act: int, tg: str, save: bool):
+    """Grouped MoE-expert launch ("g" variants): GROUPS experts of M routed rows each, every
+    expert its own weight (together far beyond the Infinity Cache: cold by construction)."""
+    E = GROUPS
+    x = (torch.randn(E * M, K, device=dev) * 0.5).bfloat16()
+    ws = [(torch.randn(N, K, device=dev) * 0.05).bfloat16() for _ in range(E)]
+    wp = torch.tensor([w.data_ptr() for w in ws], dtype=torch.int64, device=dev)
+    off = torch.arange(0, E * M + 1, M, dtype=torch.int32, device=dev)
+    if act == 4:
+        out, outs, op = torch.empty(E * M, N // 2, device=dev, dtype=torch.bfloat16), [], None
+    else:
+        out = None
+        outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(E)]
+        op = torch.tensor([o.data_ptr() for o in outs], dtype=torch.int64, device=dev)
+    best, results = None, {}
+    for cfg, sk in candidates(M, N, K, e.gemm_glds_num_configs(), tg):
+        try:
+            t = _graph_time(lambda i: e.gemm_grouped(x, ws, wp, off, act, out, outs, op, cfg), reps=4)
+        except RuntimeError:
+            continue
+        results[(cfg, sk)] = t
+        if best is None or t < best[2]:
+            best = (cfg, sk, t)
     del ws
     if best is not None:
         table()[_key(M, N, K, tg)] = (best[0], best[1])

@@ -70,6 +70,8 @@ STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
 # refills = 0.71 GB per step) the step is host-link bound (~37 GB/s) and the extra
 # cross-stream events cost more (20.4 ms) than the overlap returns (19.4 ms in order)
 PREFETCH = os.environ.get("DLS_PREFETCH", "0") == "1"
+# one grouped launch pair per MoE layer for the experts co-located on this rank (GPU)
+MOE_BATCH = os.environ.get("DLS_MOE_BATCH", "1") != "0"
 
 
 
@@ -161,11 +163,82 @@ class DAGExecutor:
             runs = [i for i in p.instrs if i.op == "run"]
             first = self.tasks[runs[0].group[0]] if runs else None
             self._zero_in_embedding = first is not None and first.op.kind == "embedding"
+        self._plan_moe_batches()
         self._hoist: Dict[int, List[int]] = {}
         self._copy_stream = None
         if self.gpu and PREFETCH and any(i.op == "load" for i in p.instrs):
             self._plan_prefetch()
             self._copy_stream = torch.cuda.Stream(self.device)
+
+    def _plan_moe_batches(self) -> None:
+        """Every expert node of one MoE layer that sits on this rank, back to back in the
+        program (only parameter loads between them), runs as ONE grouped launch pair (gate/up
+        with SwiGLU, then down) instead of two GEMMs per expert: grid = experts x column
+        tiles, so the layer's whole expert weight stream is one chip-wide launch. GPU only,
+        all experts of the layer here, and a program without evictions or p2p (parameters
+        never move, so the span's loads can be applied at the batch's first node)."""
+        self._moe_batch: Dict[int, Tuple[List[int], List[int]]] = {}
+        self._moe_skip: set = set()
+        self._moe_batched_ids: set = set()
+        self._moe_bufs: Dict[int, tuple] = {}
+        ins = self.prog.instrs
+        if not self.gpu or not MOE_BATCH or any(i.op in ("evict", "send", "recv") for i in ins):
+            return
+
+        def expert_of(j):
+            x = ins[j]
+            if x.op != "run" or len(x.group) != 1:
+                return None
+            t = self.tasks[x.group[0]]
+            return t if t.op is not None and t.op.kind == "moe_expert" else None
+
+        i = 0
+        while i < len(ins):
+            t0 = expert_of(i)
+            if t0 is None:
+                i += 1
+                continue
+            key = tuple(t0.op.inputs[:2])
+            members, loads, j = [i], [], i + 1
+            while j < len(ins):
+                t = expert_of(j)
+                if ins[j].op == "load":
+                    loads.append(j)
+                elif t is not None and tuple(t.op.inputs[:2]) == key:
+                    members.append(j)
+                else:
+                    break
+                j += 1
+            E = t0.op.attrs["n_experts"]
+            experts = sorted(self.tasks[ins[m].group[0]].op.attrs["expert"] for m in members)
+            if len(members) > 1 and experts == list(range(E)):
+                self._moe_batch[i] = (members, [ld for ld in loads if ld < members[-1]])
+                self._moe_skip |= set(members[1:])
+                self._moe_batched_ids |= {ins[m].group[0] for m in members}
+            i = j
+
+    def _run_moe_batch(self, i: int, stats: StepStats) -> None:
+        members, loads = self._moe_batch[i]
+        for ld in loads:  # fixed regions (no evictions): map the span's groups up front
+            self._load(ld, self.prog.instrs[ld].param, stats)
+        tasks = sorted((self.tasks[self.prog.instrs[m].group[0]] for m in members), key=lambda t: t.op.attrs["expert"])
+        a = tasks[0].op.attrs
+        E, K = a["n_experts"], a["top_k"]
+        off = self._moe_route(tasks[0].op.inputs[1], E, K)[4]
+        xp = self._moe_permuted(tasks[0].op.inputs[0], tasks[0].op.inputs[1], E, K)
+        R, F = xp.shape[0], a["ffn"]
+        w13 = [self._prep(t.op.weights["w_gate_up"], None, None, interleave=True)[0] for t in tasks]
+        w2 = [self._w(t.op.weights["w_down"]) for t in tasks]
+        outs = [self._flat(self._views[t.id]) for t in tasks]
+        ptrs = tuple(w.data_ptr() for w in w13 + w2 + outs)
+        cached = self._moe_bufs.get(i)
+        if cached is None or cached[0] != ptrs:
+            mk = lambda ts: torch.tensor([x.data_ptr() for x in ts], dtype=torch.int64, device=self.device)  # noqa: E731
+            cached = (ptrs, mk(w13), mk(w2), mk(outs))
+            self._moe_bufs[i] = cached
+        hbuf = self._scratch("moe_h", (R, F))
+        ops.gemm_grouped(xp, w13, off, act="swiglu", out=hbuf, w_ptrs=cached[1], rows_hint=max(1, R // E))
+        ops.gemm_grouped(hbuf, w2, off, outs=outs, w_ptrs=cached[2], out_ptrs=cached[3], rows_hint=max(1, R // E))
 
     def _plan_prefetch(self) -> None:
         """For every ``load`` at instruction i: the earliest point it may start — right after
@@ -262,7 +335,8 @@ class DAGExecutor:
                     N, K = spec[n].shape
                     if op.kind == "moe_expert":
                         hint = max(1, M * op.attrs["top_k"] // op.attrs["n_experts"])
-                        shapes.add((hint, N, K, "sr" if wk == "w_gate_up" else "r"))
+                        v = "g" if t.id in self._moe_batched_ids else "r"  # grouped launch or one range
+                        shapes.add((hint, N, K, ("s" if wk == "w_gate_up" else "") + v))
                     elif op.kind == "swiglu_mlp" and wk == "w_gate_up":
                         shapes.add((M, N, K, "s"))
                     else:
@@ -699,12 +773,17 @@ class DAGExecutor:
                         else:
                             keep.append((so, sb, w))
                     self._pending_sends = keep
-                if events is not None:
+                run = self._run_group
+                if i in self._moe_batch:  # the layer's experts in one grouped launch pair
+                    run = lambda _ins, _i=i: self._run_moe_batch(_i, stats)  # noqa: E731
+                elif i in self._moe_skip:  # ran with its layer's batch
+                    run = None
+                if run is not None and events is not None:
                     t0 = self._mark()
-                    self._run_group(ins)
+                    run(ins)
                     events.append((ins.task, "kernel", t0, self._mark()))
-                else:
-                    self._run_group(ins)
+                elif run is not None:
+                    run(ins)
                 stats.kernels += 1
             if hoist and i in hoist:  # loads whose region is free from here on
                 ev = torch.cuda.Event()

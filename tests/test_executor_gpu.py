@@ -83,6 +83,21 @@ def test_memory_capped_reloads_with_prefetch(monkeypatch, graph):
     _check(p, ex, store, 0.03)
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_moe_experts_batched_on_gpu(graph):
+    """All experts of each layer on one GPU run as one grouped launch pair; same logits."""
+    p = runtime.plan("mini-mixtral", world=1, seq=64, batch=2)
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=graph)
+    assert len(ex._moe_batch) == p.cfg.n_layer  # one batch per MoE layer
+    ex.step()
+    if graph:
+        assert ex.capture()
+        ex.step()
+    torch.cuda.synchronize()
+    _check(p, ex, store, 0.03)
+
+
 def test_device_init_fills_hbm():
     p = runtime.plan("mini-llama", world=1, seq=64)
     store = runtime.make_store(p, device_init=True)

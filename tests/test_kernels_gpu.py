@@ -246,7 +246,8 @@ def test_gemm_swiglu_epilogue(M, F, K, config, splitk):
 
 
 @pytest.mark.parametrize("act", [None, "swiglu"])
-@pytest.mark.parametrize("config,splitk", [(-1, 0), (3, 1), (7, 1), (3, 4), (0, 2), (12, 1), (15, 2)])
+@pytest.mark.parametrize("config,splitk", [(-1, 0), (3, 1), (7, 1), (3, 4), (0, 2), (12, 1), (15, 2),
+                                           (17, 1), (16, 2), (20, 1), (22, 1), (25, 1)])
 @pytest.mark.parametrize("r0,r1", [(100, 229), (0, 512), (300, 300), (448, 512)])
 def test_gemm_row_range(act, config, splitk, r0, r1):
     M, N, K = 512, 1024, 1024
@@ -297,6 +298,37 @@ def test_gemm_row_range_compact(config, splitk):
     ops.ext().gemm(x, w, None, None, 0, 1.0, out, config, splitk, None, 0, 1e-5, over, True)
     torch.cuda.synchronize()
     _close(out.cpu().float(), ops.ref_linear(x[:cap].cpu(), w.cpu()).float(), 2e-2)
+
+
+@pytest.mark.parametrize("config", [-1, 3, 15, 17, 25, 1])
+def test_gemm_grouped_experts(config):
+    """All experts of a layer in one launch: SwiGLU gate/up into shared rows, then the down
+    GEMM into per-expert compact outputs — against per-expert fp32 references."""
+    E, H, F, R = 4, 256, 384, 300
+    counts = [70, 0, 130, 100]
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=DEV)
+    x = _rand(R, H, seed=90)
+    w13 = [ops.interleave_gate_up(_rand(2 * F, H, scale=0.05, seed=91 + e)) for e in range(E)]
+    w2 = [_rand(H, F, scale=0.05, seed=95 + e) for e in range(E)]
+    h = torch.full((R, F), 5.0, dtype=torch.bfloat16, device=DEV)
+    cap = 120
+    outs = [torch.full((cap, H), 7.0, dtype=torch.bfloat16, device=DEV) for _ in range(E)]
+    ext = ops.ext()
+    wp13 = torch.tensor([w.data_ptr() for w in w13], dtype=torch.int64, device=DEV)
+    wp2 = torch.tensor([w.data_ptr() for w in w2], dtype=torch.int64, device=DEV)
+    op = torch.tensor([o.data_ptr() for o in outs], dtype=torch.int64, device=DEV)
+    ext.gemm_grouped(x, w13, wp13, off, 4, h, [], None, config)
+    ext.gemm_grouped(h, w2, wp2, off, 0, None, outs, op, config)
+    torch.cuda.synchronize()
+    o = off.tolist()
+    for e in range(E):
+        r0, r1 = o[e], o[e + 1]
+        if r1 > r0:
+            href = ops.ref_linear(x[r0:r1].cpu(), w13[e].cpu(), act="swiglu")
+            _close(h[r0:r1].cpu(), href.float(), 2e-2)
+            n = min(r1 - r0, cap)
+            _close(outs[e][:n].cpu(), ops.ref_linear(h[r0:r0 + n].cpu(), w2[e].cpu()).float(), 2e-2)
+        assert (outs[e][min(r1 - r0, cap):].cpu().float() == 7.0).all(), "rows past the expert's count were written"
 
 
 def test_moe_gather_combine():
