@@ -935,6 +935,15 @@ using C24 = Cfg<32, 48, 2, 1, 4>;
 using C25 = Cfg<64, 96, 2, 2, 3, 0, 0, 2>;
 using C26 = Cfg<32, 144, 2, 1, 3, 0, 0, 2>;
 using C27 = Cfg<32, 48, 2, 1, 4, 0, 0, 2>;
+// 128x128 with two K groups: each stage's DMA covers 256 contiguous bytes of every weight row
+// (two K-tiles back to back) — the HBM-streaming MoE expert GEMMs (128 routed rows, cold weights)
+using C28 = Cfg<128, 128, 2, 2, 2, 0, 0, 2>;
+// 192-row tiles: a top-2 expert of a 512-token batch gets ~128 +- 11 routed rows, so 128-row
+// tiles need a second pass over the WHOLE weight panel for most experts; 192 rows take any
+// such expert in one pass (its weights stream from HBM exactly once)
+using C29 = Cfg<192, 128, 2, 2, 3>;
+using C30 = Cfg<192, 128, 2, 2, 2, 0, 0, 2>;
+using C31 = Cfg<192, 128, 2, 2, 2, 0, 1>;  // split rings: 2 x 24 KiB A + 3 x 16 KiB W
 
 struct Shape {
   int bm, bn;
@@ -943,10 +952,12 @@ constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64
                              {128, 64},  {128, 128}, {256, 256}, {256, 256}, {256, 128}, {128, 128},
                              {256, 256}, {256, 256}, {256, 128}, {128, 128}, {64, 64},   {64, 64},
                              {128, 64},  {64, 128},  {64, 64},   {64, 64},   {64, 96},   {32, 144},
-                             {32, 48},   {64, 96},   {32, 144},  {32, 48}};
+                             {32, 48},   {64, 96},   {32, 144},  {32, 48},   {128, 128}, {192, 128},
+                             {192, 128}, {192, 128}};
 constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
-                          64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128};
-constexpr int kNumCfg = 28;
+                          64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128, 128,
+                          64, 128, 64};
+constexpr int kNumCfg = 32;
 
 // call f(Cfg{}) for config id cfg (unknown ids: C3)
 template <class F>
@@ -979,6 +990,10 @@ void with_cfg(int cfg, F&& f) {
     case 25: f(C25{}); break;
     case 26: f(C26{}); break;
     case 27: f(C27{}); break;
+    case 28: f(C28{}); break;
+    case 29: f(C29{}); break;
+    case 30: f(C30{}); break;
+    case 31: f(C31{}); break;
     default: f(C3{}); break;
   }
 }
@@ -1027,14 +1042,14 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
   }
   // the SwiGLU epilogue pairs 16-column gate/up fragments: wave tiles must be multiples of 32
   // columns (configs 22-27 have 48- / 144-column wave tiles)
-  if (a.act == kActSwiglu && cfg >= 22 && cfg < kNumCfg) cfg = kKStep[cfg] == 64 ? 3 : 17;
+  if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
   with_cfg(cfg, [&](auto c) { launch<decltype(c)>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist); });
 }
 
 void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const int* offsets,
                               const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s) {
   cfg &= kGemmPersist - 1;
-  if (a.act == kActSwiglu && cfg >= 22 && cfg < kNumCfg) cfg = kKStep[cfg] == 64 ? 3 : 17;
+  if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
   with_cfg(cfg, [&](auto c) {
     using C = decltype(c);
     const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs};

@@ -121,16 +121,16 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
 
 def kstep(cfg: int) -> int:
     """K granularity of an LDS-DMA config (csrc gemm_glds kKStep): 64, or 128 / 256 for the
-    two / four K-group configs 16-19, 25-27 / 20-21."""
+    two / four K-group configs 16-19, 25-28, 30 / 20-21."""
     c = cfg % PERSIST if cfg < REGSTAGE else 0
-    return 256 if c in (20, 21) else 128 if (16 <= c <= 19 or 25 <= c <= 27) else 64
+    return 256 if c in (20, 21) else 128 if (16 <= c <= 19 or 25 <= c <= 28 or c == 30) else 64
 
 
 def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
     out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1), (LIB, 1)]
     for cfg in range(n_cfg):
         ks = kstep(cfg)
-        if cfg >= 22 and "s" in tg:
+        if 22 <= cfg <= 27 and "s" in tg:
             continue  # 48/144-column wave tiles cannot pair SwiGLU gate/up fragments
         for sk in ((1,) if "g" in tg else (1, 2, 3, 4, 6, 8)):  # grouped launches: no split-K
             if K % 64 or K % (ks * sk) or (sk > 1 and N % 8) or K // (ks * sk) < 2:
@@ -199,12 +199,16 @@ def _tune_grouped(e, M: int, N: int, K: int, dev, act: int, tg: str, save: bool)
     x = (torch.randn(E * M, K, device=dev) * 0.5).bfloat16()
     ws = [(torch.randn(N, K, device=dev) * 0.05).bfloat16() for _ in range(E)]
     wp = torch.tensor([w.data_ptr() for w in ws], dtype=torch.int64, device=dev)
-    off = torch.arange(0, E * M + 1, M, dtype=torch.int32, device=dev)
+    # routed-row counts as top-k routing of random tokens spreads them (multinomial around M,
+    # so about half the experts get MORE than M rows — what a tile height must absorb)
+    g = torch.Generator().manual_seed(7)
+    cnt = torch.bincount(torch.randint(0, E, (E * M,), generator=g), minlength=E)
+    off = torch.cat([torch.zeros(1, dtype=torch.long), cnt.cumsum(0)]).to(torch.int32).to(dev)
     if act == 4:
         out, outs, op = torch.empty(E * M, N // 2, device=dev, dtype=torch.bfloat16), [], None
     else:
         out = None
-        outs = [torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(E)]
+        outs = [torch.empty(2 * M, N, device=dev, dtype=torch.bfloat16) for _ in range(E)]
         op = torch.tensor([o.data_ptr() for o in outs], dtype=torch.int64, device=dev)
     best, results = None, {}
     for cfg, sk in candidates(M, N, K, e.gemm_glds_num_configs(), tg):

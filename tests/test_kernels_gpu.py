@@ -48,7 +48,8 @@ def test_gemm_identity_asymmetric():
                                            (32, 1), (35, 1), (35, 4), (40, 1), (46, 1),  # 32+: persistent
                                            (16, 1), (17, 1), (18, 1), (19, 1), (16, 2), (17, 3), (48, 1),
                                            (20, 1), (21, 1), (21, 3), (22, 1), (23, 1), (24, 1),
-                                           (25, 1), (26, 1), (27, 1), (22, 4), (24, 2), (27, 3)])
+                                           (25, 1), (26, 1), (27, 1), (22, 4), (24, 2), (27, 3), (28, 1), (28, 2),
+                                           (29, 1), (30, 1), (31, 1), (31, 2)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
@@ -83,7 +84,7 @@ def test_gemm_epilogue(act):
 @pytest.mark.parametrize("B,S,nh,nkv,D,causal", [(1, 512, 12, 12, 64, True), (2, 200, 4, 4, 64, True),
                                                   (1, 256, 8, 2, 128, True), (1, 130, 4, 4, 64, False),
                                                   (1, 64, 32, 8, 128, True)])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", list(range(14)))
 def test_attention(B, S, nh, nkv, D, causal, variant):
     qkv = _rand(B * S, (nh + 2 * nkv) * D, seed=7)
     q, k, v = qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:]
@@ -300,7 +301,7 @@ def test_gemm_row_range_compact(config, splitk):
     _close(out.cpu().float(), ops.ref_linear(x[:cap].cpu(), w.cpu()).float(), 2e-2)
 
 
-@pytest.mark.parametrize("config", [-1, 3, 15, 17, 25, 1])
+@pytest.mark.parametrize("config", [-1, 3, 15, 17, 25, 1, 28, 29, 30, 31])
 def test_gemm_grouped_experts(config):
     """All experts of a layer in one launch: SwiGLU gate/up into shared rows, then the down
     GEMM into per-expert compact outputs — against per-expert fp32 references."""
