@@ -12,6 +12,7 @@ travel with the repository snapshot to the GPU box.
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -37,6 +38,36 @@ def _newer(out: str, srcs) -> bool:
     return any(os.path.getmtime(s) > t for s in srcs)
 
 
+def _digest(srcs) -> str:
+    h = hashlib.sha256()
+    for s in sorted(srcs):
+        h.update(os.path.relpath(s, REPO).encode())
+        with open(s, "rb") as f:
+            h.update(f.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()
+
+
+def _stale(out: str, srcs) -> bool:
+    """Does the library need a rebuild? By the sources' CONTENT hash recorded next to it at
+    link time (a copied snapshot — the GPU box, a fresh clone — keeps no meaningful mtimes,
+    and a rebuild there would be minutes of hipcc per process); by mtimes only when no
+    record exists."""
+    if not os.path.exists(out):
+        return True
+    stamp = out + ".srchash"
+    if os.path.exists(stamp):
+        with open(stamp) as f:
+            return f.read().strip() != _digest(srcs)
+    return _newer(out, srcs)
+
+
+def _record(out: str, srcs) -> None:
+    with open(out + ".srchash.tmp", "w") as f:
+        f.write(_digest(srcs))
+    os.replace(out + ".srchash.tmp", out + ".srchash")
+
+
 def _run(cmd, verbose):
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -51,7 +82,7 @@ def build_core(force: bool = False, verbose: bool = False) -> str:
 
     srcs = sorted(glob.glob(os.path.join(CSRC, "core", "*.cpp")) + glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "core", "*.h")) + glob.glob(os.path.join(CSRC, "runtime", "*.h")))
-    if not force and not _newer(CORE_SO, srcs + hdrs):
+    if not force and not _stale(CORE_SO, srcs + hdrs):
         return CORE_SO
     cmd = [
         os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
@@ -61,6 +92,7 @@ def build_core(force: bool = False, verbose: bool = False) -> str:
     ]
     _run(cmd, verbose)
     os.replace(CORE_SO + ".tmp", CORE_SO)
+    _record(CORE_SO, srcs + hdrs)
     return CORE_SO
 
 
@@ -83,7 +115,7 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
     binding = os.path.join(CSRC, "kernels", "ops_binding.cpp")
-    if not force and not _newer(OPS_SO, kern + hdrs + [binding]):
+    if not force and not _stale(OPS_SO, kern + hdrs + [binding]):
         return OPS_SO
     os.makedirs(BUILD_DIR, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
@@ -110,6 +142,7 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
               "-x", "c++", "-c", binding, "-o", bobj], verbose)
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, bobj, *libs, "-o", OPS_SO + ".tmp"], verbose)
     os.replace(OPS_SO + ".tmp", OPS_SO)
+    _record(OPS_SO, kern + hdrs + [binding])
     return OPS_SO
 
 
