@@ -22,7 +22,9 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 // last arriver resets its counter, so a region is zero again whenever it is reused.
 constexpr int64_t kSemPool = 1 << 20;
 int* split_k_counters(const at::Tensor& like, int64_t n) {
-  static at::Tensor pool[64];
+  // heap-held and never freed: a static tensor's destructor would run after the HIP runtime
+  // and the caching allocator have been torn down at interpreter exit
+  static at::Tensor* pool = new at::Tensor[64];
   static int64_t next[64];
   const int d = like.get_device();
   TORCH_CHECK(d >= 0 && d < 64 && n <= kSemPool, "split-K counters");

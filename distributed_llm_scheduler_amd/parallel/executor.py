@@ -62,6 +62,8 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
 
 
 FOLD_MAX_K = 1024  # fold a preceding norm into the GEMM only up to this K (see DAGExecutor._gemm)
+# widest norm input whose statistics a producer GEMM hands over (beyond it: a norm kernel)
+HANDOFF_MAX_K = int(os.environ.get("DLS_HANDOFF_MAX_K", str(FOLD_MAX_K)))
 GUARD_BYTES, GUARD_VALUE = 4096, 0xA5  # debug-mode canary after each arena slab
 # producer GEMMs emit row statistics for the next folded norm (GPU); DLS_STATS_HANDOFF=0 disables
 STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
@@ -298,7 +300,7 @@ class DAGExecutor:
                 # at K = 4096 the separate norm kernel is cheaper than the split-K reduce
                 # epilogue work (Llama-3-8B 9.89 vs 9.96 ms)
                 width = self.tasks[src].op.out_shape[-1] if src in self.tasks else 0
-                if pi is not None and emits(pi) and src not in need and width <= FOLD_MAX_K:
+                if pi is not None and emits(pi) and src not in need and width <= HANDOFF_MAX_K:
                     need.append(src)
         if not need:
             return
