@@ -55,6 +55,8 @@ struct Epi {
   // for compact outputs, per-group output pointers (device arrays of E addresses)
   const unsigned long long* grp_w = nullptr;
   const unsigned long long* grp_c = nullptr;
+  // grouped launch: weight DMA with the streaming (nt) cache policy (split-ring configs)
+  int w_stream = 0;
 };
 
 int gemm_pick_config(int M, int N, int K);
