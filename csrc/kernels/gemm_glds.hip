@@ -113,9 +113,12 @@ __device__ __forceinline__ void wait_ab(int a, int b) {
 
 // MFMAs of one staged K-tile: A rows at sA[row * CH], W rows at sB[row * CH] (both XOR
 // swizzled by row & 7, see the DMA source addresses).
-template <class C>
+// SKIP: only the wave's first fmv row fragments hold real rows (grouped experts: an expert's
+// routed rows end inside the tile) — the others are neither read nor multiplied
+template <class C, bool SKIP = false>
 __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int lane, int wm, int wn, bool ln_acc,
-                                         f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM], float (&st_q)[C::FM]) {
+                                         f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM], float (&st_q)[C::FM],
+                                         int fmv = C::FM) {
   // All fragments of the K-tile (both 32-deep halves) are requested before the first MFMA:
   // the second half's ds_reads then complete under the first half's MFMAs instead of
   // behind an lgkmcnt(0) (the compiler counts lgkmcnt per consumer).
@@ -130,6 +133,7 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
     }
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
+      if (SKIP && i >= fmv) break;
       const int row = wm * C::WTM + i * 16 + (lane & 15);
       af[kk][i] = sA[row * C::CH + (chunk ^ (row & 7))];
     }
@@ -151,9 +155,11 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
     // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
     if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < C::FM; ++i)
+    for (int i = 0; i < C::FM; ++i) {
+      if (SKIP && i >= fmv) break;
 #pragma unroll
       for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[kk][j], af[kk][i], acc[i][j]);
+    }
     if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
   }
 }
@@ -211,12 +217,12 @@ constexpr int kPolStream = 2;  // gfx950 CPol NT (streaming) bit of the DMA's au
 // Split rings (BXS > 0): issue order B0 [A0 B1] [A1 B2] ... — iteration t issues
 // A(t + SA - 1) then B(t + SB - 1). Waiting for A(t) then leaves a = min(SA-2, nk-1-t)
 // later A tiles and b = min(a + 1, nk-1-t) later W tiles in flight (B(t) precedes A(t)).
-template <class C, int WPOL = 0>
+template <class C, int WPOL = 0, bool SKIP = false>
 __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                                int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
                                                f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
-                                               float (&st_q)[C::FM]) {
+                                               float (&st_q)[C::FM], int fmv = C::FM) {
   static_assert(C::SB == C::SA + 1, "split rings: W ring is one deeper than A");
   const bf16* srcA[C::PWA];
   const bf16* srcB[C::PWB];
@@ -264,8 +270,8 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
     raw_barrier();
     if (kt + DA < nk) issueA(kt + DA);
     if (kt + DA + 1 < nk) issueB(kt + DA + 1);
-    mma_tile<C>(ringA + (kt % C::SA) * C::A_STAGE, ringB + (kt % C::SB) * C::B_STAGE, lane, wm, wn, ln_acc, acc,
-                st_s, st_q);
+    mma_tile<C, SKIP>(ringA + (kt % C::SA) * C::A_STAGE, ringB + (kt % C::SB) * C::B_STAGE, lane, wm, wn, ln_acc,
+                      acc, st_s, st_q, fmv);
   }
 }
 
@@ -275,7 +281,7 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 // they come from ep.ext_stats).
 // WPOL: cache policy of the split rings' weight DMA (0 default, kPolStream = nt for weights
 // read exactly once per step, e.g. MoE experts far larger than the MALL)
-template <class C, int LN, int WPOL = 0>
+template <class C, int LN, int WPOL = 0, bool SKIP = false>
 __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                           const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
                                           const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
@@ -304,8 +310,8 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
   if constexpr (C::BXS > 0)
-    mainloop_split<C, WPOL>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc, st_s,
-                            st_q);
+    mainloop_split<C, WPOL, SKIP>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
+                                  st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)));
   else
     mainloop_joint<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
                       st_q);
@@ -668,8 +674,8 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     for (int t = 0; t * C::BM < Mr; ++t) {
       if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
       if (C::BXS > 0 && ep.w_stream)
-        glds_tile<C, 0, kPolStream>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act,
-                                    alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep);
+        glds_tile<C, 0, kPolStream, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K,
+                                          act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep);
       else
         glds_tile<C, 0>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act, alpha, 0, K, t,
                         tn, ln_colsum, 0, ln_eps, ep);
