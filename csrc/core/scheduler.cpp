@@ -12,6 +12,10 @@ namespace dls {
 
 namespace {
 
+// EFT memory-fit slack (GB): fractional 'bytes' parameter costs summed in different
+// orders differ by a few ulps; 1e-9 GB = 1 byte.
+constexpr double kEftTol = 1e-9;
+
 // Kahn order over the known dependency edges. Tasks on a cycle are appended at the
 // end (they can never become ready, the reference would recurse forever on them).
 std::vector<int> topo_order(const Instance& I, std::vector<std::vector<int>>& dependents) {
@@ -173,8 +177,11 @@ struct Sched {
   }
 
   // --- assign = execute (schedulers.py:78-126) ---
-  bool assign(int t, int n) {
-    if (requirement(t, n) > avail[n]) return false;
+  // ``tol``: slack for the accumulated rounding of fractional parameter costs. The
+  // reference policies compare exactly (schedulers.py:66-76, tol = 0); EFT's dry-run
+  // eviction sums the same costs in another order, so it passes a small tolerance.
+  bool assign(int t, int n, double tol = 0.0) {
+    if (requirement(t, n) > avail[n] + tol) return false;
     for (int p : I.params[t]) {
       if (cached[n][p]) continue;
       cache_add(n, p);
@@ -408,7 +415,7 @@ struct Sched {
       for (int n = 0; n < N; ++n) {
         std::vector<int> victims;
         double need = requirement(t, n);
-        if (need > avail[n]) {
+        if (need > avail[n] + kEftTol) {
           if (!plan_eviction(t, n, need - avail[n], last_touch, victims)) continue;
         }
         double data_ready = 0.0;
@@ -444,8 +451,13 @@ struct Sched {
       R.start_time[t] = best_start;
       R.finish_time[t] = best_fin;
       // assign() completes the task and promotes dependents into live_ready; a
-      // dependent whose last missing input was t is newly ready now.
-      assign(t, best);
+      // dependent whose last missing input was t is newly ready now. plan_eviction freed
+      // >= shortage up to kEftTol, so this cannot fail; if it ever did, the task is
+      // failed explicitly instead of being left pending with its dependents orphaned.
+      if (!assign(t, best, kEftTol)) {
+        fail(t);
+        continue;
+      }
       for (int p : I.params[t]) {
         last_touch[static_cast<size_t>(best) * P + p] = best_fin;
         ++usage[p];
@@ -454,6 +466,10 @@ struct Sched {
       for (int d : dependents[t])
         if (remaining[d] == 0 && pending[d] && !unknown[d]) ready.insert(d);
     }
+    // Invariant: a task still pending here has a failed, orphaned or unknown input.
+    for (int t = 0; t < T; ++t)
+      if (pending[t] && remaining[t] == 0 && !unknown[t])
+        throw std::logic_error("EFT left a ready task unscheduled: " + I.task_ids[t]);
     R.rounds = step;
   }
 
@@ -476,11 +492,11 @@ struct Sched {
     });
     double freed = 0;
     for (int p : cand) {
-      if (freed >= shortage) break;
+      if (freed >= shortage - kEftTol) break;
       victims.push_back(p);
       freed += I.param_cost[p];
     }
-    return freed >= shortage;
+    return freed >= shortage - kEftTol;
   }
 
   Result finish() {

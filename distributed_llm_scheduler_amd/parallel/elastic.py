@@ -28,7 +28,8 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank: int, world: int, port: int, plan_kw: Dict, steps: int, device: str, fail: Optional[tuple], q):
+def _worker(rank: int, world: int, port: int, plan_kw: Dict, steps: int, device: str, fail: Optional[tuple], q,
+            devices: Optional[Sequence[int]] = None):
     import torch
     import torch.distributed as dist
 
@@ -36,7 +37,10 @@ def _worker(rank: int, world: int, port: int, plan_kw: Dict, steps: int, device:
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     gpu = device == "cuda"
-    dev = torch.device(f"cuda:{rank}") if gpu else torch.device("cpu")
+    # rank -> physical GPU: after a loss the survivors are renumbered 0..n-1 but keep their
+    # own devices (rank 1 of 3 lost: new ranks 0, 1 run on cuda:0, cuda:2)
+    phys = devices[rank] if devices is not None else rank
+    dev = torch.device(f"cuda:{phys}") if gpu else torch.device("cpu")
     if gpu:
         torch.cuda.set_device(dev)
     dist.init_process_group("nccl" if gpu else "gloo", rank=rank, world_size=world)
@@ -50,7 +54,7 @@ def _worker(rank: int, world: int, port: int, plan_kw: Dict, steps: int, device:
             ex.step()
         if gpu:
             torch.cuda.synchronize(dev)
-        res = {"rank": rank, "ok": True, "tasks": sum(1 for r in p.placement.values() if r == rank)}
+        res = {"rank": rank, "device": phys, "ok": True, "tasks": sum(1 for r in p.placement.values() if r == rank)}
         head = [t for t in p.placement if t.split("/")[-1] == "output_projection" and p.placement[t] == rank]
         if head:
             res["logits_sum"] = {t: float(ex.output(t).float().sum()) for t in head}
@@ -62,11 +66,14 @@ def _worker(rank: int, world: int, port: int, plan_kw: Dict, steps: int, device:
             pass
 
 
-def _launch(world: int, plan_kw: Dict, steps: int, device: str, fail: Optional[tuple], timeout: float):
+def _launch(world: int, plan_kw: Dict, steps: int, device: str, fail: Optional[tuple], timeout: float,
+            devices: Optional[Sequence[int]] = None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, plan_kw, steps, device, fail, q)) for r in range(world)]
+    devices = list(devices) if devices is not None else list(range(world))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, plan_kw, steps, device, fail, q, devices))
+             for r in range(world)]
     for pr in procs:
         pr.start()
     deadline = time.time() + timeout
@@ -92,21 +99,31 @@ def _launch(world: int, plan_kw: Dict, steps: int, device: str, fail: Optional[t
 
 
 def run_elastic(world: int, steps: int = 2, fail_rank: Optional[int] = None, fail_step: int = 1,
-                device: str = "cpu", timeout: float = 300.0, max_restarts: int = 2, **plan_kw) -> Dict:
+                device: str = "cpu", timeout: float = 300.0, max_restarts: int = 2,
+                devices: Optional[Sequence[int]] = None, **plan_kw) -> Dict:
     """Run ``steps`` DAG steps on ``world`` devices, surviving device loss by re-planning.
-    ``plan_kw`` are :func:`runtime.plan` arguments (model, scheduler, cap_gb, replicas, ...).
-    Returns the attempts (world size, lost ranks) and the final per-rank results."""
+    ``plan_kw`` are :func:`runtime.plan` arguments (model, scheduler, cap_gb, replicas, ...);
+    ``devices`` the physical GPU of each initial rank (default 0..world-1). Returns the
+    attempts (world size, lost ranks, physical devices) and the final per-rank results."""
     from . import runtime
 
     attempts = []
     fail = (fail_rank, fail_step) if fail_rank is not None else None
     cur = world
+    devs = list(devices) if devices is not None else list(range(world))
+    if len(devs) != world:
+        raise ValueError(f"{len(devs)} devices given for world {world}")
+    kw = dict(plan_kw)
     for _ in range(max_restarts + 1):
-        lost, results = _launch(cur, plan_kw, steps, device, fail, timeout)
-        attempts.append({"world": cur, "lost": lost})
+        lost, results = _launch(cur, kw, steps, device, fail, timeout, devs)
+        attempts.append({"world": cur, "lost": lost, "devices": list(devs)})
         if not lost:
-            return {"attempts": attempts, "world": cur, "results": results}
-        base = runtime.plan(world=cur, **plan_kw)
-        cur = runtime.replan(base, lost).world
+            return {"attempts": attempts, "world": cur, "devices": devs, "results": results}
+        base = runtime.plan(world=cur, **kw)
+        new = runtime.replan(base, lost)
+        # the survivors keep their physical devices and (via replan) their node speeds
+        devs = [d for r, d in enumerate(devs) if r not in set(lost)]
+        cur = new.world
+        kw = {k: v for k, v in new.args.items() if k != "world"}
         fail = None  # the injected loss happened once
     raise RuntimeError(f"giving up after {len(attempts)} attempts: {attempts}")

@@ -14,7 +14,8 @@ One process per GPU (``torch.distributed`` world, backend ``nccl`` = RCCL on ROC
 * ``recv``/``send`` are RCCL point-to-point ops (``dist.irecv``/``dist.isend``): RCCL runs
   them on its own stream ordered after the producing kernels, and the consumer waits
   stream-side (``work.wait()``), so transfers overlap the next independent kernels; a
-  sent buffer is only overwritten after its send completes;
+  sent buffer is only overwritten (by a kernel or by a recv from another peer) after its
+  send completes (waits planned statically, ``Instr.wait_sends``);
 * ``run`` launches the (fused) kernel group through :mod:`ops` — HIP kernels on GPU;
 * programs without p2p ops are captured once into a hipGraph (``torch.cuda.CUDAGraph``)
   and replayed, removing per-kernel host launch cost from the step.
@@ -107,7 +108,7 @@ class DAGExecutor:
         self._ext_stats: Dict[str, torch.Tensor] = {}   # the same buffers, by the tensor a norm reads
         self._stats_slab: Optional[torch.Tensor] = None
         self._moe_ptrs: Dict[tuple, torch.Tensor] = {}
-        self._pending_sends: List[Tuple[int, int, object]] = []
+        self._pending_sends: Dict[int, object] = {}  # send instruction index -> RCCL work
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._setup()
@@ -713,7 +714,7 @@ class DAGExecutor:
         """Issue the program. ``events`` (profiling) collects (name, category, t0, t1) tokens."""
         pg = self.pg
         tr = self.trace
-        self._pending_sends = []
+        self._pending_sends = {}
         self._moe_memo = {}
         if self._stats_slab is not None and not self._zero_in_embedding:
             self._stats_slab.zero_()
@@ -745,6 +746,7 @@ class DAGExecutor:
             elif ins.op == "evict":
                 self._evict(ins.param)
             elif ins.op == "recv":
+                self._wait_sends(ins)  # the recv buffer may still be read by a send to another peer
                 t0 = self._mark() if events is not None else None
                 recv_work[ins.task] = (dist.irecv(self._views[ins.task], src=ins.peer, group=pg), t0)
                 stats.recvs += 1
@@ -752,8 +754,7 @@ class DAGExecutor:
                 buf = self._views[ins.task]
                 t0 = self._mark() if events is not None else None
                 w = dist.isend(buf, dst=ins.peer, group=pg)
-                off = self.prog.act_offset[ins.task]
-                self._pending_sends.append((off, self.prog.act_bytes[ins.task], w))
+                self._pending_sends[i] = w
                 if events is not None:
                     events.append((f"{ins.task}->gpu{ins.peer}", "send", t0, self._mark()))
                 stats.sends += 1
@@ -766,15 +767,7 @@ class DAGExecutor:
                             rw[0].wait()
                             if events is not None:
                                 events.append((d, "recv", rw[1], self._mark()))
-                off, nb = self.prog.act_offset[ins.task], self.prog.act_bytes[ins.task]
-                if self._pending_sends:
-                    keep = []
-                    for so, sb, w in self._pending_sends:
-                        if so < off + nb and off < so + sb:
-                            w.wait()  # buffer about to be overwritten: its send must be done
-                        else:
-                            keep.append((so, sb, w))
-                    self._pending_sends = keep
+                self._wait_sends(ins)  # output region about to be overwritten: its sends must be done
                 run = self._run_group
                 if i in self._moe_batch:  # the layer's experts in one grouped launch pair
                     run = lambda _ins, _i=i: self._run_moe_batch(_i, stats)  # noqa: E731
@@ -799,9 +792,17 @@ class DAGExecutor:
                 torch.cuda.current_stream(self.device).wait_event(done)
         for w, _ in recv_work.values():
             w.wait()
-        for _, _, w in self._pending_sends:
+        for w in self._pending_sends.values():
             w.wait()
-        self._pending_sends = []
+        self._pending_sends = {}
+
+    def _wait_sends(self, ins) -> None:
+        """Complete the in-flight sends whose buffer ``ins`` is about to overwrite (planned
+        statically: Instr.wait_sends, program._plan_send_waits)."""
+        for j in ins.wait_sends:
+            w = self._pending_sends.pop(j, None)
+            if w is not None:
+                w.wait()
 
     def step(self, profile: bool = False) -> StepStats:
         """Execute the rank's program once (asynchronously on the GPU). ``profile=True`` runs

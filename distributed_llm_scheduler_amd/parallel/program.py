@@ -40,6 +40,9 @@ class Instr:
     kind: str = ""                  # run: fused kind (e.g. "linear+gelu")
     peer: int = -1                  # recv: source rank, send: destination rank
     param: Optional[str] = None     # load/evict
+    # run/recv: indices of earlier ``send`` instructions whose buffer this instruction's
+    # output region overlaps — they must complete before it writes (see _plan_send_waits)
+    wait_sends: Tuple[int, ...] = ()
 
 
 @dataclass
@@ -213,6 +216,12 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
         prog.param_arena_bytes = extent
         sinks = {t for t in order if not consumers.get(t)}
         _plan_activations(core, prog, tmap, sinks)
+        _plan_send_waits(prog)
+        if prog.failed_loads:
+            raise RuntimeError(
+                f"rank {rank}: parameter groups {sorted(set(prog.failed_loads))} do not fit the fragmented "
+                f"parameter arena ({caps.get(rank, 0)} B cap) even after evicting every group their task "
+                "does not need; raise the cap or use a policy that places fewer parameters on this rank")
         programs.append(prog)
     return programs
 
@@ -257,3 +266,24 @@ def _plan_activations(core, prog: Program, tmap: Dict[str, Task], sinks=frozense
             if tid in live:
                 act.release(live.pop(tid))
     prog.act_arena_bytes = extent  # slab size = highest byte any activation reaches
+
+
+def _plan_send_waits(prog: Program) -> None:
+    """A ``send`` reads its buffer asynchronously (RCCL stream of that peer pair) until the
+    receiver has taken it; the activation plan frees the buffer at the send, so a later
+    ``run`` OR ``recv`` (another peer pair, another RCCL stream) may be given the same
+    bytes. Every such writer gets the overlapping in-flight sends in ``wait_sends``; the
+    executor completes them before the write, and the validator checks the list and the
+    deadlock freedom of the waits (parallel/validate.py)."""
+    inflight: List[Tuple[int, int, int]] = []  # (send index, lo, hi)
+    for i, ins in enumerate(prog.instrs):
+        if ins.op == "send":
+            lo = prog.act_offset[ins.task]
+            inflight.append((i, lo, lo + prog.act_bytes[ins.task]))
+        elif ins.op in ("run", "recv") and inflight and ins.task in prog.act_offset:
+            lo = prog.act_offset[ins.task]
+            hi = lo + prog.act_bytes[ins.task]
+            hit = [s for s in inflight if s[1] < hi and lo < s[2]]
+            if hit:
+                ins.wait_sends = tuple(s[0] for s in hit)
+                inflight = [s for s in inflight if s not in hit]

@@ -12,9 +12,12 @@ ordering" of SURVEY §5 (race detection), run on the host before anything touche
   by order, there are no tags);
 * **deadlock freedom** — a simulation of all ranks with non-blocking sends and blocking
   receives (the executor's isend/irecv + wait-at-use) runs every program to completion;
+  a send the executor completes before reusing its buffer (``Instr.wait_sends``) blocks
+  its rank until the receiver has posted the matching recv (rendezvous);
 * **memory** — no two activations whose live ranges intersect share bytes of the
-  activation arena, no two resident parameter groups share bytes of the parameter arena,
-  and everything stays inside the arena sizes the executor allocates.
+  activation arena, no ``run`` or ``recv`` writes bytes an in-flight ``send`` still reads
+  unless it waits for that send first, no two resident parameter groups share bytes of
+  the parameter arena, and everything stays inside the arena sizes the executor allocates.
 """
 from __future__ import annotations
 
@@ -41,6 +44,7 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
         have = set()
         resident: Dict[str, Tuple[int, int]] = {}
         act_live: Dict[str, Tuple[int, int, int]] = {}  # tid -> (lo, hi, last use index)
+        inflight: Dict[int, Tuple[int, int]] = {}  # send index -> buffer region, until waited
         last_use: Dict[str, int] = {}
         for i, ins in enumerate(prog.instrs):
             if ins.op == "run":
@@ -75,6 +79,9 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
                 if ins.task not in have:
                     errs.append(f"{where}: sends a tensor not produced/received on this rank")
                 sends[(r, ins.peer)].append(ins.task)
+                if ins.task in prog.act_offset:
+                    lo = prog.act_offset[ins.task]
+                    inflight[i] = (lo, lo + prog.act_bytes[ins.task])
             elif ins.op == "run":
                 group = set(ins.group)
                 for tid in ins.group:
@@ -90,6 +97,12 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
             if ins.op in ("run", "recv") and ins.task in prog.act_offset:
                 lo = prog.act_offset[ins.task]
                 hi = lo + prog.act_bytes[ins.task]
+                for j in ins.wait_sends:
+                    inflight.pop(j, None)
+                for j, reg in inflight.items():
+                    if _overlap((lo, hi), reg):
+                        errs.append(f"{where}: writes the buffer of in-flight send {j} "
+                                    f"({prog.instrs[j].task}->gpu{prog.instrs[j].peer}) without waiting for it")
                 if hi > prog.act_arena_bytes:
                     errs.append(f"{where}: activation region [{lo},{hi}) exceeds the arena ({prog.act_arena_bytes} B)")
                 for other, (olo, ohi, oend) in act_live.items():
@@ -107,10 +120,12 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
 
 
 def _deadlock_check(programs: Sequence[Program]) -> List[str]:
-    """Run all programs: sends complete immediately into a per-pair FIFO, a recv blocks until
-    the matching message is at the head of its FIFO."""
+    """Run all programs: a send is posted into a per-pair FIFO without blocking, a recv
+    blocks until the matching message is at the head of its FIFO, and an instruction with
+    ``wait_sends`` blocks until each of those sends has been taken by its receiver."""
     pc = [0] * len(programs)
     fifo: Dict[Tuple[int, int], deque] = defaultdict(deque)
+    taken = set()  # (rank, send index) whose matching recv has been posted
     progress = True
     while progress:
         progress = False
@@ -118,15 +133,17 @@ def _deadlock_check(programs: Sequence[Program]) -> List[str]:
             r = prog.rank
             while pc[r] < len(prog.instrs):
                 ins = prog.instrs[pc[r]]
+                if any((r, j) not in taken for j in ins.wait_sends):
+                    break
                 if ins.op == "send":
-                    fifo[(r, ins.peer)].append(ins.task)
+                    fifo[(r, ins.peer)].append((ins.task, pc[r]))
                 elif ins.op == "recv":
                     q = fifo[(ins.peer, r)]
                     if not q:
                         break
-                    if q[0] != ins.task:
-                        return [f"rank {r}: recv {ins.task} from {ins.peer} but the next message is {q[0]}"]
-                    q.popleft()
+                    if q[0][0] != ins.task:
+                        return [f"rank {r}: recv {ins.task} from {ins.peer} but the next message is {q[0][0]}"]
+                    taken.add((ins.peer, q.popleft()[1]))
                 pc[r] += 1
                 progress = True
     stuck = [(p.rank, pc[p.rank]) for p in programs if pc[p.rank] < len(p.instrs)]

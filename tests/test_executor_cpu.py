@@ -67,18 +67,18 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, placement, scheduler, q):
+def _worker(rank, world, port, placement, scheduler, q, replicas=2, model="tiny-gpt2", seq=32):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        p = runtime.plan("tiny-gpt2", world=world, scheduler=scheduler, seq=32, batch=1, replicas=2,
+        p = runtime.plan(model, world=world, scheduler=scheduler, seq=seq, batch=1, replicas=replicas,
                          placement=placement)
         store = runtime.make_store(p)
         ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
         for _ in range(2):
             st = ex.step()
         res = {"rank": rank, "sends": st.sends, "recvs": st.recvs, "errs": []}
-        for rid in ("r0/", "r1/"):
+        for rid in (f"r{k}/" for k in range(replicas)):
             if p.placement.get(f"{rid}output_projection") == rank:
                 res["errs"].append(_ref_check(p, ex, store, rid))
         q.put(res)
@@ -106,6 +106,31 @@ def test_two_ranks_gloo(placement, scheduler):
         assert err < 0.02 * scale
     if placement == "pipeline":
         assert sum(r["sends"] for r in results) > 0 and sum(r["recvs"] for r in results) > 0
+
+
+def test_three_ranks_pipeline_reuses_sent_buffers():
+    """GPT-2 on 3 ranks, pipeline placement, 3 micro-batches: rank 1 receives
+    r1/layer_3_output into bytes of r0/layer_7_output that are still being sent to rank 2
+    (the plan's recv carries a wait for that send); every request's logits must match the
+    fp32 reference."""
+    world, replicas = 3, 3
+    p = runtime.plan("gpt2", world=world, seq=64, batch=1, replicas=replicas, placement="pipeline")
+    assert any(ins.op == "recv" and ins.wait_sends for pr in p.programs for ins in pr.instrs)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "pipeline", "EFT", q, replicas, "gpt2", 64))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    results = [q.get(timeout=5) for _ in range(world)]
+    errs = [e for r in results for e in r["errs"]]
+    assert len(errs) == replicas
+    for err, scale in errs:
+        assert err < 0.02 * scale
 
 
 @pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])

@@ -258,3 +258,29 @@ def test_paper_variants_on_llm_dags(name):
         s, sch = run(ALL_SCHEDULERS[name], tasks, nodes)
         assert len(s.completed_tasks) + len(s.failed_tasks) + len(s.orphaned_tasks) == len(tasks)
         assert len(s.completed_tasks) >= floor * len(tasks), (regime, len(s.completed_tasks))
+
+
+@pytest.mark.parametrize("seed", range(300))
+def test_eft_fractional_costs_never_strand_a_task(seed):
+    """Fuzz: with fractional parameter costs EFT's dry-run eviction and its
+    assignment must agree, so every task ends completed, failed, or behind a failed input —
+    never pending with all inputs done, and failed only when it cannot fit an empty node
+    (without the tolerance 6 of the first 31 seeds fail feasible tasks)."""
+    rng = random.Random(seed)
+    n_tasks, P = rng.randint(4, 30), rng.randint(3, 12)
+    tasks = []
+    for i in range(n_tasks):  # mostly chains over few shared parameters: heavy eviction churn
+        deps = [f"t{i - 1}"] if i and rng.random() < 0.7 else []
+        params = {f"p{rng.randrange(P)}" for _ in range(rng.randint(1, 2))}
+        tasks.append(Task(f"t{i}", rng.choice([0.0, 0.1, 0.2]), 0.1, deps, params))
+    pc = {f"p{k}": rng.choice([0.1, 0.15, 0.3, 0.7, 1.1]) for k in range(P)}
+    nodes = [Node(f"n{k}", rng.choice([1.0, 1.2, 1.5, 2.0, 2.5]), 1.0) for k in range(rng.choice([1, 2]))]
+    s, _ = run(EFTScheduler, tasks, nodes, param_cost=pc)
+    for t in tasks:
+        if t.id in s.failed_tasks:
+            # EFT may evict every cached group the task does not need: it fails only when
+            # the task cannot fit an empty node
+            need = t.memory_required + sum(pc[p] for p in t.params_needed)
+            assert all(need > n.total_memory + 1e-9 for n in nodes), f"{t.id} failed but fits (seed {seed})"
+        elif t.id not in s.completed_tasks:
+            assert any(d not in s.completed_tasks for d in t.dependencies), f"{t.id} stranded (seed {seed})"

@@ -15,6 +15,11 @@ CASES = [
     dict(model="tiny-gpt2", world=2, tp=2, placement="tensor", seq=16),
     dict(model="gpt2-medium", world=2, cap_gb=0.3),
     dict(model="tiny-mixtral", world=3, scheduler="MRU_spec", seq=16, cap_gb=0.0002),
+    # a sent buffer is later the target of a recv from another peer (rank 1
+    # receives r1/layer_3_output into r0/layer_7_output's bytes while that is being sent)
+    dict(model="gpt2", world=3, placement="pipeline", replicas=3, seq=64),
+    dict(model="gpt2", world=4, scheduler="MRU_spec", replicas=4, seq=64),
+    dict(model="gpt2", world=4, scheduler="EFT", replicas=4, seq=64),
 ]
 
 
@@ -89,3 +94,47 @@ def test_debug_executor_guards_and_validation():
     del bad.programs[0].instrs[i]
     with pytest.raises(RuntimeError, match="invalid plan"):
         runtime.make_executor(bad, 0, "cpu", debug=True)
+
+
+def test_recv_into_inflight_send_buffer_waits():
+    """The pipeline plan that reuses a sent buffer for a recv from another peer: the recv
+    carries a planned wait for that send, and dropping the wait is flagged."""
+    p = runtime.plan("gpt2", world=3, placement="pipeline", replicas=3, seq=64)
+    hits = [(pr.rank, i) for pr in p.programs for i, ins in enumerate(pr.instrs) if ins.op == "recv" and ins.wait_sends]
+    assert hits, "expected a recv that reuses an in-flight send buffer"
+    for pr in p.programs:
+        for ins in pr.instrs:
+            for j in ins.wait_sends:
+                assert pr.instrs[j].op == "send"
+    progs = copy.deepcopy(p.programs)
+    r, i = hits[0]
+    progs[r].instrs[i].wait_sends = ()
+    errs = validate_programs(p.tasks, progs, p.param_bytes)
+    assert any("in-flight send" in e for e in errs), errs
+
+
+def test_send_wait_deadlock_detected():
+    """A wait on a send whose receiver only posts the recv after receiving from the waiter
+    is a rendezvous deadlock."""
+    p = _plan2()
+    progs = copy.deepcopy(p.programs)
+    s = next(k for k, ins in enumerate(progs[0].instrs) if ins.op == "send")
+    # rank 0 waits for its send before even issuing it, so the receiver can never take it
+    first = next(k for k, ins in enumerate(progs[0].instrs) if ins.op == "run")
+    progs[0].instrs[first].wait_sends = (s,)
+    errs = validate_programs(p.tasks, progs, p.param_bytes)
+    assert any("deadlock" in e for e in errs), errs
+
+
+def test_fragmented_parameter_arena_fails_at_plan_time():
+    """A parameter group that cannot be placed in the arena raises while planning instead
+    of surfacing as a KeyError in the executor."""
+    from distributed_llm_scheduler_amd.core import native
+    from distributed_llm_scheduler_amd.core.task import Task
+    from distributed_llm_scheduler_amd.parallel.program import build_programs
+
+    if not native.available():
+        pytest.skip(native.error())
+    tasks = [Task("a", 0.0, 0.1, [], {"p1", "p2"})]
+    with pytest.raises(RuntimeError, match="do not fit"):
+        build_programs(tasks, {"a": 0}, ["a"], 1, {"p1": 600, "p2": 600}, {0: 1000})
