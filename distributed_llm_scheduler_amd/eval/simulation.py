@@ -8,7 +8,8 @@
   ``dag_makespan_sim`` (dependency-respecting replay of the same placement — the
   reference's makespan ignores dependencies), ``orphaned_tasks``,
   ``param_loads``, ``param_evictions``, ``rounds``, ``engine``, ``seed`` and, when the
-  sweep executes on GPUs, ``wall_makespan_ms``.
+  sweep executes a model DAG on the devices (eval/execute.py, ``simulation.py --execute``),
+  ``wall_makespan_ms``, ``hbm_peak_gb``, ``bytes_moved_p2p``, ``param_fill_bytes``, ``device``.
 * The 2x2 figure ``scheduler_performance.png`` and the three console summaries match the
   reference's panels and headings.
 * Reproducible: every random draw goes through one seeded ``random.Random``.
@@ -33,7 +34,7 @@ REF_COLUMNS = ["scheduler_name", "dag_type", "memory_regime", "total_tasks", "co
                "makespan", "avg_node_utilization", "param_cache_hits", "param_cache_misses", "load_balance_score",
                "execution_time", "completion_rate", "num_nodes"]
 EXTRA_COLUMNS = ["dag_makespan_sim", "orphaned_tasks", "param_loads", "param_evictions", "rounds", "engine", "seed",
-                 "wall_makespan_ms"]
+                 "wall_makespan_ms", "hbm_peak_gb", "bytes_moved_p2p", "param_fill_bytes", "device"]
 
 
 @dataclass
@@ -60,6 +61,12 @@ class TestResult:
     engine: str = ""
     seed: int = -1
     wall_makespan_ms: float = float("nan")
+    # executed sweeps only (eval/execute.py): largest rank's arenas, per-step p2p and
+    # parameter-refill bytes over all ranks, and the device the DAG ran on
+    hbm_peak_gb: float = float("nan")
+    bytes_moved_p2p: float = float("nan")
+    param_fill_bytes: float = float("nan")
+    device: str = ""
 
     __test__ = False  # not a pytest class
 

@@ -50,7 +50,8 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
          node_speeds: Optional[Sequence[float]] = None, link_bw_gbps: float = 153.0,
          placement: str = "scheduler", tp: int = 1, resume: Optional[str] = None, sp: int = 1) -> Plan:
     """Build the DAG of ``replicas`` requests of ``model``, place it on ``world`` GPUs with
-    ``scheduler`` under a per-GPU cap of ``cap_gb`` and lower it to per-rank programs.
+    ``scheduler`` under a per-GPU cap of ``cap_gb`` (one value, or one per GPU — the
+    reference's heterogeneous node splits) and lower it to per-rank programs.
 
     ``placement``:
       * ``"scheduler"`` — the policy decides (default),
@@ -68,6 +69,11 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     order per GPU and the LOAD/EVICT trace) is reused instead of re-running the policy; the
     DAG is rebuilt from the saved arguments, which must match this call's.
     """
+    caps_gb = [float(c) for c in cap_gb] if isinstance(cap_gb, (list, tuple)) else [float(cap_gb)] * world
+    if len(caps_gb) != world:
+        raise ValueError(f"{len(caps_gb)} per-GPU caps for world {world}")
+    if isinstance(cap_gb, (list, tuple)):
+        cap_gb = list(caps_gb)
     args = dict(model=model, world=world, scheduler=scheduler, cap_gb=cap_gb, replicas=replicas, batch=batch,
                 seq=seq, cost_model=cost_model, fuse=fuse, node_speeds=list(node_speeds) if node_speeds else None,
                 link_bw_gbps=link_bw_gbps, placement=placement, tp=tp)
@@ -76,7 +82,7 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     tasks, groups, cfg = registry.build(model, batch=batch, seq=seq, replicas=replicas, cost_model=cost_model, tp=tp,
                                         sp=sp)
     param_bytes = {pid: group_layout(g)[0] for pid, g in groups.items()}
-    nodes = [Node(f"gpu{r}", cap_gb, (node_speeds[r] if node_speeds else 1.0), device=r) for r in range(world)]
+    nodes = [Node(f"gpu{r}", caps_gb[r], (node_speeds[r] if node_speeds else 1.0), device=r) for r in range(world)]
     node_rank = {n.id: r for r, n in enumerate(nodes)}
     cls = get_scheduler(scheduler)
     kw = {}
@@ -97,7 +103,7 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         raise ValueError(f"unknown placement {placement!r}")
     place = {tid: node_rank[sched.tasks[tid].assigned_node] for tid in sched.completed_tasks}
     order = [item for _, act, _, item in sched.events if act == "RUN"]
-    caps = {r: int(cap_gb * 1e9) for r in range(world)}
+    caps = {r: int(caps_gb[r] * 1e9) for r in range(world)}
     programs = build_programs(tasks, place, order, world, param_bytes, caps, events=sched.events,
                               node_rank=node_rank, fuse=fuse)
     name = cls.name if placement == "scheduler" else placement
@@ -164,6 +170,8 @@ def replan(p: Plan, lost_ranks: Sequence[int], **overrides) -> Plan:
     a.update(world=len(keep))
     if a.get("node_speeds"):
         a["node_speeds"] = [a["node_speeds"][r] for r in keep]
+    if isinstance(a.get("cap_gb"), list):
+        a["cap_gb"] = [a["cap_gb"][r] for r in keep]
     a.update(overrides)
     return plan(**a)
 

@@ -7,6 +7,13 @@
 Sweeps 6 DAG families x {2,4,8} nodes x {100,90,80}% memory x runs x 4 policies and writes
 evaluation_results/raw_results.csv (the reference's 14 columns, extra columns appended)
 and evaluation_results/scheduler_performance.png, then prints the summary tables.
+
+    python simulation.py --execute [--model gpt2] [--steps 10]      # 1 GPU
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 simulation.py --execute   # N GPUs
+
+EXECUTES instead of simulating: every policy x regime places the model's DAG on the job's
+GPUs (the reference's node splits and memory formula) and runs it with the native executor;
+rows carry the measured ``wall_makespan_ms`` next to the reference columns.
 """
 import argparse
 import os
@@ -28,9 +35,42 @@ def main(argv=None):
     ap.add_argument("--schedulers", default=None,
                     help="comma-separated policy names (default DFS,Greedy,Critical,MRU_spec; also EFT, Greedy_chain, "
                          "MRU_paper)")
+    ap.add_argument("--execute", action="store_true", help="run the placed model DAG on this job's devices")
+    ap.add_argument("--model", default="gpt2", help="--execute: model DAG (gpt2, gpt2-medium, llama3-8b, ...)")
+    ap.add_argument("--steps", type=int, default=10, help="--execute: timed steps per configuration")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--cost-model", default="reference", choices=["reference", "bytes"])
+    ap.add_argument("--regimes", default="1.0,0.9,0.8")
+    ap.add_argument("--nodes", default="equal", choices=["equal", "reference", "laptops"],
+                    help="--execute: memory split over the devices (BASELINE.md 2.3 equal nodes, the sweep's "
+                         "heterogeneous split, or test_gpt2.py's 4 laptops)")
     a = ap.parse_args(argv)
+    if a.execute:
+        return _execute_main(a)
     return _main(num_runs=a.runs, seed=a.seed, out_dir=a.out, engine=a.engine,
                  schedulers=a.schedulers.split(",") if a.schedulers else None)
+
+
+def _execute_main(a):
+    import torch
+    import torch.distributed as dist
+
+    from distributed_llm_scheduler_amd.eval import execute
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    gpu = torch.cuda.is_available()
+    if gpu:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    if world > 1:
+        dist.init_process_group("nccl" if gpu else "gloo")
+    try:
+        return execute.main(a.model, a.schedulers.split(",") if a.schedulers else None,
+                            tuple(float(x) for x in a.regimes.split(",")), a.steps, a.warmup, a.seq,
+                            cost_model=a.cost_model, seed=a.seed, out_dir=a.out, nodes=a.nodes)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
 
 
 if __name__ == "__main__":
