@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--sp", type=int, default=1, help="sequence chunks per request (context-parallel DAG transform)")
     ap.add_argument("--init", default="auto", choices=["auto", "host", "device"],
                     help="weight init: device RNG straight into HBM, or host master copy (auto: device "
-                         "unless the program re-loads evicted groups, whose cost must be a real copy)")
+                         "unless the program re-fills groups in the steady state, whose cost must be a real copy)")
     ap.add_argument("--refine-tuning", action="store_true",
                     help="before timing, pick GEMM configs by whole-step hipGraph time (persists ops/gemm_tuning.json)")
     ap.add_argument("--no-graph", action="store_true")
@@ -88,8 +88,7 @@ def main():
                         placement=args.placement, tp=args.tp, sp=args.sp)
     log(f"[bench] rank {rank}: planned {plan.stats['tasks_completed']}/{plan.stats['tasks_total']} tasks in "
         f"{(time.time() - t0) * 1e3:.1f} ms; {plan.stats}")
-    loads = [i.param for i in plan.programs[rank].instrs if i.op == "load"]
-    dev_init = args.init == "device" or (args.init == "auto" and gpu and len(loads) == len(set(loads)))
+    dev_init = args.init == "device" or (args.init == "auto" and gpu and runtime.device_init_ok(plan, rank))
     store = runtime.make_store(plan, device_init=dev_init)
     t0 = time.time()
     ex = runtime.make_executor(plan, rank, device, store, pg=pg, use_graph=not args.no_graph, trace=args.roctx)

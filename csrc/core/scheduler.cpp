@@ -395,6 +395,18 @@ struct Sched {
     }
     std::vector<double> node_free(N, 0.0), copy_free(N, 0.0);
     std::vector<double> last_touch(P * static_cast<size_t>(std::max(N, 1)), -1.0);
+    // next-use model for the eviction order (plan_eviction)
+    eft_rank = rank;
+    eft_users.assign(P, {});
+    eft_first.assign(P, -std::numeric_limits<double>::infinity());
+    eft_rmax = 0.0;
+    for (int t = 0; t < T; ++t) {
+      eft_rmax = std::max(eft_rmax, rank[t]);
+      for (int p : I.params[t]) {
+        eft_users[p].push_back(t);
+        eft_first[p] = std::max(eft_first[p], rank[t]);
+      }
+    }
     R.start_time.assign(T, 0.0);
     R.finish_time.assign(T, 0.0);
     auto cmp = [&](int a, int b) {
@@ -473,8 +485,31 @@ struct Sched {
     R.rounds = step;
   }
 
-  // Dry-run eviction: least useful first = not needed by any ready task, then oldest
-  // last use, then name. Never evicts this task's own params.
+  // EFT next-use model: upward rank per task (tasks run in decreasing rank), the tasks
+  // using each parameter and the highest rank among them (its first use in a repetition).
+  std::vector<double> eft_rank;
+  std::vector<std::vector<int>> eft_users;
+  std::vector<double> eft_first;
+  double eft_rmax = 0.0;
+
+  // Rank distance from task t to parameter p's next use: a pending user later in this
+  // repetition, else (cyclic) p's first use in the next repetition of the DAG.
+  double next_use_distance(int t, int p) const {
+    const double now = eft_rank[t];
+    double best = -std::numeric_limits<double>::infinity();
+    for (int u : eft_users[p])
+      if (pending[u] && u != t) best = std::max(best, eft_rank[u]);
+    if (best > -std::numeric_limits<double>::infinity()) return std::max(0.0, now - best);
+    return now + (eft_rmax - eft_first[p]) + 1e-12;
+  }
+
+  // Dry-run eviction. Never evicts this task's own params. Order:
+  // * cyclic (default): farthest next use first (Belady's rule under a repeating DAG): for a
+  //   layer chain served step after step this keeps the FIRST layers' weights resident across
+  //   the step boundary, so only the overflow is re-filled per step — least-recently-used
+  //   order evicts every group before its next use and re-fills all of them;
+  // * otherwise least useful first = not needed by any ready task, then oldest last use.
+  // Ties: parameter name.
   bool plan_eviction(int t, int n, double shortage, const std::vector<double>& last_touch,
                      std::vector<int>& victims) const {
     std::vector<char> needed(P, 0);
@@ -482,14 +517,23 @@ struct Sched {
     std::vector<int> cand;
     for (int p : cached_list[n])
       if (!needed[p]) cand.push_back(p);
-    std::sort(cand.begin(), cand.end(), [&](int a, int b) {
-      const bool ra = ready_need[a] > 0, rb = ready_need[b] > 0;
-      if (ra != rb) return rb;  // not-needed-now first
-      const double la = last_touch[static_cast<size_t>(n) * P + a];
-      const double lb = last_touch[static_cast<size_t>(n) * P + b];
-      if (la != lb) return la < lb;
-      return name_rank[a] < name_rank[b];
-    });
+    if (I.cyclic) {
+      std::vector<double> dist(P, 0.0);
+      for (int p : cand) dist[p] = next_use_distance(t, p);
+      std::sort(cand.begin(), cand.end(), [&](int a, int b) {
+        if (dist[a] != dist[b]) return dist[a] > dist[b];
+        return name_rank[a] < name_rank[b];
+      });
+    } else {
+      std::sort(cand.begin(), cand.end(), [&](int a, int b) {
+        const bool ra = ready_need[a] > 0, rb = ready_need[b] > 0;
+        if (ra != rb) return rb;  // not-needed-now first
+        const double la = last_touch[static_cast<size_t>(n) * P + a];
+        const double lb = last_touch[static_cast<size_t>(n) * P + b];
+        if (la != lb) return la < lb;
+        return name_rank[a] < name_rank[b];
+      });
+    }
     double freed = 0;
     for (int p : cand) {
       if (freed >= shortage - kEftTol) break;

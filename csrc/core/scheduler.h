@@ -53,6 +53,9 @@ struct Instance {
   double link_bw = 153.0;        // GB/s per xGMI link
   double link_lat = 5e-6;        // s per point-to-point message
   double load_bw = 50.0;         // GB/s for a parameter cache fill (H2D)
+  // EFT eviction: true = the DAG repeats (one DAG per serving step; farthest next use,
+  // counting the next repetition), false = least recently used among those no ready task needs
+  bool cyclic = true;
 };
 
 struct NodeResult {

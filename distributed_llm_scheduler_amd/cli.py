@@ -90,7 +90,7 @@ def cmd_run(a) -> int:
                                 **({"device_id": dev} if gpu else {}))
         pg = dist.group.WORLD
     p = _plan(a, world, resume=a.resume)
-    store = runtime.make_store(p, seed=a.seed, device_init=gpu and a.init == "device")
+    store = runtime.make_store(p, seed=a.seed, device_init=gpu and a.init == "device" and runtime.device_init_ok(p, rank))
     ex = runtime.make_executor(p, rank, dev, store, pg=pg, use_graph=gpu and not a.no_graph, trace=a.roctx)
 
     def sync():

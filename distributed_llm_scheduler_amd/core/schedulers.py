@@ -504,8 +504,12 @@ class EFTScheduler(BaseScheduler):
     Priority = upward rank (compute + expected xGMI transfer to successors). Each ready
     task goes to the node minimising its finish time given the node's timeline, input
     arrivals (cross-GPU edges pay ``link_latency_s + bytes/link_bw``), parameter-cache
-    fills on the node's copy engine (overlapped with compute) and the per-node memory cap
-    (least-useful-first eviction: not needed by a ready task, then oldest use). Sets
+    fills on the node's copy engine (overlapped with compute) and the per-node memory cap.
+    Eviction (``cyclic=True``, default): farthest next use first, counting the DAG's next
+    repetition — the executor replays the plan every serving step, and for a layer chain
+    under a cap this keeps the first layers resident across the step boundary so only the
+    overflow is re-filled per step (least-recently-used order re-fills everything).
+    ``cyclic=False``: least useful first (not needed by a ready task, then oldest use). Sets
     ``start_time`` / ``finish_time`` per task (the planned, dependency-respecting timeline).
     """
 
@@ -513,8 +517,9 @@ class EFTScheduler(BaseScheduler):
     name = "EFT"
 
     def __init__(self, nodes, *, link_bw_gbps: float = 153.0, link_latency_s: float = 5e-6,
-                 load_bw_gbps: float = 50.0, **kw):
+                 load_bw_gbps: float = 50.0, cyclic: bool = True, **kw):
         super().__init__(nodes, **kw)
+        self.cyclic = cyclic
         self.link_bw_gbps = link_bw_gbps
         self.link_latency_s = link_latency_s
         self.load_bw_gbps = load_bw_gbps
@@ -525,6 +530,7 @@ class EFTScheduler(BaseScheduler):
         inst.link_bw = float(self.link_bw_gbps)
         inst.link_lat = float(self.link_latency_s)
         inst.load_bw = float(self.load_bw_gbps)
+        inst.cyclic = bool(self.cyclic)
 
     def _after_native(self, res, ids, pnames):
         self.start_time = {ids[i]: s for i, s in enumerate(res.start_time) if res.completed[i]}

@@ -131,10 +131,9 @@ def _execute(p, rank, device, pg, steps, warmup, use_graph, gpu):
     parameter-fill bytes per steady-state step summed over ranks)."""
     from ..parallel import runtime
 
-    loads = [i.param for i in p.programs[rank].instrs if i.op == "load"]
-    # device RNG init straight into HBM, unless the program re-loads evicted groups: then
-    # every refill must be a real host->HBM copy
-    store = runtime.make_store(p, device_init=gpu and len(loads) == len(set(loads)))
+    # device RNG init straight into HBM, unless the program re-fills groups in the steady
+    # state: then every refill must be a real host->HBM copy
+    store = runtime.make_store(p, device_init=gpu and runtime.device_init_ok(p, rank))
     ex = runtime.make_executor(p, rank, device, store, pg=pg, use_graph=use_graph)
     stats = None
     for _ in range(max(warmup, 2)):

@@ -159,6 +159,12 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             ins.append(Instr("evict", param=pid))
             par.release(where.pop(pid))
 
+        # parameters of fused-away members whose group has not run yet: the group reads them
+        # at its tail's position, so an eviction the policy decided in between is deferred
+        # until the group has run (cancelled if the policy loads the group again first)
+        pinned: Dict[str, int] = defaultdict(int)
+        deferred: List[str] = []
+
         def load(pid, needed):
             nonlocal extent
             nbytes = int(param_bytes.get(pid, 0)) or 1
@@ -166,7 +172,8 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             while off < 0:
                 # fragmentation (the scheduler accounts bytes, not contiguity): evict the
                 # least recently used resident group this task does not need, retry
-                victims = sorted((q for q in where if q not in needed), key=lambda q: last_use.get(q, -1))
+                victims = sorted((q for q in where if q not in needed and not pinned.get(q)),
+                                 key=lambda q: last_use.get(q, -1))
                 if not victims:
                     prog.failed_loads.append(pid)
                     return
@@ -187,14 +194,23 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 if events is not None:  # replay the policy's cache decisions
                     for op, pid in load_before.get(tid, []):
                         if op == "evict" and pid in where and pid not in needed:
-                            evict(pid)
-                        elif op == "load" and pid not in where:
-                            load(pid, needed)
+                            if pinned.get(pid):
+                                if pid not in deferred:
+                                    deferred.append(pid)
+                            else:
+                                evict(pid)
+                        elif op == "load":
+                            if pid in deferred:
+                                deferred.remove(pid)  # still resident: the reload is free
+                            elif pid not in where:
+                                load(pid, needed | {q for q, c in pinned.items() if c})
                 for pid in sorted(needed):
                     if pid not in where:
-                        load(pid, needed)
+                        load(pid, needed | {q for q, c in pinned.items() if c})
                     last_use[pid] = len(ins)
                 if tid in fused_into:
+                    for pid in needed:
+                        pinned[pid] += 1
                     continue  # executed as part of its consumer's group
                 grp = tuple(group_of.get(tid, [tid]))
                 if grp in emitted_group:
@@ -203,6 +219,13 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 kind = _group_kind(tmap, grp)
                 ins.append(Instr("run", task=grp[-1], group=grp, kind=kind))
                 prog.n_kernels += 1
+                for member in grp[:-1]:
+                    for pid in tmap[member].params_needed:
+                        pinned[pid] -= 1
+                for pid in [q for q in deferred if not pinned.get(q)]:
+                    deferred.remove(pid)
+                    if pid in where:
+                        evict(pid)
                 dsts = sorted({placement[c] for c in consumers.get(grp[-1], []) if placement[c] != rank})
                 for dst in dsts:
                     ins.append(Instr("send", task=grp[-1], peer=dst))
@@ -287,3 +310,26 @@ def _plan_send_waits(prog: Program) -> None:
             if hit:
                 ins.wait_sends = tuple(s[0] for s in hit)
                 inflight = [s for s in inflight if s not in hit]
+
+
+def steady_fill_bytes(prog: Program, param_bytes: Dict[str, int], steps: int = 2) -> int:
+    """Parameter bytes the executor copies in the ``steps``-th repetition of the program:
+    a ``load`` costs nothing when its arena region still holds the group from before
+    (the executor's steady-state residency, DAGExecutor._fill), else one DMA of the group."""
+    valid: List[Tuple[int, int, str]] = []
+    filled = 0
+    for _ in range(steps):
+        filled = 0
+        for i, ins in enumerate(prog.instrs):
+            if ins.op != "load":
+                continue
+            off = prog.param_offset.get((i, ins.param))
+            if off is None:
+                continue
+            size = int(param_bytes.get(ins.param, 0)) or 1
+            if (off, size, ins.param) in valid:
+                continue
+            valid = [r for r in valid if r[0] + r[1] <= off or off + size <= r[0]]
+            valid.append((off, size, ins.param))
+            filled += size
+    return filled

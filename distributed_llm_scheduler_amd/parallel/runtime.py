@@ -14,7 +14,7 @@ from ..core import Node, get_scheduler
 from ..core.task import Task
 from ..models import registry
 from ..models.params import ParamStore, group_layout
-from .program import Program, build_programs
+from .program import Program, build_programs, steady_fill_bytes
 
 
 @dataclass
@@ -229,12 +229,21 @@ def plan_stats(p: Plan) -> Dict:
         "kernels_per_rank": [pr.n_kernels for pr in p.programs],
         "param_peak_gb_per_rank": [pr.param_peak_bytes / 1e9 for pr in p.programs],
         "act_arena_gb_per_rank": [pr.act_arena_bytes / 1e9 for pr in p.programs],
+        # parameter bytes re-filled per steady-state step (evict/reload traffic of the plan)
+        "refill_gb_per_step_per_rank": [steady_fill_bytes(pr, p.param_bytes) / 1e9 for pr in p.programs],
         "tasks_per_rank": [sum(1 for r in p.placement.values() if r == k) for k in range(p.world)],
     }
 
 
 def make_store(p: Plan, seed: int = 0, device_init: bool = False) -> ParamStore:
     return ParamStore(p.groups, seed=seed, device_init=device_init)
+
+
+def device_init_ok(p: Plan, rank: int) -> bool:
+    """Can rank's weights be random-initialised straight into HBM? Only when its program
+    re-fills nothing in the steady state: every refill of an evicted/overwritten group must
+    be a real host->HBM copy (a measured cost, and capturable in a hipGraph)."""
+    return steady_fill_bytes(p.programs[rank], p.param_bytes) == 0
 
 
 def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None, pg=None, use_graph: bool = True,

@@ -44,6 +44,23 @@ def test_fusion_reduces_kernels():
     assert kinds[:4] == ["embedding", "layernorm+attention+residual", "layernorm+linear+gelu", "linear+residual"]
 
 
+@pytest.mark.parametrize("sched", ["EFT", "MRU_spec"])
+def test_capped_plan_steady_state_matches_reference(sched):
+    """Under a cap that forces evictions (and, for cyclic EFT, deferred evictions of fused
+    norms' weights), repeated steps stay correct and re-fill exactly the planned bytes."""
+    from distributed_llm_scheduler_amd.parallel.program import steady_fill_bytes
+
+    p = runtime.plan("tiny-gpt2", world=1, scheduler=sched, seq=16, cap_gb=0.00012)
+    assert p.completed == p.total and p.programs[0].counts().get("evict", 0) > 0
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, "cpu", store, debug=True)
+    for _ in range(3):
+        st = ex.step()
+    assert st.bytes_filled == steady_fill_bytes(p.programs[0], p.param_bytes)
+    err, scale = _ref_check(p, ex, store)
+    assert err < 0.02 * scale
+
+
 def test_memory_cap_enforced_by_scheduler():
     p = runtime.plan("tiny-gpt2", world=1, scheduler="DFS", seq=16, cap_gb=0.00005)
     assert p.completed < p.total

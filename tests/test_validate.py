@@ -20,6 +20,12 @@ CASES = [
     dict(model="gpt2", world=3, placement="pipeline", replicas=3, seq=64),
     dict(model="gpt2", world=4, scheduler="MRU_spec", replicas=4, seq=64),
     dict(model="gpt2", world=4, scheduler="EFT", replicas=4, seq=64),
+    # memory pressure + fusion: the policy evicts a fused-away norm's weights before its
+    # group runs (cyclic EFT evicts just-used groups first) -> the eviction is deferred
+    dict(model="gpt2", world=1, scheduler="EFT", cost_model="reference", cap_gb=38.8094 * 0.9),
+    dict(model="gpt2", world=1, scheduler="EFT", cost_model="reference", cap_gb=38.8094 * 0.6),
+    dict(model="gpt2", world=1, scheduler="EFT", cost_model="bytes", cap_gb=0.2),
+    dict(model="llama3-8b", world=2, scheduler="EFT", cost_model="bytes", cap_gb=9.0),
 ]
 
 
