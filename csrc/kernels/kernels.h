@@ -133,3 +133,7 @@ void launch_grouped_gemm(const void* X, const int32_t* offsets, const void* W, v
 void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t* idx, const int32_t* slot_of,
                                const int32_t* off, const float* w, const void* r, void* y, int M, int topk, int H,
                                int E, hipStream_t s);
+
+// dst (HBM) <- src (pinned host memory, device-accessible address); bytes % 16 == 0, both
+// 16-byte aligned; at most `blocks` workgroups of 256 lanes pull over the host link
+void launch_host_pull(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t s);

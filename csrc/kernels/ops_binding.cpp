@@ -478,8 +478,25 @@ at::Tensor moe_gather_combine(const std::vector<at::Tensor>& experts, const at::
 
 }  // namespace
 
+// dst[:src.numel()] <- src: a pinned host uint8 tensor pulled into a GPU uint8 tensor by a kernel
+void host_pull(const at::Tensor& dst, const at::Tensor& src, int64_t blocks) {
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous() && dst.scalar_type() == at::kByte, "dst: contiguous GPU uint8");
+  TORCH_CHECK(!src.is_cuda() && src.is_pinned() && src.is_contiguous() && src.scalar_type() == at::kByte,
+              "src: contiguous pinned host uint8");
+  const int64_t n = src.numel();
+  TORCH_CHECK(dst.numel() >= n && n % 16 == 0, "sizes: dst >= src, multiple of 16 bytes");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0,
+              "16-byte alignment");
+  TORCH_CHECK(blocks >= 1 && blocks <= 4096, "blocks");
+  void* dev_src = nullptr;
+  TORCH_CHECK(hipHostGetDevicePointer(&dev_src, src.data_ptr(), 0) == hipSuccess && dev_src != nullptr,
+              "pinned host image is not mapped into the GPU address space");
+  launch_host_pull(dev_src, dst.data_ptr(), n, (int)blocks, cur_stream());
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Hand-written HIP/CDNA4 (gfx950) kernels for distributed_llm_scheduler_amd";
+  m.def("host_pull", &host_pull, py::arg("dst"), py::arg("src"), py::arg("blocks") = 256);
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),
         py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1,
         py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5,

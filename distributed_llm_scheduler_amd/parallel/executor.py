@@ -75,6 +75,11 @@ STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
 PREFETCH = os.environ.get("DLS_PREFETCH", "0") == "1"
 # one grouped launch pair per MoE layer for the experts co-located on this rank (GPU)
 MOE_BATCH = os.environ.get("DLS_MOE_BATCH", "1") != "0"
+# parameter refills: "pull" = the host-pull kernel reads the pinned group image over the host
+# link (benchmarks/bench_h2d.py: 50-56 GB/s from 2.4 MB up, 32 GB/s at 0.25 MB, on 32-64
+# workgroups), "dma" = hipMemcpyAsync (42-51 GB/s, 15 GB/s at 0.25 MB)
+REFILL = os.environ.get("DLS_REFILL", "pull")
+REFILL_BLOCKS = int(os.environ.get("DLS_REFILL_BLOCKS", "64"))
 
 
 
@@ -100,6 +105,13 @@ class DAGExecutor:
         self._params: Dict[str, Dict[str, torch.Tensor]] = {}  # pid -> {tensor name -> view}
         self._wflat: Dict[str, torch.Tensor] = {}               # tensor name -> resident view
         self._derived_cache: Dict[tuple, tuple] = {}             # (weight, ptr) -> (colsum, bias') for folded norms
+        # GPU, host-image refills: a transformed weight's bytes are written back into a private
+        # copy of its group's pinned image, so every later refill restores the TRANSFORMED
+        # weight and its (colsum, bias') stay valid wherever the group lands (no re-derivation
+        # kernels per refill)
+        self._img_override: Dict[str, torch.Tensor] = {}         # pid -> pinned image
+        self._derived_named: Dict[str, tuple] = {}                # weight -> (colsum, bias')
+        self._tensor_home: Dict[str, Tuple[str, int]] = {}        # weight -> (pid, byte offset in group)
         self._valid: List[Tuple[int, int, str]] = []  # param arena regions holding data
         self._inputs: Dict[str, torch.Tensor] = {}
         self._scratch_bufs: Dict[str, torch.Tensor] = {}
@@ -394,9 +406,14 @@ class DAGExecutor:
             return False  # region still holds this group (steady-state residency)
         self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
         for spec, _ in layout:  # these weights are original again: drop stale folded-norm state
-            self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
-        img = self.store.group_image(pid) if self.gpu else None
-        if img is not None:  # one DMA of the whole group image
+            if spec.name not in self._derived_named:
+                self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
+        img = self._img_override.get(pid)
+        if img is None and self.gpu:
+            img = self.store.group_image(pid)
+        if img is not None and REFILL == "pull" and img.is_pinned():
+            ops.ext().host_pull(self.param_slab[off:off + total], img, REFILL_BLOCKS)
+        elif img is not None:  # one DMA of the whole group image
             self.param_slab[off:off + total].copy_(img, non_blocking=True)
         else:
             for spec, _ in layout:
@@ -468,6 +485,9 @@ class DAGExecutor:
         (``rope_perm = (n_q_heads, n_k_heads, head_dim)``). W is read by this fused group only,
         so overwriting it is safe."""
         W = self._w(w_name)
+        named = self._derived_named.get(w_name)
+        if named is not None:  # the arena holds the transformed weight (refilled from its image)
+            return W, named[0], named[1]
         key = (w_name, W.data_ptr())
         d = self._derived_cache.get(key)
         if d is None:
@@ -493,7 +513,30 @@ class DAGExecutor:
                 W.copy_(wd)
             d = (cs, bias)
             self._derived_cache[key] = d
+            if wd is not W:
+                self._persist_transform(w_name, W, d)
         return W, d[0], d[1]
+
+    def _persist_transform(self, w_name: str, W: torch.Tensor, d: tuple) -> None:
+        """Write the transformed weight into a private copy of its group's pinned host image
+        (GPU stores with host images only; once, in an eager step)."""
+        if not self.gpu or torch.cuda.is_current_stream_capturing():
+            return
+        if not self._tensor_home:
+            for gid, grp in self.store.groups.items():
+                for spec, sub in group_layout(grp)[1]:
+                    self._tensor_home[spec.name] = (gid, sub)
+        pid, sub = self._tensor_home[w_name]
+        img = self._img_override.get(pid)
+        if img is None:
+            base = self.store.group_image(pid)
+            if base is None or not base.is_pinned():
+                return  # device-initialised store: nothing is ever re-filled from the host
+            img = base.clone().pin_memory()
+            self._img_override[pid] = img
+        nb = W.numel() * W.element_size()
+        img[sub:sub + nb].copy_(W.reshape(-1).view(torch.uint8))  # blocking D2H
+        self._derived_named[w_name] = d
 
     def _gemm(self, x, w_name, b_name, norm: Optional[Task], act=None, residual=None, out=None, rope=None,
               rope_perm=None, stats_out=None):

@@ -419,3 +419,16 @@ def test_gemm_folded_norm_external_stats(mode, config, splitk, act):
                        None, False, None, None, 1, 2, 0, None, st)
     torch.cuda.synchronize()
     _close(y.cpu(), ref, 3e-2)
+
+
+@pytest.mark.parametrize("nbytes,blocks", [(256, 1), (6144, 64), (1 << 20, 128), ((9 << 20) + 4096, 512)])
+def test_host_pull_copies_exact_bytes(nbytes, blocks):
+    """Parameter refill by the host-pull kernel: pinned host image -> HBM, bit-exact, and
+    nothing past the destination prefix is written."""
+    g = torch.Generator().manual_seed(nbytes)
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, generator=g).pin_memory()
+    dst = torch.full((nbytes + 4096,), 0xA5, dtype=torch.uint8, device=DEV)
+    ops.ext().host_pull(dst, src, blocks)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:nbytes].cpu(), src)
+    assert bool((dst[nbytes:] == 0xA5).all())
