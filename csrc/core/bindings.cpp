@@ -26,7 +26,8 @@ PYBIND11_MODULE(_dlsched_core, m) {
       .def_readwrite("link_bw", &dls::Instance::link_bw)
       .def_readwrite("link_lat", &dls::Instance::link_lat)
       .def_readwrite("load_bw", &dls::Instance::load_bw)
-      .def_readwrite("cyclic", &dls::Instance::cyclic);
+      .def_readwrite("cyclic", &dls::Instance::cyclic)
+      .def_readwrite("param_refill", &dls::Instance::param_refill);
 
   py::class_<dls::NodeResult>(m, "NodeResult")
       .def_readonly("available_memory", &dls::NodeResult::available_memory)

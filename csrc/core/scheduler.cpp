@@ -504,10 +504,11 @@ struct Sched {
   }
 
   // Dry-run eviction. Never evicts this task's own params. Order:
-  // * cyclic (default): farthest next use first (Belady's rule under a repeating DAG): for a
-  //   layer chain served step after step this keeps the FIRST layers' weights resident across
-  //   the step boundary, so only the overflow is re-filled per step — least-recently-used
-  //   order evicts every group before its next use and re-fills all of them;
+  // * cyclic (default): cheapest refill per unit of budget freed first (param_refill), then
+  //   farthest next use (Belady's rule under a repeating DAG): for a layer chain served step
+  //   after step this keeps the FIRST layers' weights resident across the step boundary, so
+  //   only the overflow is re-filled per step — least-recently-used order evicts every group
+  //   before its next use and re-fills all of them;
   // * otherwise least useful first = not needed by any ready task, then oldest last use.
   // Ties: parameter name.
   bool plan_eviction(int t, int n, double shortage, const std::vector<double>& last_touch,
@@ -518,9 +519,17 @@ struct Sched {
     for (int p : cached_list[n])
       if (!needed[p]) cand.push_back(p);
     if (I.cyclic) {
-      std::vector<double> dist(P, 0.0);
-      for (int p : cand) dist[p] = next_use_distance(t, p);
+      // refill bytes per unit of budget freed: 1 when the budget counts real bytes; under
+      // the reference's flat cost a 6 KB norm frees as much budget as a 77 MB embedding,
+      // so the cheap-to-refill groups are streamed and the expensive ones stay resident
+      std::vector<double> dist(P, 0.0), ratio(P, 1.0);
+      const bool weighted = I.param_refill.size() == static_cast<size_t>(P);
+      for (int p : cand) {
+        dist[p] = next_use_distance(t, p);
+        if (weighted && I.param_cost[p] > 0) ratio[p] = I.param_refill[p] / I.param_cost[p];
+      }
       std::sort(cand.begin(), cand.end(), [&](int a, int b) {
+        if (std::fabs(ratio[a] - ratio[b]) > 1e-6 * std::max(ratio[a], ratio[b])) return ratio[a] < ratio[b];
         if (dist[a] != dist[b]) return dist[a] > dist[b];
         return name_rank[a] < name_rank[b];
       });

@@ -56,6 +56,9 @@ struct Instance {
   // EFT eviction: true = the DAG repeats (one DAG per serving step; farthest next use,
   // counting the next repetition), false = least recently used among those no ready task needs
   bool cyclic = true;
+  // Optional: bytes (GB) a refill of each parameter really moves, when the budget cost
+  // model differs (the reference's flat 0.5 GB per parameter). Empty = param_cost.
+  std::vector<double> param_refill;
 };
 
 struct NodeResult {

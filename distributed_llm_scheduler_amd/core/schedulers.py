@@ -509,6 +509,9 @@ class EFTScheduler(BaseScheduler):
     repetition — the executor replays the plan every serving step, and for a layer chain
     under a cap this keeps the first layers resident across the step boundary so only the
     overflow is re-filled per step (least-recently-used order re-fills everything).
+    ``refill_gb`` (pid -> GB a refill really moves, when the budget cost model differs, e.g.
+    the reference's 0.5 GB per parameter): among eviction candidates the cheapest refill per
+    unit of budget freed goes first, so under a flat cost the big groups stay resident.
     ``cyclic=False``: least useful first (not needed by a ready task, then oldest use). Sets
     ``start_time`` / ``finish_time`` per task (the planned, dependency-respecting timeline).
     """
@@ -517,9 +520,11 @@ class EFTScheduler(BaseScheduler):
     name = "EFT"
 
     def __init__(self, nodes, *, link_bw_gbps: float = 153.0, link_latency_s: float = 5e-6,
-                 load_bw_gbps: float = 50.0, cyclic: bool = True, **kw):
+                 load_bw_gbps: float = 50.0, cyclic: bool = True, refill_gb: Optional[Dict[str, float]] = None,
+                 **kw):
         super().__init__(nodes, **kw)
         self.cyclic = cyclic
+        self.refill_gb = refill_gb
         self.link_bw_gbps = link_bw_gbps
         self.link_latency_s = link_latency_s
         self.load_bw_gbps = load_bw_gbps
@@ -531,6 +536,8 @@ class EFTScheduler(BaseScheduler):
         inst.link_lat = float(self.link_latency_s)
         inst.load_bw = float(self.load_bw_gbps)
         inst.cyclic = bool(self.cyclic)
+        if self.refill_gb is not None:
+            inst.param_refill = [float(self.refill_gb.get(p, self.param_size(p))) for p in inst.param_names]
 
     def _after_native(self, res, ids, pnames):
         self.start_time = {ids[i]: s for i, s in enumerate(res.start_time) if res.completed[i]}

@@ -90,6 +90,7 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         kw["param_cost"] = {pid: b / 1e9 for pid, b in param_bytes.items()}
     if cls.__name__ == "EFTScheduler":
         kw["link_bw_gbps"] = link_bw_gbps
+        kw["refill_gb"] = {pid: b / 1e9 for pid, b in param_bytes.items()}  # what a refill really moves
     sched = cls([n.fresh() for n in nodes], **kw)
     for t in tasks:
         sched.add_task(t.clone())
