@@ -7,7 +7,8 @@ Commands (defaults reproduce the reference's settings where one exists, SURVEY Â
   run       execute a plan on this machine: one process per GPU under torchrun
             (RANK/WORLD_SIZE from the environment), or one CPU/GPU process; prints the
             measured step makespan; ``--trace`` writes a Chrome trace, ``--gantt`` a PNG
-  simulate  the reference evaluation sweep (raw_results.csv + 2x2 figure)
+  simulate  the reference evaluation sweep (raw_results.csv + 2x2 figure); --execute runs each
+            policy's placement of a model DAG on the devices (measured makespan column)
   extract   the reference GPT-2 DAG (test_gpt2.py semantics) to JSON (test_gpt2.py also pickles it)
   elastic   run with device-loss injection: a worker dies, the DAG is re-planned onto the
             surviving devices and the step is re-executed
@@ -141,6 +142,26 @@ def cmd_run(a) -> int:
 
 
 def cmd_simulate(a) -> int:
+    if a.execute:  # same policies and regimes, the model DAG RUN on this job's devices
+        import torch
+        import torch.distributed as dist
+
+        from .eval import execute
+
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        gpu = torch.cuda.is_available()
+        if gpu:
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        if world > 1:
+            dist.init_process_group("nccl" if gpu else "gloo")
+        try:
+            execute.main(a.model, a.schedulers.split(",") if a.schedulers else None,
+                         tuple(float(x) for x in a.regimes.split(",")), a.steps, a.warmup, a.seq,
+                         cost_model=a.cost_model, seed=a.seed, out_dir=a.out, nodes=a.nodes)
+        finally:
+            if world > 1:
+                dist.destroy_process_group()
+        return 0
     from .eval.simulation import main as sim_main
 
     sim_main(num_runs=a.runs, seed=a.seed, out_dir=a.out, engine=a.engine,
@@ -208,6 +229,15 @@ def main(argv: Optional[List[str]] = None) -> int:
     s.add_argument("--out", default="evaluation_results")
     s.add_argument("--engine", choices=["native", "python"], default=None)
     s.add_argument("--schedulers", default=None)
+    s.add_argument("--execute", action="store_true",
+                   help="run each policy's placement of --model on this job's devices (measured makespan column)")
+    s.add_argument("--model", default="gpt2")
+    s.add_argument("--steps", type=int, default=10)
+    s.add_argument("--warmup", type=int, default=3)
+    s.add_argument("--seq", type=int, default=512)
+    s.add_argument("--cost-model", choices=["bytes", "reference"], default="reference")
+    s.add_argument("--regimes", default="1.0,0.9,0.8")
+    s.add_argument("--nodes", choices=["equal", "reference", "laptops"], default="equal")
     s.set_defaults(fn=cmd_simulate)
     e = sub.add_parser("extract", help="reference GPT-2 DAG to JSON")
     e.add_argument("--model", default="gpt2")

@@ -30,3 +30,14 @@ def test_cli_extract_and_models(tmp_path, capsys):
     assert len(json.load(open(path))["tasks"]) == 99
     assert cli.main(["models"]) == 0
     assert "llama3-8b" in capsys.readouterr().out
+
+
+def test_cli_simulate_execute(tmp_path, capsys):
+    out = str(tmp_path / "ev")
+    assert cli.main(["simulate", "--execute", "--model", "tiny-llama", "--seq", "16", "--steps", "1", "--warmup", "1",
+                     "--regimes", "1.0,0.8", "--schedulers", "DFS,EFT", "--out", out]) == 0
+    import pandas as pd
+    df = pd.read_csv(f"{out}/raw_results.csv")
+    assert len(df) == 4 and (df["wall_makespan_ms"] > 0).all()
+    eft = df[(df.scheduler_name == "EFT") & (df.memory_regime == 0.8)].iloc[0]
+    assert eft.completed_tasks == eft.total_tasks
