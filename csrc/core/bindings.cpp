@@ -85,6 +85,7 @@ PYBIND11_MODULE(_dlsched_core, m) {
   py::class_<dls::Arena>(m, "Arena")
       .def(py::init<uint64_t, uint64_t>(), py::arg("capacity"), py::arg("align") = 256)
       .def("alloc", &dls::Arena::alloc)
+      .def("reserve", &dls::Arena::reserve)
       .def("release", &dls::Arena::release)
       .def_property_readonly("capacity", &dls::Arena::capacity)
       .def_property_readonly("used", &dls::Arena::used)

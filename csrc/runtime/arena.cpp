@@ -40,6 +40,25 @@ int64_t Arena::alloc(uint64_t bytes) {
   return static_cast<int64_t>(off);
 }
 
+bool Arena::reserve(uint64_t off, uint64_t bytes) {
+  if (bytes == 0) bytes = 1;
+  const uint64_t need = (bytes + align_ - 1) & ~(align_ - 1);
+  if (off % align_ != 0) return false;
+  // the free block that contains [off, off + need)
+  auto it = free_by_off_.upper_bound(off);
+  if (it == free_by_off_.begin()) return false;
+  --it;
+  const uint64_t boff = it->first, bsize = it->second;
+  if (off < boff || off + need > boff + bsize) return false;
+  erase_free(it);
+  if (off > boff) insert_free(boff, off - boff);
+  if (off + need < boff + bsize) insert_free(off + need, boff + bsize - off - need);
+  live_.emplace(off, need);
+  used_ += need;
+  peak_ = std::max(peak_, used_);
+  return true;
+}
+
 void Arena::release(int64_t offset) {
   auto lv = live_.find(static_cast<uint64_t>(offset));
   if (lv == live_.end()) throw std::invalid_argument("arena: release of unknown offset");

@@ -23,6 +23,9 @@ class Arena {
   explicit Arena(uint64_t capacity, uint64_t align = 256);
   // Returns the byte offset, or -1 if no free block is large enough.
   int64_t alloc(uint64_t bytes);
+  // Carve exactly [off, off + bytes) out of a free block (a warm start that must keep a
+  // resident block where it already is). False if that range is not entirely free.
+  bool reserve(uint64_t off, uint64_t bytes);
   void release(int64_t offset);
   uint64_t capacity() const { return capacity_; }
   uint64_t used() const { return used_; }

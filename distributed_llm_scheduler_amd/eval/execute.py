@@ -82,6 +82,7 @@ def run_executed(model: str = "gpt2", schedulers: Optional[Sequence[str]] = None
         total = max(t.memory_required + sum(gb[p] for p in t.params_needed) for t in tasks) + sum(gb.values())
     dev_name = torch.cuda.get_device_name(device) if gpu else "cpu"
     rows: List[TestResult] = []
+    stores = {}  # device_init flag -> ParamStore, shared by every configuration (same weights)
     for regime in regimes:
         spec = _node_spec(ev, nodes, total, regime, world, seed)
         for name in names:
@@ -96,7 +97,7 @@ def run_executed(model: str = "gpt2", schedulers: Optional[Sequence[str]] = None
             loads = sum(1 for e in sched.events if e[1] == "LOAD")
             evicts = sum(1 for e in sched.events if e[1] == "EVICT")
             done, failed = len(sched.completed_tasks), len(sched.failed_tasks)
-            wall, hbm, p2p, fills = _execute(p, rank, device, pg, steps, warmup, use_graph, gpu)
+            wall, hbm, p2p, fills = _execute(p, rank, device, pg, steps, warmup, use_graph, gpu, stores)
             row = TestResult(
                 name, DAG_TYPE.get(model, f"LLM-{model}"), regime, len(tasks), done, failed, makespan, util,
                 st["param_cache_hits"], st["param_cache_misses"], ev.calculate_load_balance(sched, schedule),
@@ -126,14 +127,18 @@ def _node_spec(ev, mode, total, regime, world, seed):
     raise ValueError(f"unknown node construction {mode!r}")
 
 
-def _execute(p, rank, device, pg, steps, warmup, use_graph, gpu):
+def _execute(p, rank, device, pg, steps, warmup, use_graph, gpu, stores=None):
     """(wall ms per step max over ranks, peak HBM GB max over ranks, p2p bytes and
     parameter-fill bytes per steady-state step summed over ranks)."""
     from ..parallel import runtime
 
     # device RNG init straight into HBM, unless the program re-fills groups in the steady
     # state: then every refill must be a real host->HBM copy
-    store = runtime.make_store(p, device_init=gpu and runtime.device_init_ok(p, rank))
+    dev_init = gpu and runtime.device_init_ok(p, rank)
+    stores = {} if stores is None else stores
+    if dev_init not in stores:
+        stores[dev_init] = runtime.make_store(p, device_init=dev_init)
+    store = stores[dev_init]
     ex = runtime.make_executor(p, rank, device, store, pg=pg, use_graph=use_graph)
     stats = None
     for _ in range(max(warmup, 2)):

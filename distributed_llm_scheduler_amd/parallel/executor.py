@@ -79,6 +79,10 @@ MOE_BATCH = os.environ.get("DLS_MOE_BATCH", "1") != "0"
 # link (benchmarks/bench_h2d.py: 50-56 GB/s from 2.4 MB up, 32 GB/s at 0.25 MB, on 32-64
 # workgroups), "dma" = hipMemcpyAsync (42-51 GB/s, 15 GB/s at 0.25 MB)
 REFILL = os.environ.get("DLS_REFILL", "pull")
+# a group the policy evicted counts as gone (default: the executed refill traffic is exactly
+# the policy's decisions); DLS_VICTIM_REUSE=1 instead re-uses its bytes when the region was not
+# overwritten before the group is loaded again at the same offset
+VICTIM_REUSE = os.environ.get("DLS_VICTIM_REUSE", "0") == "1"
 REFILL_BLOCKS = int(os.environ.get("DLS_REFILL_BLOCKS", "64"))
 
 
@@ -121,6 +125,7 @@ class DAGExecutor:
         self._stats_slab: Optional[torch.Tensor] = None
         self._moe_ptrs: Dict[tuple, torch.Tensor] = {}
         self._pending_sends: Dict[int, object] = {}  # send instruction index -> RCCL work
+        self._started = False
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._setup()
@@ -393,6 +398,9 @@ class DAGExecutor:
         off = self.prog.param_offset.get((instr_index, pid))
         if off is None:
             raise RuntimeError(f"parameter group {pid} did not fit the per-GPU parameter budget")
+        return self._views_at(off, pid)
+
+    def _views_at(self, off: int, pid: str):
         total, layout = group_layout(self.store.groups[pid])
         views = {}
         for spec, sub in layout:
@@ -450,8 +458,13 @@ class DAGExecutor:
         self._fill(off, total, layout, views, pid, stats)
 
     def _evict(self, pid: str) -> None:
+        """The policy dropped the group: its bytes count as gone (a later load re-fills it even
+        if the region was not reused meanwhile), so the executed refill traffic is exactly the
+        policy's evict/reload decisions."""
         for name in self._params.pop(pid, {}):
             self._wflat.pop(name, None)
+        if not VICTIM_REUSE:
+            self._valid = [r for r in self._valid if r[2] != pid]
 
     def _w(self, name: str) -> torch.Tensor:
         t = self._wflat.get(name)
@@ -759,6 +772,15 @@ class DAGExecutor:
         tr = self.trace
         self._pending_sends = {}
         self._moe_memo = {}
+        if self.prog.start_resident:  # warm-started program: its start groups are resident
+            first = not self._started
+            for pid, off in self.prog.start_resident.items():
+                o, total, layout, views = self._views_at(off, pid)
+                if first:  # one-time fill before the first step
+                    self._fill(o, total, layout, views, pid, stats)
+                self._params[pid] = views
+                self._wflat.update(views)
+        self._started = True
         if self._stats_slab is not None and not self._zero_in_embedding:
             self._stats_slab.zero_()
 

@@ -22,6 +22,7 @@ at run time, so a rank's whole program is hipGraph-capturable.
 """
 from __future__ import annotations
 
+import os
 from collections import defaultdict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -57,6 +58,11 @@ class Program:
     param_peak_bytes: int = 0
     failed_loads: List[str] = field(default_factory=list)
     n_kernels: int = 0
+    # parameter groups resident (at these arena offsets) when the program starts; the
+    # executor fills them once before the first step, and a warm-started program ends by
+    # restoring them (epilogue loads), so it can repeat step after step
+    start_resident: Dict[str, int] = field(default_factory=dict)
+    end_resident: Dict[str, int] = field(default_factory=dict)      # before the epilogue
 
     @property
     def has_comm(self) -> bool:
@@ -88,9 +94,14 @@ def _fuse_kind(prev_kind: str, nxt: Task) -> Optional[str]:
 def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
                    param_bytes: Dict[str, int], param_cap_bytes: Optional[Dict[int, int]] = None,
                    events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
-                   fuse: bool = True) -> List[Program]:
+                   fuse: bool = True, start_resident: Optional[Dict[int, Dict[str, int]]] = None) -> List[Program]:
     """Build every rank's program. ``placement`` maps task id -> rank; tasks absent from it
-    (failed or orphaned by the scheduler) are skipped together with their dependents."""
+    (failed or orphaned by the scheduler) are skipped together with their dependents.
+
+    ``start_resident`` (rank -> {group: arena offset}): a WARM start — those groups are
+    resident where they are when the program begins (the policy's loads of them become
+    no-ops), and the program ends with the loads that restore exactly that state, so one
+    program is the repeating steady-state step (see :func:`build_steady_programs`)."""
     core = _native.load()
     if core is None:
         raise RuntimeError("native core (_dlsched_core) is required for memory planning")
@@ -158,6 +169,15 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
         def evict(pid):
             ins.append(Instr("evict", param=pid))
             par.release(where.pop(pid))
+
+        start = dict((start_resident or {}).get(rank, {}))
+        for pid, off in sorted(start.items(), key=lambda kv: kv[1]):
+            nbytes = int(param_bytes.get(pid, 0)) or 1
+            if not par.reserve(off, nbytes):
+                raise RuntimeError(f"rank {rank}: warm-start group {pid} does not fit at offset {off}")
+            where[pid] = off
+            extent = max(extent, off + nbytes)
+        prog.start_resident = dict(start)
 
         # parameters of fused-away members whose group has not run yet: the group reads them
         # at its tail's position, so an eviction the policy decided in between is deferred
@@ -235,6 +255,18 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 if any(placement[c] == rank for c in consumers.get(tid, [])) and tid not in received:
                     ins.append(Instr("recv", task=tid, peer=r))
                     received.add(tid)
+        prog.end_resident = dict(where)
+        if start_resident is not None:  # epilogue: restore the start state for the next step
+            for pid in [q for q in where if start.get(q) != where[q]]:
+                evict(pid)
+            for pid, off in sorted(start.items(), key=lambda kv: kv[1]):
+                if pid in where:
+                    continue
+                if not par.reserve(off, int(param_bytes.get(pid, 0)) or 1):
+                    raise RuntimeError(f"rank {rank}: cannot restore {pid} at offset {off}")
+                where[pid] = off
+                ins.append(Instr("load", param=pid))
+                prog.param_offset[(len(ins) - 1, pid)] = off
         prog.param_peak_bytes = par.peak
         prog.param_arena_bytes = extent
         sinks = {t for t in order if not consumers.get(t)}
@@ -312,15 +344,50 @@ def _plan_send_waits(prog: Program) -> None:
                 inflight = [s for s in inflight if s not in hit]
 
 
-def steady_fill_bytes(prog: Program, param_bytes: Dict[str, int], steps: int = 2) -> int:
+def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
+                          param_bytes: Dict[str, int], param_cap_bytes: Optional[Dict[int, int]] = None,
+                          events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
+                          fuse: bool = True, rounds: int = 3) -> List[Program]:
+    """Programs for the repeating step. The cold lowering (empty arenas) plans every load at
+    the offsets an empty arena gives; in steady state the arena instead holds whatever the
+    previous step left, so many of those loads would overwrite resident groups and re-fill
+    them. Instead: start each rank from the state the previous lowering ENDS in (warm start),
+    restore it at the end, and iterate a few rounds; keep the programs that re-fill the fewest
+    bytes per step (every load of a warm program is a real copy)."""
+    progs = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, events, node_rank, fuse)
+    # the cold lowering repeated as is (no start state) is a candidate too
+    best, best_bytes = progs, sum(steady_fill_bytes(p, param_bytes) for p in progs)
+    for _ in range(rounds):
+        warm = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, events, node_rank, fuse,
+                              start_resident={p.rank: p.end_resident for p in progs})
+        nbytes = sum(steady_fill_bytes(p, param_bytes) for p in warm)
+        if nbytes < best_bytes:
+            best, best_bytes = warm, nbytes
+        if all(w.end_resident == p.end_resident for w, p in zip(warm, progs)):
+            break  # fixed point: the next round would lower the same programs
+        progs = warm
+    return best
+
+
+def steady_fill_bytes(prog: Program, param_bytes: Dict[str, int], steps: int = 2,
+                      victim_reuse: Optional[bool] = None) -> int:
     """Parameter bytes the executor copies in the ``steps``-th repetition of the program:
-    a ``load`` costs nothing when its arena region still holds the group from before
-    (the executor's steady-state residency, DAGExecutor._fill), else one DMA of the group."""
-    valid: List[Tuple[int, int, str]] = []
+    a ``load`` costs nothing when its arena region still holds the group from before and it
+    was not evicted since (the executor's steady-state residency, DAGExecutor._fill), else
+    one copy of the group.
+    A warm-started program's start groups are valid from the executor's one-time fill."""
+    if victim_reuse is None:
+        victim_reuse = os.environ.get("DLS_VICTIM_REUSE", "0") == "1"  # executor.VICTIM_REUSE
+    valid: List[Tuple[int, int, str]] = [(off, int(param_bytes.get(pid, 0)) or 1, pid)
+                                         for pid, off in prog.start_resident.items()]
     filled = 0
     for _ in range(steps):
         filled = 0
         for i, ins in enumerate(prog.instrs):
+            if ins.op == "evict":  # an evicted group's bytes are gone (DAGExecutor._evict)
+                if not victim_reuse:
+                    valid = [r for r in valid if r[2] != ins.param]
+                continue
             if ins.op != "load":
                 continue
             off = prog.param_offset.get((i, ins.param))

@@ -14,7 +14,7 @@ from ..core import Node, get_scheduler
 from ..core.task import Task
 from ..models import registry
 from ..models.params import ParamStore, group_layout
-from .program import Program, build_programs, steady_fill_bytes
+from .program import Program, build_programs, build_steady_programs, steady_fill_bytes
 
 
 @dataclass
@@ -105,8 +105,8 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     place = {tid: node_rank[sched.tasks[tid].assigned_node] for tid in sched.completed_tasks}
     order = [item for _, act, _, item in sched.events if act == "RUN"]
     caps = {r: int(caps_gb[r] * 1e9) for r in range(world)}
-    programs = build_programs(tasks, place, order, world, param_bytes, caps, events=sched.events,
-                              node_rank=node_rank, fuse=fuse)
+    programs = build_steady_programs(tasks, place, order, world, param_bytes, caps, events=sched.events,
+                                     node_rank=node_rank, fuse=fuse)
     name = cls.name if placement == "scheduler" else placement
     p = Plan(model, tasks, groups, cfg, name, sched, schedule, place, order, node_rank, programs, param_bytes,
              world, cap_gb, args=args)

@@ -5,8 +5,9 @@ ordering" of SURVEY §5 (race detection), run on the host before anything touche
 
 * **dataflow** — every input of a kernel group is an external input, produced earlier on
   the same rank, or received (``recv``) earlier; a ``send`` only ships a produced tensor;
-* **parameters** — every parameter group a kernel reads is resident (loaded, not
-  evicted) when the group runs;
+* **parameters** — every parameter group a kernel reads is resident (loaded or resident at
+  a warm start, not evicted) when the group runs, and a warm-started program ends in the
+  state it started from;
 * **p2p pairing** — for each ordered pair of ranks the sequence of ``send(t, dst)`` on the
   source equals the sequence of ``recv(t, src)`` on the destination (RCCL p2p matches
   by order, there are no tags);
@@ -42,7 +43,8 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
     for prog in programs:
         r = prog.rank
         have = set()
-        resident: Dict[str, Tuple[int, int]] = {}
+        resident: Dict[str, Tuple[int, int]] = {pid: (off, off + param_bytes.get(pid, 0))
+                                                for pid, off in prog.start_resident.items()}
         act_live: Dict[str, Tuple[int, int, int]] = {}  # tid -> (lo, hi, last use index)
         inflight: Dict[int, Tuple[int, int]] = {}  # send index -> buffer region, until waited
         last_use: Dict[str, int] = {}
@@ -109,6 +111,11 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
                     if oend >= i and _overlap((lo, hi), (olo, ohi)):
                         errs.append(f"{where}: output {ins.task} overwrites live activation {other}")
                 act_live[ins.task] = (lo, hi, last_use.get(ins.task, len(prog.instrs)))
+        if prog.start_resident:
+            end = {pid: reg[0] for pid, reg in resident.items()}
+            if end != prog.start_resident:
+                errs.append(f"rank {r}: warm-started program does not restore its start state "
+                            f"({sorted(set(end.items()) ^ set(prog.start_resident.items()))[:4]}...)")
     # p2p pairing
     for key in set(sends) | set(recvs):
         if sends.get(key, []) != recvs.get(key, []):
