@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--cap-gb", type=float, default=288.0, help="per-GPU HBM budget for parameters")
+    ap.add_argument("--regime", type=float, default=None,
+                    help="memory regime instead of --cap-gb: each GPU's cap is regime x the reference's total "
+                         "need of one request DAG (simulation.py:194-214), e.g. 0.8 = the paper's 80%% experiments")
     ap.add_argument("--cost-model", default="bytes", choices=["bytes", "reference"],
                     help="planning cost model: real tensor bytes, or the reference's 0.5 GB per parameter "
                          "(memory-regime experiments: e.g. gpt2-medium under an 8 GB cap forces evict/reload)")
@@ -82,6 +85,19 @@ def main():
         pg = dist.group.WORLD
 
     replicas = world * args.replicas_per_gpu
+    if args.regime is not None:
+        from distributed_llm_scheduler_amd.eval.simulation import ImprovedSchedulerEvaluator
+        from distributed_llm_scheduler_amd.models import registry
+        from distributed_llm_scheduler_amd.models.params import group_layout
+
+        tasks1, groups1, _ = registry.build(args.model, batch=args.batch, seq=args.seq, cost_model=args.cost_model)
+        if args.cost_model == "reference":
+            need = ImprovedSchedulerEvaluator({}).calculate_total_memory_needed(tasks1)
+        else:
+            gb = {pid: group_layout(g)[0] / 1e9 for pid, g in groups1.items()}
+            need = max(t.memory_required + sum(gb[q] for q in t.params_needed) for t in tasks1) + sum(gb.values())
+        args.cap_gb = round(need * args.regime, 6)
+        log(f"[bench] regime {args.regime}: per-GPU cap {args.cap_gb} GB ({args.cost_model} cost model)")
     t0 = time.time()
     plan = runtime.plan(args.model, world=world, scheduler=args.scheduler, cap_gb=args.cap_gb, replicas=replicas,
                         batch=args.batch, seq=args.seq, cost_model=args.cost_model, fuse=not args.no_fuse,
@@ -162,8 +178,10 @@ def main():
             "tasks_completed": plan.stats["tasks_completed"],
             "tasks_total": plan.stats["tasks_total"],
             "mem_cap_gb_per_gpu": args.cap_gb,
+            "memory_regime": args.regime,
+            "refill_gb_per_step": round(sum(plan.stats["refill_gb_per_step_per_rank"]), 6),
             "cost_model": args.cost_model,
-            "param_loads_per_step": sum(1 for i in plan.programs[rank].instrs if i.op == "load"),
+            "param_loads_per_step": sum(1 for i in plan.programs[rank].instrs if i.op == "load"),  # 0 = all resident
             "param_evictions_per_step": sum(1 for i in plan.programs[rank].instrs if i.op == "evict"),
             "scheduler": plan.scheduler_name,
             "tokens_per_s": round(tokens / (ms_per_step / 1e3), 1),
