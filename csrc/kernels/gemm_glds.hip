@@ -960,6 +960,13 @@ using C28 = Cfg<128, 128, 2, 2, 2, 0, 0, 2>;
 using C29 = Cfg<192, 128, 2, 2, 3>;
 using C30 = Cfg<192, 128, 2, 2, 2, 0, 0, 2>;
 using C31 = Cfg<192, 128, 2, 2, 2, 0, 1>;  // split rings: 2 x 24 KiB A + 3 x 16 KiB W
+// deeper split rings for the HBM-streaming expert GEMMs: 3 x 24 KiB A + 4 x 16 KiB W = 136 KiB
+// keeps 2 A and 3 W tiles in flight (C31: 1 and 2); C33 issues them from 8 waves (48 x 64 wave
+// tiles). Measured (Mixtral-8x7B grouped launches): C33 441 / 206 us for gate-up / down vs C31
+// 465 / 215; C32 (same rings, 4 waves) no faster than C31 — the wave count, not the ring
+// depth, moved it. A 192 x 256 tile (half the routed-row bytes per weight byte) ran > 550 us.
+using C32 = Cfg<192, 128, 2, 2, 3, 0, 1>;
+using C33 = Cfg<192, 128, 4, 2, 3, 0, 1>;
 
 struct Shape {
   int bm, bn;
@@ -969,11 +976,12 @@ constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64
                              {256, 256}, {256, 256}, {256, 128}, {128, 128}, {64, 64},   {64, 64},
                              {128, 64},  {64, 128},  {64, 64},   {64, 64},   {64, 96},   {32, 144},
                              {32, 48},   {64, 96},   {32, 144},  {32, 48},   {128, 128}, {192, 128},
-                             {192, 128}, {192, 128}};
+                             {192, 128}, {192, 128}, {192, 128}, {192, 128}};
 constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
                           64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128, 128,
-                          64, 128, 64};
-constexpr int kNumCfg = 32;
+                          64, 128, 64, 64, 64};
+constexpr int kNumCfg = 34;
+static_assert(kNumCfg <= kGemmPersist, "config ids must stay below the persistent-launch flag");
 
 // call f(Cfg{}) for config id cfg (unknown ids: C3)
 template <class F>
@@ -1010,6 +1018,8 @@ void with_cfg(int cfg, F&& f) {
     case 29: f(C29{}); break;
     case 30: f(C30{}); break;
     case 31: f(C31{}); break;
+    case 32: f(C32{}); break;
+    case 33: f(C33{}); break;
     default: f(C3{}); break;
   }
 }

@@ -67,7 +67,7 @@ int gemm_glds_num_configs();
 int gemm_glds_kstep(int cfg);  // K granularity of a config (64, or 128 for two K groups)
 // cfg | kGemmPersist: the same tile config as a persistent launch (a resident grid walks the
 // tiles; one tile's store drain overlaps the next tile's first loads)
-constexpr int kGemmPersist = 32;
+constexpr int kGemmPersist = 64;
 void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk);
 size_t gemm_glds_workspace_bytes(int M, int N, int splitk);
 // ln_mode: 0 none, 1 LayerNorm, 2 RMSNorm folded into the GEMM (A = raw input rows,

@@ -25,7 +25,7 @@ _table: Optional[Dict[str, Tuple[int, int]]] = None
 _cands: Dict[str, list] = {}     # key -> runner-up (cfg, splitk) by microbenchmark time (for in-DAG refinement)
 _refined: Dict[str, bool] = {}   # key -> chosen by whole-step timing inside a DAG
 REGSTAGE = 100  # config ids >= 100 select the register-staged kernel (csrc ops_binding kRegStage)
-PERSIST = 32    # config | 32: the same LDS-DMA tile config as a persistent launch (kernels.h kGemmPersist)
+PERSIST = 64    # config | 64: the same LDS-DMA tile config as a persistent launch (kernels.h kGemmPersist)
 LIB = 200       # the vendor library (hipBLASLt through torch.mm): a candidate for PLAIN GEMMs only —
                 # a GEMM with a fused epilogue (activation, residual, folded norm, RoPE, row
                 # statistics, SwiGLU, row range) always runs on the HIP kernels
@@ -140,7 +140,7 @@ def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
             out.append((cfg, sk))
     if M * N >= (8 << 20) and K % 64 == 0 and not tg:
         # many more tiles than resident blocks (LM heads): the persistent tile walk of the
-        # 256x128 / 64x64 configs (ops_binding PERSIST = 32)
+        # 256x128 / 64x64 configs (kernels.h kGemmPersist = 64)
         out += [(PERSIST + c, 1) for c in (0, 3, 14) if c < n_cfg]
     return out
 

@@ -301,7 +301,7 @@ def test_gemm_row_range_compact(config, splitk):
     _close(out.cpu().float(), ops.ref_linear(x[:cap].cpu(), w.cpu()).float(), 2e-2)
 
 
-@pytest.mark.parametrize("config", [-1, 3, 15, 17, 25, 1, 28, 29, 30, 31])
+@pytest.mark.parametrize("config", [-1, 3, 15, 17, 25, 1, 28, 29, 30, 31, 32, 33])
 def test_gemm_grouped_experts(config):
     """All experts of a layer in one launch: SwiGLU gate/up into shared rows, then the down
     GEMM into per-expert compact outputs — against per-expert fp32 references."""
