@@ -45,11 +45,11 @@ def test_gemm_identity_asymmetric():
 @pytest.mark.parametrize("config,splitk", [(-1, 0), (100, 1), (103, 1), (0, 1), (1, 1), (2, 1), (3, 1), (4, 1),
                                            (3, 2), (3, 4), (2, 3), (8, 1), (9, 1), (10, 1), (11, 1), (8, 2),
                                            (12, 1), (13, 1), (14, 1), (15, 1), (12, 2), (14, 4),
-                                           (32, 1), (35, 1), (35, 4), (40, 1), (46, 1),  # 32+: persistent
-                                           (16, 1), (17, 1), (18, 1), (19, 1), (16, 2), (17, 3), (48, 1),
+                                           (64, 1), (67, 1), (67, 4), (72, 1), (78, 1),  # 64+: persistent
+                                           (16, 1), (17, 1), (18, 1), (19, 1), (16, 2), (17, 3), (80, 1),
                                            (20, 1), (21, 1), (21, 3), (22, 1), (23, 1), (24, 1),
                                            (25, 1), (26, 1), (27, 1), (22, 4), (24, 2), (27, 3), (28, 1), (28, 2),
-                                           (29, 1), (30, 1), (31, 1), (31, 2)])
+                                           (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
@@ -195,7 +195,7 @@ def test_moe_pipeline():
 @pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
 @pytest.mark.parametrize("M,N,K,cfg", [(512, 2304, 768, -1), (300, 1024, 4096, 0), (512, 3072, 768, 2),
                                        (512, 1024, 1024, 8), (256, 512, 768, 14),
-                                       (512, 2304, 768, 35), (512, 3072, 768, 32), (512, 768, 768, 16),
+                                       (512, 2304, 768, 67), (512, 3072, 768, 64), (512, 768, 768, 16),
                                        (512, 3072, 768, 22), (512, 2304, 768, 23), (512, 768, 768, 24)])
 def test_gemm_with_folded_norm(mode, M, N, K, cfg):
     x = _rand(M, K, scale=2.0, seed=40) + 0.5  # non-zero mean rows exercise the mean correction
