@@ -84,13 +84,20 @@ def lookup_fused(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
 
 
 def _save() -> None:
+    """Write the table atomically (temp file + rename): the ranks of a multi-GPU job share the
+    file, and a reader must never see a half-written one."""
+    tmp = f"{_PATH}.{os.getpid()}.tmp"
     try:
-        with open(_PATH, "w") as f:
+        with open(tmp, "w") as f:
             json.dump({"device": "MI355X (gfx950)", "gemm": {k: list(v) for k, v in sorted(table().items())},
                        "candidates": {k: [list(c) for c in v] for k, v in sorted(_cands.items())},
                        "refined": dict(sorted(_refined.items()))}, f, indent=1)
+        os.replace(tmp, _PATH)
     except OSError:
-        pass
+        try:
+            os.remove(tmp)
+        except OSError:
+            pass
 
 
 def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
@@ -250,9 +257,12 @@ def save() -> None:
 
 def ensure_tuned(shapes: Iterable[tuple], device=None) -> None:
     """Tune every (M, N, K[, variant]) not yet in the table (called by the executor at setup)."""
+    tuned = False
     for sh in sorted(set(shapes)):
         M, N, K = sh[:3]
         tg = sh[3] if len(sh) > 3 else ""
         if _key(M, N, K, tg) not in table():
             tune(M, N, K, device=device, save=False, tg=tg)
-    _save()
+            tuned = True
+    if tuned:  # every shape already known (the usual case, all ranks): leave the file alone
+        _save()
