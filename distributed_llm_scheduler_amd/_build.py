@@ -68,6 +68,30 @@ def _record(out: str, srcs) -> None:
     os.replace(out + ".srchash.tmp", out + ".srchash")
 
 
+class _BuildLock:
+    """Cross-process lock around a staleness check + build: the ranks of a multi-GPU job import
+    the package at the same time, and only one of them may compile (the others wait, then find
+    the library fresh)."""
+
+    def __init__(self, name: str):
+        os.makedirs(BUILD_DIR, exist_ok=True)
+        self.path = os.path.join(BUILD_DIR, name + ".lock")
+        self.f = None
+
+    def __enter__(self):
+        import fcntl
+
+        self.f = open(self.path, "a+")
+        fcntl.flock(self.f.fileno(), fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+
+        fcntl.flock(self.f.fileno(), fcntl.LOCK_UN)
+        self.f.close()
+
+
 def _run(cmd, verbose):
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -84,6 +108,13 @@ def build_core(force: bool = False, verbose: bool = False) -> str:
     hdrs = sorted(glob.glob(os.path.join(CSRC, "core", "*.h")) + glob.glob(os.path.join(CSRC, "runtime", "*.h")))
     if not force and not _stale(CORE_SO, srcs + hdrs):
         return CORE_SO
+    with _BuildLock("core"):
+        if not force and not _stale(CORE_SO, srcs + hdrs):
+            return CORE_SO  # another process built it while we waited
+        return _build_core(srcs, hdrs, pybind11, verbose)
+
+
+def _build_core(srcs, hdrs, pybind11, verbose) -> str:
     cmd = [
         os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
         "-Wall", "-Wno-sign-compare",
@@ -117,6 +148,13 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     binding = os.path.join(CSRC, "kernels", "ops_binding.cpp")
     if not force and not _stale(OPS_SO, kern + hdrs + [binding]):
         return OPS_SO
+    with _BuildLock("ops"):
+        if not force and not _stale(OPS_SO, kern + hdrs + [binding]):
+            return OPS_SO  # another process built it while we waited
+        return _build_ops(kern, hdrs, binding, force, verbose, jobs)
+
+
+def _build_ops(kern, hdrs, binding, force, verbose, jobs) -> str:
     os.makedirs(BUILD_DIR, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     inc, defs, libs = _torch_flags()
