@@ -265,7 +265,9 @@ class DAGExecutor:
         the last earlier instruction that touches an overlapping arena region (a kernel
         group using a parameter group resident there, or an earlier load into it). The
         copy is issued there on the copy stream; the mapping switch stays at i."""
-        region: Dict[str, Tuple[int, int]] = {}
+        # groups resident from a warm start occupy their regions until evicted
+        region: Dict[str, Tuple[int, int]] = {pid: (off, group_layout(self.store.groups[pid])[0])
+                                              for pid, off in self.prog.start_resident.items()}
         touches: List[Tuple[int, List[Tuple[int, int]]]] = []
         for i, ins in enumerate(self.prog.instrs):
             if ins.op == "load":
