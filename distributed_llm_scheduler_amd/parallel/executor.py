@@ -51,6 +51,8 @@ class StepStats:
     bytes_sent: int = 0
     param_fills: int = 0
     bytes_filled: int = 0
+    peer_fills: int = 0   # parameter groups received from a peer's HBM over xGMI
+    bytes_peer: int = 0
     timeline: List[Tuple[str, float, float]] = field(default_factory=list)  # (group, start_ms, end_ms)
     events: List[Tuple[str, str, float, float]] = field(default_factory=list)  # (name, category, start, end)
 
@@ -125,7 +127,9 @@ class DAGExecutor:
         self._stats_slab: Optional[torch.Tensor] = None
         self._moe_ptrs: Dict[tuple, torch.Tensor] = {}
         self._pending_sends: Dict[int, object] = {}  # send instruction index -> RCCL work
+        self._param_recv: Dict[str, object] = {}     # group -> RCCL work of its peer fill
         self._started = False
+        self._steps_done = 0
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._setup()
@@ -270,6 +274,8 @@ class DAGExecutor:
                                               for pid, off in self.prog.start_resident.items()}
         touches: List[Tuple[int, List[Tuple[int, int]]]] = []
         for i, ins in enumerate(self.prog.instrs):
+            if ins.op == "load" and ins.peer >= 0:
+                continue  # fetched from a peer in the step's message order, never hoisted
             if ins.op == "load":
                 off = self.prog.param_offset.get((i, ins.param))
                 if off is None:
@@ -421,7 +427,7 @@ class DAGExecutor:
         img = self._img_override.get(pid)
         if img is None and self.gpu:
             img = self.store.group_image(pid)
-        if img is not None and REFILL == "pull" and img.is_pinned():
+        if img is not None and self.gpu and REFILL == "pull" and img.is_pinned():
             ops.ext().host_pull(self.param_slab[off:off + total], img, REFILL_BLOCKS)
         elif img is not None:  # one DMA of the whole group image
             self.param_slab[off:off + total].copy_(img, non_blocking=True)
@@ -533,9 +539,10 @@ class DAGExecutor:
         return W, d[0], d[1]
 
     def _persist_transform(self, w_name: str, W: torch.Tensor, d: tuple) -> None:
-        """Write the transformed weight into a private copy of its group's pinned host image
-        (GPU stores with host images only; once, in an eager step)."""
-        if not self.gpu or torch.cuda.is_current_stream_capturing():
+        """Write the transformed weight into a private copy of its group's host image (pinned
+        on GPU; once, in an eager step). Every later refill — from the host image, or from a
+        peer that holds the group in the same form — then carries the transformed bytes."""
+        if self.gpu and torch.cuda.is_current_stream_capturing():
             return
         if not self._tensor_home:
             for gid, grp in self.store.groups.items():
@@ -545,9 +552,9 @@ class DAGExecutor:
         img = self._img_override.get(pid)
         if img is None:
             base = self.store.group_image(pid)
-            if base is None or not base.is_pinned():
+            if base is None or (self.gpu and not base.is_pinned()):
                 return  # device-initialised store: nothing is ever re-filled from the host
-            img = base.clone().pin_memory()
+            img = base.clone().pin_memory() if self.gpu else base.clone()
             self._img_override[pid] = img
         nb = W.numel() * W.element_size()
         img[sub:sub + nb].copy_(W.reshape(-1).view(torch.uint8))  # blocking D2H
@@ -797,7 +804,11 @@ class DAGExecutor:
         for i, ins in enumerate(self.prog.instrs):
             if tr:
                 Roctx.push(f"{ins.op}:{ins.task or ins.param}")
-            if ins.op == "load" and hoist is not None and i in pending:
+            if ins.op == "psend":
+                self._psend(i, ins, stats)
+            elif ins.op == "load" and ins.peer >= 0 and self._steps_done > 0:
+                self._peer_load(i, ins, stats)
+            elif ins.op == "load" and hoist is not None and i in pending:
                 off, total, layout, views = self._group_views(i, ins.param)
                 self._params[ins.param] = views
                 self._wflat.update(views)
@@ -805,6 +816,7 @@ class DAGExecutor:
                 if done is not None:
                     torch.cuda.current_stream(self.device).wait_event(done)
             elif ins.op == "load":
+                self._wait_sends(ins)  # the region may still be read by a parameter send
                 t0 = self._mark() if events is not None else None
                 fills = stats.param_fills
                 self._load(i, ins.param, stats)
@@ -828,6 +840,10 @@ class DAGExecutor:
                 stats.bytes_sent += buf.numel() * buf.element_size()
             elif ins.op == "run":
                 for tid in ins.group:
+                    for pid in self.tasks[tid].params_needed:
+                        pw = self._param_recv.pop(pid, None)
+                        if pw is not None:
+                            pw.wait()  # the group arrives from a peer's HBM
                     for d in self.tasks[tid].dependencies:
                         rw = recv_work.pop(d, None)
                         if rw is not None:
@@ -862,6 +878,41 @@ class DAGExecutor:
         for w in self._pending_sends.values():
             w.wait()
         self._pending_sends = {}
+        for w in self._param_recv.values():
+            w.wait()
+        self._param_recv = {}
+        self._steps_done += 1
+
+    def _psend(self, i: int, ins, stats: StepStats) -> None:
+        """Send a resident parameter group to a peer that re-fills it from this rank's HBM
+        (program.plan_peer_fills). The first step has no parameter transfers: every rank fills
+        from its host image and applies its kernels' in-place weight transforms first."""
+        if self._steps_done == 0:
+            return
+        pw = self._param_recv.pop(ins.param, None)
+        if pw is not None:
+            pw.wait()  # this rank received the group itself: forward it once it arrived
+        total = group_layout(self.store.groups[ins.param])[0]
+        buf = self.param_slab[ins.param_off:ins.param_off + total]
+        self._pending_sends[i] = dist.isend(buf, dst=ins.peer, group=self.pg)
+        stats.sends += 1
+        stats.bytes_sent += total
+
+    def _peer_load(self, i: int, ins, stats: StepStats) -> None:
+        """Load a parameter group by receiving it from the peer that holds it."""
+        self._wait_sends(ins)
+        off, total, layout, views = self._group_views(i, ins.param)
+        self._params[ins.param] = views
+        self._wflat.update(views)
+        self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
+        for spec, _ in layout:
+            if spec.name not in self._derived_named:
+                self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
+        self._param_recv[ins.param] = dist.irecv(self.param_slab[off:off + total], src=ins.peer, group=self.pg)
+        self._valid.append((off, total, ins.param))
+        stats.recvs += 1
+        stats.peer_fills += 1
+        stats.bytes_peer += total
 
     def _wait_sends(self, ins) -> None:
         """Complete the in-flight sends whose buffer ``ins`` is about to overwrite (planned

@@ -35,12 +35,16 @@ ALIGN = 256
 
 @dataclass
 class Instr:
-    op: str  # load | evict | recv | send | run
+    op: str  # load | evict | recv | send | psend | run
     task: Optional[str] = None      # producing task (recv/send) or output task (run)
     group: Tuple[str, ...] = ()     # run: fused task ids, execution order
     kind: str = ""                  # run: fused kind (e.g. "linear+gelu")
-    peer: int = -1                  # recv: source rank, send: destination rank
-    param: Optional[str] = None     # load/evict
+    # recv: source rank, send: destination rank; load: >= 0 = fetch the group from this
+    # rank's arena over xGMI (RCCL p2p) instead of the host image; psend: destination rank
+    peer: int = -1
+    param: Optional[str] = None     # load/evict/psend
+    gpos: int = -1                  # position in the global task order this instruction belongs to
+    param_off: int = -1             # psend: the group's offset in this rank's parameter arena
     # run/recv: indices of earlier ``send`` instructions whose buffer this instruction's
     # output region overlaps — they must complete before it writes (see _plan_send_waits)
     wait_sends: Tuple[int, ...] = ()
@@ -66,7 +70,7 @@ class Program:
 
     @property
     def has_comm(self) -> bool:
-        return any(i.op in ("send", "recv") for i in self.instrs)
+        return any(i.op in ("send", "recv", "psend") or (i.op == "load" and i.peer >= 0) for i in self.instrs)
 
     def counts(self) -> Dict[str, int]:
         c: Dict[str, int] = defaultdict(int)
@@ -206,7 +210,11 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
 
         received = set()
         emitted_group = set()
-        for tid in order:
+        n0 = len(ins)
+        for gi, tid in enumerate(order):
+            for x in ins[n0:]:
+                x.gpos = gi - 1
+            n0 = len(ins)
             r = placement[tid]
             t = tmap[tid]
             if r == rank:
@@ -255,6 +263,9 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 if any(placement[c] == rank for c in consumers.get(tid, [])) and tid not in received:
                     ins.append(Instr("recv", task=tid, peer=r))
                     received.add(tid)
+        for x in ins[n0:]:
+            x.gpos = len(order) - 1
+        n0 = len(ins)
         prog.end_resident = dict(where)
         if start_resident is not None:  # epilogue: restore the start state for the next step
             for pid in [q for q in where if start.get(q) != where[q]]:
@@ -267,6 +278,8 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 where[pid] = off
                 ins.append(Instr("load", param=pid))
                 prog.param_offset[(len(ins) - 1, pid)] = off
+        for x in ins[n0:]:
+            x.gpos = len(order)
         prog.param_peak_bytes = par.peak
         prog.param_arena_bytes = extent
         sinks = {t for t in order if not consumers.get(t)}
@@ -400,3 +413,129 @@ def steady_fill_bytes(prog: Program, param_bytes: Dict[str, int], steps: int = 2
             valid.append((off, size, ins.param))
             filled += size
     return filled
+
+
+def _fill_loads(prog: Program, param_bytes: Dict[str, int]) -> set:
+    """Indices of the load instructions that copy bytes in the steady state (every step)."""
+    valid = [(off, int(param_bytes.get(pid, 0)) or 1, pid) for pid, off in prog.start_resident.items()]
+    fills = set()
+    for step in range(2):
+        for i, ins in enumerate(prog.instrs):
+            if ins.op == "evict":
+                valid = [r for r in valid if r[2] != ins.param]
+            elif ins.op == "load":
+                off = prog.param_offset.get((i, ins.param))
+                if off is None:
+                    continue
+                size = int(param_bytes.get(ins.param, 0)) or 1
+                if (off, size, ins.param) in valid:
+                    continue
+                valid = [r for r in valid if r[0] + r[1] <= off or off + size <= r[0]]
+                valid.append((off, size, ins.param))
+                if step == 1:
+                    fills.add(i)
+    return fills
+
+
+def plan_peer_fills(programs: List[Program], tasks: Sequence[Task], param_bytes: Dict[str, int]) -> int:
+    """Parameter refills over xGMI: a steady-state refill of group g on rank B at global
+    position k is fetched from a rank A that holds g at k (loaded earlier in the step, not yet
+    evicted) — an RCCL p2p transfer over one xGMI link (≈153 GB/s) instead of the host link
+    (≈52 GB/s measured). A posts a ``psend`` at position k (ahead of its receives at k, so the
+    per-pair message order matches on both ends); B's load becomes a receive into its region;
+    A's later writes into that region wait for the send. Only between ranks that use g the same
+    way (same fused kernel kinds): a weight is transformed in place for its fused kernel
+    (folded norm, SwiGLU interleave, RoPE order), so bytes are exchanged only in equal form.
+    Senders are spread over the holders (fewest sends first). Returns the number of fetches."""
+    tmap = {t.id: t for t in tasks}
+    if len(programs) < 2:
+        return 0
+    # how each rank uses each group (the in-place transform a fused kernel applies)
+    sig: Dict[Tuple[int, str], frozenset] = defaultdict(frozenset)
+    for pr in programs:
+        acc: Dict[str, set] = defaultdict(set)
+        for ins in pr.instrs:
+            if ins.op == "run":
+                for j, tid in enumerate(ins.group):
+                    for pid in tmap[tid].params_needed:
+                        acc[pid].add((ins.kind, j, tmap[tid].op.kind if tmap[tid].op else ""))
+        for pid, v in acc.items():
+            sig[(pr.rank, pid)] = frozenset(v)
+    # residency intervals (start gpos, end gpos, offset): resident strictly inside (start, end)
+    spans: Dict[str, List[Tuple[int, float, int, int]]] = defaultdict(list)  # pid -> (s, e, off, rank)
+    for pr in programs:
+        open_: Dict[str, Tuple[int, int]] = {pid: (-2, off) for pid, off in pr.start_resident.items()}
+        for i, ins in enumerate(pr.instrs):
+            if ins.op == "load":
+                off = pr.param_offset.get((i, ins.param))
+                if off is not None:
+                    open_[ins.param] = (ins.gpos, off)
+            elif ins.op == "evict" and ins.param in open_:
+                s0, off = open_.pop(ins.param)
+                spans[ins.param].append((s0, ins.gpos, off, pr.rank))
+        for pid, (s0, off) in open_.items():
+            spans[pid].append((s0, float("inf"), off, pr.rank))
+    sends_by: Dict[int, int] = defaultdict(int)
+    plan: Dict[int, List[Tuple[int, str, int, int]]] = defaultdict(list)  # holder -> (gpos, pid, dst, off)
+    n = 0
+    for pr in programs:
+        for i in sorted(_fill_loads(pr, param_bytes)):
+            ins = pr.instrs[i]
+            k, g = ins.gpos, ins.param
+            holders = [(sends_by[r], r, off) for s0, e, off, r in spans[g]
+                       if r != pr.rank and s0 < k < e and sig[(r, g)] == sig[(pr.rank, g)]]
+            if not holders:
+                continue
+            _, a, off = min(holders)
+            ins.peer = a
+            sends_by[a] += 1
+            plan[a].append((k, g, pr.rank, off))
+            n += 1
+    for pr in programs:
+        if plan.get(pr.rank):
+            _insert_psends(pr, plan[pr.rank], param_bytes)
+    return n
+
+
+def _insert_psends(pr: Program, sends: List[Tuple[int, str, int, int]], param_bytes: Dict[str, int]) -> None:
+    """Insert psend(g -> dst) at global position k: before the first instruction of a later
+    position, and before this rank's receives at k. Instruction indices change, so the
+    index-keyed parameter offsets and the send waits are rebuilt."""
+    sends = sorted(sends)
+    old = pr.instrs
+    new: List[Instr] = []
+    remap: Dict[int, int] = {}
+    si = 0
+    for i, ins in enumerate(old):
+        while si < len(sends) and (ins.gpos > sends[si][0] or (ins.gpos == sends[si][0] and ins.op == "recv")):
+            k, g, dst, off = sends[si]
+            new.append(Instr("psend", param=g, peer=dst, gpos=k, param_off=off))
+            si += 1
+        remap[i] = len(new)
+        new.append(ins)
+    for k, g, dst, off in sends[si:]:
+        new.append(Instr("psend", param=g, peer=dst, gpos=k, param_off=off))
+    pr.instrs = new
+    pr.param_offset = {(remap[i], pid): off for (i, pid), off in pr.param_offset.items()}
+    for ins in new:
+        ins.wait_sends = ()
+    _plan_send_waits(pr)
+    _plan_psend_waits(pr, param_bytes)
+
+
+def _plan_psend_waits(pr: Program, param_bytes: Dict[str, int]) -> None:
+    """A psend reads its group's region until the receiver took it: a later load into an
+    overlapping region (a host fill or a peer receive) waits for it first."""
+    inflight: List[Tuple[int, int, int]] = []
+    for i, ins in enumerate(pr.instrs):
+        if ins.op == "psend":
+            inflight.append((i, ins.param_off, ins.param_off + (int(param_bytes.get(ins.param, 0)) or 1)))
+        elif ins.op == "load" and inflight:
+            off = pr.param_offset.get((i, ins.param))
+            if off is None:
+                continue
+            hi = off + (int(param_bytes.get(ins.param, 0)) or 1)
+            hit = [x for x in inflight if x[1] < hi and off < x[2]]
+            if hit:
+                ins.wait_sends = tuple(ins.wait_sends) + tuple(x[0] for x in hit)
+                inflight = [x for x in inflight if x not in hit]

@@ -7,6 +7,7 @@ lowering are pure functions of their arguments.
 from __future__ import annotations
 
 import json
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -14,7 +15,7 @@ from ..core import Node, get_scheduler
 from ..core.task import Task
 from ..models import registry
 from ..models.params import ParamStore, group_layout
-from .program import Program, build_programs, build_steady_programs, steady_fill_bytes
+from .program import Program, build_programs, build_steady_programs, plan_peer_fills, steady_fill_bytes
 
 
 @dataclass
@@ -107,6 +108,8 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     caps = {r: int(caps_gb[r] * 1e9) for r in range(world)}
     programs = build_steady_programs(tasks, place, order, world, param_bytes, caps, events=sched.events,
                                      node_rank=node_rank, fuse=fuse)
+    if world > 1 and os.environ.get("DLS_PEER_FILL", "1") != "0":
+        plan_peer_fills(programs, tasks, param_bytes)  # refills from a peer's HBM over xGMI
     name = cls.name if placement == "scheduler" else placement
     p = Plan(model, tasks, groups, cfg, name, sched, schedule, place, order, node_rank, programs, param_bytes,
              world, cap_gb, args=args)

@@ -8,9 +8,10 @@ ordering" of SURVEY §5 (race detection), run on the host before anything touche
 * **parameters** — every parameter group a kernel reads is resident (loaded or resident at
   a warm start, not evicted) when the group runs, and a warm-started program ends in the
   state it started from;
-* **p2p pairing** — for each ordered pair of ranks the sequence of ``send(t, dst)`` on the
-  source equals the sequence of ``recv(t, src)`` on the destination (RCCL p2p matches
-  by order, there are no tags);
+* **p2p pairing** — for each ordered pair of ranks the sequence of ``send(t, dst)`` /
+  ``psend(group, dst)`` on the source equals the sequence of ``recv(t, src)`` / peer loads on
+  the destination (RCCL p2p matches by order, there are no tags); a psend's group is resident
+  at the offset it sends from, and no load overwrites it before the send is waited;
 * **deadlock freedom** — a simulation of all ranks with non-blocking sends and blocking
   receives (the executor's isend/irecv + wait-at-use) runs every program to completion;
   a send the executor completes before reusing its buffer (``Instr.wait_sends``) blocks
@@ -47,6 +48,7 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
                                                 for pid, off in prog.start_resident.items()}
         act_live: Dict[str, Tuple[int, int, int]] = {}  # tid -> (lo, hi, last use index)
         inflight: Dict[int, Tuple[int, int]] = {}  # send index -> buffer region, until waited
+        pinflight: Dict[int, Tuple[int, int]] = {}  # psend index -> parameter region, until waited
         last_use: Dict[str, int] = {}
         for i, ins in enumerate(prog.instrs):
             if ins.op == "run":
@@ -57,12 +59,27 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
                 last_use[ins.task] = max(last_use.get(ins.task, i), i)
         for i, ins in enumerate(prog.instrs):
             where = f"rank {r} instr {i} ({ins.op} {ins.task or ins.param})"
+            if ins.op == "psend":
+                if ins.param not in resident:
+                    errs.append(f"{where}: sends parameter group {ins.param} it does not hold")
+                elif resident[ins.param][0] != ins.param_off:
+                    errs.append(f"{where}: psend offset {ins.param_off} != resident offset {resident[ins.param][0]}")
+                sends[(r, ins.peer)].append(("param", ins.param))
+                pinflight[i] = (ins.param_off, ins.param_off + param_bytes.get(ins.param, 0))
+                continue
             if ins.op == "load":
                 off = prog.param_offset.get((i, ins.param))
                 if off is None:
                     errs.append(f"{where}: no arena offset for the load")
                     continue
                 reg = (off, off + param_bytes.get(ins.param, 0))
+                if ins.peer >= 0:
+                    recvs[(ins.peer, r)].append(("param", ins.param))
+                for j in ins.wait_sends:
+                    pinflight.pop(j, None)
+                for j, preg in pinflight.items():
+                    if _overlap(reg, preg):
+                        errs.append(f"{where}: overwrites the region of in-flight parameter send {j} without waiting")
                 if reg[1] > prog.param_arena_bytes:
                     errs.append(f"{where}: parameter region {reg} exceeds the arena ({prog.param_arena_bytes} B)")
                 for pid, other in resident.items():
@@ -142,14 +159,17 @@ def _deadlock_check(programs: Sequence[Program]) -> List[str]:
                 ins = prog.instrs[pc[r]]
                 if any((r, j) not in taken for j in ins.wait_sends):
                     break
-                if ins.op == "send":
-                    fifo[(r, ins.peer)].append((ins.task, pc[r]))
-                elif ins.op == "recv":
+                is_precv = ins.op == "load" and ins.peer >= 0
+                if ins.op in ("send", "psend"):
+                    msg = ins.task if ins.op == "send" else ("param", ins.param)
+                    fifo[(r, ins.peer)].append((msg, pc[r]))
+                elif ins.op == "recv" or is_precv:
+                    msg = ins.task if ins.op == "recv" else ("param", ins.param)
                     q = fifo[(ins.peer, r)]
                     if not q:
                         break
-                    if q[0][0] != ins.task:
-                        return [f"rank {r}: recv {ins.task} from {ins.peer} but the next message is {q[0][0]}"]
+                    if q[0][0] != msg:
+                        return [f"rank {r}: recv {msg} from {ins.peer} but the next message is {q[0][0]}"]
                     taken.add((ins.peer, q.popleft()[1]))
                 pc[r] += 1
                 progress = True

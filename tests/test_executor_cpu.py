@@ -274,3 +274,50 @@ def test_replan_after_device_loss():
     assert q.world == 2 and q.args["node_speeds"] == [1.0, 0.8]
     assert q.completed == q.total
     assert set(q.placement.values()) <= {0, 1}
+
+
+def _peer_worker(rank, world, port, model, cap, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = runtime.plan(model, world=world, seq=16, batch=1, replicas=world, cap_gb=cap, cost_model="bytes")
+        store = runtime.make_store(p)
+        ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
+        stats = [ex.step() for _ in range(3)]
+        res = {"rank": rank, "peer": [s.peer_fills for s in stats], "errs": []}
+        for rid in (f"r{k}/" for k in range(world)):
+            if p.placement.get(f"{rid}output_projection") == rank:
+                res["errs"].append(_ref_check(p, ex, store, rid))
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model,cap", [("tiny-gpt2", 0.00012), ("tiny-llama", 0.0002)])
+def test_peer_parameter_fills_two_ranks(model, cap):
+    """Capped replicas on 2 ranks: steady-state refills of a group the other rank holds are
+    received from that rank's arena (RCCL/gloo p2p, the xGMI path) instead of the host image;
+    the first step fills from the host (in-place weight transforms happen there). Logits of
+    every request must still match the fp32 reference after several steps (for Llama the
+    received weights are in their transformed SwiGLU / RoPE form)."""
+    from distributed_llm_scheduler_amd.parallel.validate import check_plan
+
+    p = runtime.plan(model, world=2, seq=16, batch=1, replicas=2, cap_gb=cap, cost_model="bytes")
+    peers = sum(1 for pr in p.programs for i in pr.instrs if i.op == "load" and i.peer >= 0)
+    assert peers > 0 and check_plan(p) == []
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_peer_worker, args=(r, 2, port, model, cap, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    results = [q.get(timeout=5) for _ in range(2)]
+    assert sum(r["peer"][0] for r in results) == 0  # first step: host fills only
+    assert sum(r["peer"][-1] for r in results) == peers
+    errs = [e for r in results for e in r["errs"]]
+    assert len(errs) == 2
+    for err, scale in errs:
+        assert err < 0.02 * scale
