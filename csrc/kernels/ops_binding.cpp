@@ -494,8 +494,22 @@ void host_pull(const at::Tensor& dst, const at::Tensor& src, int64_t blocks) {
   launch_host_pull(dev_src, dst.data_ptr(), n, (int)blocks, cur_stream());
 }
 
+// A device buffer with HIP allocation flags (hipDeviceMallocUncached = 3: reads and writes bypass
+// the caches, so a once-per-step stream — the LM head's 77 MB weight, its 51 MB of logits —
+// does not evict the layer weights from the 256 MB Infinity Cache). Freed with the tensor.
+at::Tensor alloc_device(int64_t nbytes, int64_t flags) {
+  TORCH_CHECK(nbytes > 0 && (flags == 0 || flags == 1 || flags == 3), "alloc_device: bytes > 0, flags 0/1/3");
+  void* p = nullptr;
+  TORCH_CHECK(hipExtMallocWithFlags(&p, (size_t)nbytes, (unsigned)flags) == hipSuccess && p, "hipExtMallocWithFlags failed");
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+  return torch::from_blob(p, {nbytes}, [](void* q) { (void)hipFree(q); },
+                          at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Hand-written HIP/CDNA4 (gfx950) kernels for distributed_llm_scheduler_amd";
+  m.def("alloc_device", &alloc_device, py::arg("nbytes"), py::arg("flags") = 3);
   m.def("host_pull", &host_pull, py::arg("dst"), py::arg("src"), py::arg("blocks") = 256);
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),
         py::arg("act") = 0, py::arg("alpha") = 1.0, py::arg("out") = py::none(), py::arg("config") = -1,
