@@ -67,6 +67,9 @@ class Program:
     # restoring them (epilogue loads), so it can repeat step after step
     start_resident: Dict[str, int] = field(default_factory=dict)
     end_resident: Dict[str, int] = field(default_factory=dict)      # before the epilogue
+    # how the parameter residency was lowered: "cold" / "warm" (the policy's trace from an
+    # empty / a warm arena) or "planned" (plan_keep_sets: kept groups + streamed groups)
+    residency: str = "cold"
 
     @property
     def has_comm(self) -> bool:
@@ -95,58 +98,76 @@ def _fuse_kind(prev_kind: str, nxt: Task) -> Optional[str]:
     return None
 
 
+def _fusion(tmap: Dict[str, Task], placement: Dict[str, int], order: Sequence[str],
+            consumers: Dict[str, List[str]], pos: Dict[str, int], fuse: bool):
+    """Fusion: chains on one rank, consumer is the producer's only consumer, every other
+    input of the consumer is produced before the producer runs. Returns (producer ->
+    consumer that absorbs it, chain end / chain start -> chain)."""
+    fused_into: Dict[str, str] = {}
+    group_of: Dict[str, List[str]] = {}
+    if not fuse:
+        return fused_into, group_of
+    for tid in order:
+        if tid in fused_into:
+            continue
+        chain = [tid]
+        kind = tmap[tid].op.kind if tmap[tid].op else ""
+        while True:
+            cons = consumers.get(chain[-1], [])
+            if len(cons) != 1 or placement[cons[0]] != placement[chain[-1]]:
+                break
+            nxt = cons[0]
+            fk = _fuse_kind(kind, tmap[nxt])
+            if fk is None:
+                break
+            # every other input of nxt must exist before the group starts
+            others = [d for d in tmap[nxt].dependencies if d != chain[-1]]
+            if any(o not in placement or pos.get(o, 1 << 60) > pos[chain[0]] for o in others):
+                break
+            chain.append(nxt)
+            kind = fk
+        if len(chain) > 1:
+            for a in chain[:-1]:
+                fused_into[a] = chain[-1]
+            group_of[chain[-1]] = chain
+            group_of[chain[0]] = chain
+    return fused_into, group_of
+
+
+def _consumers(tmap, placement, order):
+    consumers: Dict[str, List[str]] = defaultdict(list)
+    for tid in order:
+        for d in tmap[tid].dependencies:
+            if d in placement:
+                consumers[d].append(tid)
+    return consumers
+
+
 def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
                    param_bytes: Dict[str, int], param_cap_bytes: Optional[Dict[int, int]] = None,
                    events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
-                   fuse: bool = True, start_resident: Optional[Dict[int, Dict[str, int]]] = None) -> List[Program]:
+                   fuse: bool = True, start_resident: Optional[Dict[int, Dict[str, int]]] = None,
+                   keep: Optional[Dict[int, Sequence[str]]] = None) -> List[Program]:
     """Build every rank's program. ``placement`` maps task id -> rank; tasks absent from it
     (failed or orphaned by the scheduler) are skipped together with their dependents.
 
     ``start_resident`` (rank -> {group: arena offset}): a WARM start — those groups are
     resident where they are when the program begins (the policy's loads of them become
     no-ops), and the program ends with the loads that restore exactly that state, so one
-    program is the repeating steady-state step (see :func:`build_steady_programs`)."""
+    program is the repeating steady-state step (see :func:`build_steady_programs`).
+
+    ``keep`` (rank -> groups): PLANNED residency instead of the policy's trace on those ranks
+    — the kept groups are packed at the bottom of the arena and stay resident step after
+    step; every other group is streamed: loaded before its first use in the step and evicted
+    after its last (see :func:`plan_keep_sets`)."""
     core = _native.load()
     if core is None:
         raise RuntimeError("native core (_dlsched_core) is required for memory planning")
     tmap = {t.id: t for t in tasks}
     pos = {tid: i for i, tid in enumerate(order)}
     order = [t for t in order if t in placement]
-    consumers: Dict[str, List[str]] = defaultdict(list)
-    for tid in order:
-        for d in tmap[tid].dependencies:
-            if d in placement:
-                consumers[d].append(tid)
-
-    # --- fusion: chains on one rank, consumer is the producer's only consumer, every
-    # other input of the consumer is produced before the producer runs
-    fused_into: Dict[str, str] = {}   # producer -> consumer that absorbs it
-    group_of: Dict[str, List[str]] = {}
-    if fuse:
-        for tid in order:
-            if tid in fused_into:
-                continue
-            chain = [tid]
-            kind = tmap[tid].op.kind if tmap[tid].op else ""
-            while True:
-                cons = consumers.get(chain[-1], [])
-                if len(cons) != 1 or placement[cons[0]] != placement[chain[-1]]:
-                    break
-                nxt = cons[0]
-                fk = _fuse_kind(kind, tmap[nxt])
-                if fk is None:
-                    break
-                # every other input of nxt must exist before the group starts
-                others = [d for d in tmap[nxt].dependencies if d != chain[-1]]
-                if any(o not in placement or pos.get(o, 1 << 60) > pos[chain[0]] for o in others):
-                    break
-                chain.append(nxt)
-                kind = fk
-            if len(chain) > 1:
-                for a in chain[:-1]:
-                    fused_into[a] = chain[-1]
-                group_of[chain[-1]] = chain
-                group_of[chain[0]] = chain
+    consumers = _consumers(tmap, placement, order)
+    fused_into, group_of = _fusion(tmap, placement, order, consumers, pos, fuse)
 
     # --- parameter plan per node from the scheduler trace (load-on-first-use otherwise)
     load_before: Dict[str, List[Tuple[str, str]]] = defaultdict(list)  # task -> [(op, pid)] on its rank
@@ -174,14 +195,32 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             ins.append(Instr("evict", param=pid))
             par.release(where.pop(pid))
 
-        start = dict((start_resident or {}).get(rank, {}))
-        for pid, off in sorted(start.items(), key=lambda kv: kv[1]):
-            nbytes = int(param_bytes.get(pid, 0)) or 1
-            if not par.reserve(off, nbytes):
-                raise RuntimeError(f"rank {rank}: warm-start group {pid} does not fit at offset {off}")
-            where[pid] = off
-            extent = max(extent, off + nbytes)
+        kept = None if keep is None or keep.get(rank) is None else list(keep[rank])
+        kept_set = set(kept or ())
+        uses_left: Dict[str, int] = defaultdict(int)  # planned mode: uses of each group still ahead
+        if kept is not None:
+            start = {}
+            for pid in kept:
+                off = par.alloc(int(param_bytes.get(pid, 0)) or 1)
+                if off < 0:
+                    raise RuntimeError(f"rank {rank}: kept groups exceed the parameter arena at {pid}")
+                start[pid] = off
+                where[pid] = off
+                extent = max(extent, off + (int(param_bytes.get(pid, 0)) or 1))
+            for tid in order:
+                if placement[tid] == rank:
+                    for pid in tmap[tid].params_needed:
+                        uses_left[pid] += 1
+        else:
+            start = dict((start_resident or {}).get(rank, {}))
+            for pid, off in sorted(start.items(), key=lambda kv: kv[1]):
+                nbytes = int(param_bytes.get(pid, 0)) or 1
+                if not par.reserve(off, nbytes):
+                    raise RuntimeError(f"rank {rank}: warm-start group {pid} does not fit at offset {off}")
+                where[pid] = off
+                extent = max(extent, off + nbytes)
         prog.start_resident = dict(start)
+        prog.residency = "planned" if kept is not None else ("warm" if start_resident is not None else "cold")
 
         # parameters of fused-away members whose group has not run yet: the group reads them
         # at its tail's position, so an eviction the policy decided in between is deferred
@@ -195,9 +234,10 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             off = par.alloc(nbytes)
             while off < 0:
                 # fragmentation (the scheduler accounts bytes, not contiguity): evict the
-                # least recently used resident group this task does not need, retry
+                # least recently used resident group this task does not need (streamed groups
+                # before kept ones in planned mode), retry
                 victims = sorted((q for q in where if q not in needed and not pinned.get(q)),
-                                 key=lambda q: last_use.get(q, -1))
+                                 key=lambda q: (q in kept_set, last_use.get(q, -1)))
                 if not victims:
                     prog.failed_loads.append(pid)
                     return
@@ -219,7 +259,7 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             t = tmap[tid]
             if r == rank:
                 needed = set(t.params_needed)
-                if events is not None:  # replay the policy's cache decisions
+                if events is not None and kept is None:  # replay the policy's cache decisions
                     for op, pid in load_before.get(tid, []):
                         if op == "evict" and pid in where and pid not in needed:
                             if pinned.get(pid):
@@ -236,6 +276,11 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                     if pid not in where:
                         load(pid, needed | {q for q, c in pinned.items() if c})
                     last_use[pid] = len(ins)
+                if kept is not None:  # streamed group after its last use: out once its group has run
+                    for pid in sorted(needed):
+                        uses_left[pid] -= 1
+                        if uses_left[pid] == 0 and pid not in kept_set and pid not in deferred:
+                            deferred.append(pid)
                 if tid in fused_into:
                     for pid in needed:
                         pinned[pid] += 1
@@ -267,7 +312,7 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             x.gpos = len(order) - 1
         n0 = len(ins)
         prog.end_resident = dict(where)
-        if start_resident is not None:  # epilogue: restore the start state for the next step
+        if start_resident is not None or kept is not None:  # epilogue: restore the start state
             for pid in [q for q in where if start.get(q) != where[q]]:
                 evict(pid)
             for pid, off in sorted(start.items(), key=lambda kv: kv[1]):
@@ -357,16 +402,92 @@ def _plan_send_waits(prog: Program) -> None:
                 inflight = [s for s in inflight if s not in hit]
 
 
+def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
+                   param_bytes: Dict[str, int], budget: Dict[int, float], param_units: Dict[str, float],
+                   param_cap_bytes: Optional[Dict[int, int]] = None, fuse: bool = True) -> Dict[int, List[str]]:
+    """Steady-state residency for a repeating step: per rank, the parameter groups to keep
+    resident; the rest are streamed (loaded before first use, evicted after last use).
+
+    Every group is used once per step, so a kept group saves its whole refill and the
+    per-step refill is the streamed bytes. The constraint is that the kept groups plus the
+    streamed groups live at the same moment fit the budget (``budget[rank]``, the policy's
+    cost units, e.g. the node cap minus the largest activation requirement; and the byte
+    arena ``param_cap_bytes``). Recency-based eviction (the policy's one-pass trace) streams
+    whatever came last — for Llama-3-8B the 1.05 GB LM head, whose buffer then displaces ~1 GB
+    of layers. Here groups are kept greedily by refill bytes per budget unit, largest first,
+    so the streaming buffer is sized by the SMALL groups that remain.
+    """
+    import numpy as np
+
+    tmap = {t.id: t for t in tasks}
+    pos = {tid: i for i, tid in enumerate(order)}
+    order = [t for t in order if t in placement]
+    consumers = _consumers(tmap, placement, order)
+    fused_into, _ = _fusion(tmap, placement, order, consumers, pos, fuse)
+    at = {tid: i for i, tid in enumerate(order)}
+
+    def tail(tid):
+        while tid in fused_into:
+            tid = fused_into[tid]
+        return tid
+
+    caps = param_cap_bytes or {}
+    out: Dict[int, List[str]] = {}
+    for rank in range(world):
+        span: Dict[str, List[int]] = {}
+        for tid in order:
+            if placement[tid] != rank:
+                continue
+            lo, hi = at[tid], at[tail(tid)]
+            for pid in tmap[tid].params_needed:
+                sp = span.setdefault(pid, [lo, hi])
+                sp[0], sp[1] = min(sp[0], lo), max(sp[1], hi)
+        n = max(len(order), 1)
+        live_u, live_b = np.zeros(n), np.zeros(n)
+        units = {pid: float(param_units.get(pid, 0.0)) for pid in span}
+        nbytes = {pid: float(_aligned(param_bytes.get(pid, 0))) for pid in span}
+        for pid, (lo, hi) in span.items():
+            live_u[lo:hi + 1] += units[pid]
+            live_b[lo:hi + 1] += nbytes[pid]
+        cap_u, cap_b = float(budget.get(rank, 0.0)), float(caps.get(rank, 1 << 50))
+        keep_u = keep_b = 0.0
+        kept: List[str] = []
+        ratio = {q: float(param_bytes.get(q, 0)) / max(units[q], 1e-30) for q in span}
+        top = max(ratio.values(), default=1.0) or 1.0
+        for pid in sorted(span, key=lambda q: (-round(ratio[q] / top, 6), -nbytes[q], q)):
+            lo, hi = span[pid]
+            tu, tb = live_u.copy(), live_b.copy()
+            tu[lo:hi + 1] -= units[pid]
+            tb[lo:hi + 1] -= nbytes[pid]
+            if keep_u + units[pid] + max(tu.max(), 0.0) <= cap_u + 1e-9 and \
+                    keep_b + nbytes[pid] + max(tb.max(), 0.0) <= cap_b:
+                kept.append(pid)
+                keep_u += units[pid]
+                keep_b += nbytes[pid]
+                live_u, live_b = tu, tb
+        out[rank] = sorted(kept, key=lambda q: (span[q][0], q))
+    return out
+
+
+def _aligned(nbytes) -> int:
+    nbytes = int(nbytes) or 1
+    return (nbytes + ALIGN - 1) // ALIGN * ALIGN
+
+
 def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
                           param_bytes: Dict[str, int], param_cap_bytes: Optional[Dict[int, int]] = None,
                           events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
-                          fuse: bool = True, rounds: int = 3) -> List[Program]:
+                          fuse: bool = True, rounds: int = 3,
+                          planned: Optional[Tuple[Dict[int, float], Dict[str, float]]] = None) -> List[Program]:
     """Programs for the repeating step. The cold lowering (empty arenas) plans every load at
     the offsets an empty arena gives; in steady state the arena instead holds whatever the
     previous step left, so many of those loads would overwrite resident groups and re-fill
     them. Instead: start each rank from the state the previous lowering ENDS in (warm start),
     restore it at the end, and iterate a few rounds; keep the programs that re-fill the fewest
-    bytes per step (every load of a warm program is a real copy)."""
+    bytes per step (every load of a warm program is a real copy).
+
+    ``planned`` = (budget per rank, budget units per group): a policy whose memory model is
+    the repeating step (EFT) also offers the :func:`plan_keep_sets` residency as a candidate."""
     progs = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, events, node_rank, fuse)
     # the cold lowering repeated as is (no start state) is a candidate too
     best, best_bytes = progs, sum(steady_fill_bytes(p, param_bytes) for p in progs)
@@ -379,6 +500,20 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
         if all(w.end_resident == p.end_resident for w, p in zip(warm, progs)):
             break  # fixed point: the next round would lower the same programs
         progs = warm
+    if planned is not None and best_bytes > 0:
+        keep = plan_keep_sets(tasks, placement, order, world, param_bytes, planned[0], planned[1],
+                              param_cap_bytes, fuse)
+        for _ in range(8):  # best-fit fragmentation of the streaming region: shed kept groups
+            try:
+                cand = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, None, node_rank,
+                                      fuse, keep=keep)
+            except RuntimeError:
+                keep = {r: k[:-1] for r, k in keep.items()}
+                continue
+            nbytes = sum(steady_fill_bytes(p, param_bytes) for p in cand)
+            if nbytes < best_bytes:
+                best, best_bytes = cand, nbytes
+            break
     return best
 
 

@@ -49,7 +49,8 @@ class Plan:
 def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: float = 288.0, replicas: int = 1,
          batch: int = 1, seq: int = 512, cost_model: str = "bytes", fuse: bool = True,
          node_speeds: Optional[Sequence[float]] = None, link_bw_gbps: float = 153.0,
-         placement: str = "scheduler", tp: int = 1, resume: Optional[str] = None, sp: int = 1) -> Plan:
+         placement: str = "scheduler", tp: int = 1, resume: Optional[str] = None, sp: int = 1,
+         residency: Optional[str] = None) -> Plan:
     """Build the DAG of ``replicas`` requests of ``model``, place it on ``world`` GPUs with
     ``scheduler`` under a per-GPU cap of ``cap_gb`` (one value, or one per GPU — the
     reference's heterogeneous node splits) and lower it to per-rank programs.
@@ -65,6 +66,12 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         (context parallelism; the K/V edges between chunks are the cross-GPU transfers).
     The fixed placements still go through the scheduler's memory accounting (tasks that
     do not fit fail exactly as in the policies).
+
+    ``residency`` (default ``$DLS_RESIDENCY`` or ``"auto"``): how parameter residency of the
+    repeating step is lowered — ``"trace"`` replays the policy's LOAD/EVICT trace (cold or
+    warm-started, program.build_steady_programs); ``"auto"`` additionally offers a policy
+    whose memory model is the repeating step (EFT) the planned keep set
+    (program.plan_keep_sets) and keeps whichever re-fills fewer bytes per step.
 
     ``resume``: path of a placement saved by :func:`save_plan` — the saved decision (task
     order per GPU and the LOAD/EVICT trace) is reused instead of re-running the policy; the
@@ -106,8 +113,20 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     place = {tid: node_rank[sched.tasks[tid].assigned_node] for tid in sched.completed_tasks}
     order = [item for _, act, _, item in sched.events if act == "RUN"]
     caps = {r: int(caps_gb[r] * 1e9) for r in range(world)}
+    residency = residency or os.environ.get("DLS_RESIDENCY", "auto")
+    if residency not in ("auto", "trace"):
+        raise ValueError(f"unknown residency {residency!r}")
+    planned = None
+    if residency == "auto" and getattr(sched, "cyclic", False):
+        # EFT's memory model is the repeating step: its residency may be the planned keep set
+        # (program.plan_keep_sets) under the same budget the policy accounted: the node cap
+        # minus the largest activation requirement among the node's tasks
+        tmem = {t.id: t.memory_required for t in tasks}
+        budget = {r: caps_gb[r] - max([tmem[tid] for tid, rr in place.items() if rr == r] or [0.0])
+                  for r in range(world)}
+        planned = (budget, {pid: sched.param_size(pid) for pid in param_bytes})
     programs = build_steady_programs(tasks, place, order, world, param_bytes, caps, events=sched.events,
-                                     node_rank=node_rank, fuse=fuse)
+                                     node_rank=node_rank, fuse=fuse, planned=planned)
     if world > 1 and os.environ.get("DLS_PEER_FILL", "1") != "0":
         plan_peer_fills(programs, tasks, param_bytes)  # refills from a peer's HBM over xGMI
     name = cls.name if placement == "scheduler" else placement

@@ -44,18 +44,23 @@ def test_fusion_reduces_kernels():
     assert kinds[:4] == ["embedding", "layernorm+attention+residual", "layernorm+linear+gelu", "linear+residual"]
 
 
-@pytest.mark.parametrize("sched,cap,warm", [("EFT", 0.00012, False), ("MRU_spec", 0.00012, False),
-                                            ("EFT", 0.0001, True)])
-def test_capped_plan_steady_state_matches_reference(sched, cap, warm):
+@pytest.mark.parametrize("sched,cap,residency,mode", [("EFT", 0.00012, "trace", "cold"),
+                                                     ("MRU_spec", 0.00012, "auto", "cold"),
+                                                     ("EFT", 0.0001, "trace", "warm"),
+                                                     ("EFT", 0.00012, "auto", "planned"),
+                                                     ("EFT", 0.00008, "auto", "planned")])
+def test_capped_plan_steady_state_matches_reference(sched, cap, residency, mode):
     """Under a cap that forces evictions (and, for cyclic EFT, deferred evictions of fused
     norms' weights), repeated steps stay correct and re-fill exactly the planned bytes —
-    for a cold-lowered program and for a warm-started one (start groups filled once, the
-    program restores them at its end)."""
+    for a cold-lowered program, a warm-started one (start groups filled once, the program
+    restores them at its end) and a planned keep set (kept groups resident, the rest
+    streamed)."""
     from distributed_llm_scheduler_amd.parallel.program import steady_fill_bytes
 
-    p = runtime.plan("tiny-gpt2", world=1, scheduler=sched, seq=16, cap_gb=cap)
+    p = runtime.plan("tiny-gpt2", world=1, scheduler=sched, seq=16, cap_gb=cap, residency=residency)
     assert p.completed == p.total and p.programs[0].counts().get("evict", 0) > 0
-    assert bool(p.programs[0].start_resident) is warm
+    assert p.programs[0].residency == mode
+    assert bool(p.programs[0].start_resident) is (mode != "cold")
     store = runtime.make_store(p)
     ex = runtime.make_executor(p, 0, "cpu", store, debug=True)
     for _ in range(3):
