@@ -70,11 +70,14 @@ HANDOFF_MAX_K = int(os.environ.get("DLS_HANDOFF_MAX_K", str(FOLD_MAX_K)))
 GUARD_BYTES, GUARD_VALUE = 4096, 0xA5  # debug-mode canary after each arena slab
 # producer GEMMs emit row statistics for the next folded norm (GPU); DLS_STATS_HANDOFF=0 disables
 STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
-# parameter refills on a side copy stream, hoisted to the earliest safe point (GPU). Off by
-# default: measured on MI355X (gpt2-medium, 8 GB reference-cost cap, MRU_spec: 148 group
-# refills = 0.71 GB per step) the step is host-link bound (~37 GB/s) and the extra
-# cross-stream events cost more (20.4 ms) than the overlap returns (19.4 ms in order)
-PREFETCH = os.environ.get("DLS_PREFETCH", "0") == "1"
+# parameter refills on a side copy stream, hoisted to the earliest safe point (GPU), and the
+# step then runs eagerly (the branches of a captured hipGraph execute one after the other on
+# this stack, benchmarks/bench_graph_concurrency.py). "auto" (default): for planned-residency
+# programs whose streamed loads are issued ahead (Program.prefetch); "1": every program with
+# loads — measured slower for replayed policy traces (gpt2-medium, 8 GB reference-cost cap,
+# MRU_spec: 20.4 vs 19.4 ms: their evictions free a region just before it is re-filled);
+# "0": never (the plans then issue no loads ahead either, runtime.plan)
+PREFETCH = os.environ.get("DLS_PREFETCH", "auto")
 # one grouped launch pair per MoE layer for the experts co-located on this rank (GPU)
 MOE_BATCH = os.environ.get("DLS_MOE_BATCH", "1") != "0"
 # parameter refills: "pull" = the host-pull kernel reads the pinned group image over the host
@@ -190,7 +193,8 @@ class DAGExecutor:
         self._plan_moe_batches()
         self._hoist: Dict[int, List[int]] = {}
         self._copy_stream = None
-        if self.gpu and PREFETCH and any(i.op == "load" for i in p.instrs):
+        if self.gpu and (PREFETCH == "1" or (PREFETCH == "auto" and p.prefetch)) \
+                and any(i.op == "load" for i in p.instrs):
             self._plan_prefetch()
             self._copy_stream = torch.cuda.Stream(self.device)
 
@@ -984,8 +988,8 @@ class DAGExecutor:
 
     def capture(self) -> bool:
         """Capture the steady-state step into a hipGraph (comm-free programs only)."""
-        if not self.use_graph:
-            return False
+        if not self.use_graph or self._copy_stream is not None:
+            return False  # refills overlap kernels only as eager streams
         torch.cuda.synchronize(self.device)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))

@@ -31,6 +31,7 @@ from ..core import native as _native
 from ..core.task import Task
 
 ALIGN = 256
+AHEAD_MAX_EXTRA = 1.10  # issuing streamed loads ahead may cost at most 10 % more refill bytes
 
 
 @dataclass
@@ -70,6 +71,7 @@ class Program:
     # how the parameter residency was lowered: "cold" / "warm" (the policy's trace from an
     # empty / a warm arena) or "planned" (plan_keep_sets: kept groups + streamed groups)
     residency: str = "cold"
+    prefetch: bool = False  # planned with lookahead: loads are issued ahead for a copy stream
 
     @property
     def has_comm(self) -> bool:
@@ -147,7 +149,8 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                    param_bytes: Dict[str, int], param_cap_bytes: Optional[Dict[int, int]] = None,
                    events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
                    fuse: bool = True, start_resident: Optional[Dict[int, Dict[str, int]]] = None,
-                   keep: Optional[Dict[int, Sequence[str]]] = None) -> List[Program]:
+                   keep: Optional[Dict[int, Sequence[str]]] = None,
+                   load_at: Optional[Dict[int, Dict[str, str]]] = None) -> List[Program]:
     """Build every rank's program. ``placement`` maps task id -> rank; tasks absent from it
     (failed or orphaned by the scheduler) are skipped together with their dependents.
 
@@ -159,7 +162,9 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
     ``keep`` (rank -> groups): PLANNED residency instead of the policy's trace on those ranks
     — the kept groups are packed at the bottom of the arena and stay resident step after
     step; every other group is streamed: loaded before its first use in the step and evicted
-    after its last (see :func:`plan_keep_sets`)."""
+    after its last (see :func:`plan_keep_sets`). ``load_at`` (rank -> {streamed group: task}):
+    its load is issued before that earlier task instead, so a copy stream can fill it while
+    the kernels in between run (``Program.prefetch``)."""
     core = _native.load()
     if core is None:
         raise RuntimeError("native core (_dlsched_core) is required for memory planning")
@@ -211,6 +216,11 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 if placement[tid] == rank:
                     for pid in tmap[tid].params_needed:
                         uses_left[pid] += 1
+            ahead: Dict[str, List[str]] = defaultdict(list)
+            for pid, tid in sorted(((load_at or {}).get(rank) or {}).items()):
+                if pid not in kept_set:
+                    ahead[tid].append(pid)
+            prog.prefetch = bool(ahead)
         else:
             start = dict((start_resident or {}).get(rank, {}))
             for pid, off in sorted(start.items(), key=lambda kv: kv[1]):
@@ -227,6 +237,7 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
         # until the group has run (cancelled if the policy loads the group again first)
         pinned: Dict[str, int] = defaultdict(int)
         deferred: List[str] = []
+        early: set = set()  # planned mode: streamed groups loaded ahead, not used yet
 
         def load(pid, needed):
             nonlocal extent
@@ -259,6 +270,12 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             t = tmap[tid]
             if r == rank:
                 needed = set(t.params_needed)
+                if kept is not None:
+                    for pid in ahead.get(tid, ()):
+                        if pid not in where:
+                            load(pid, needed | early | {q for q, c in pinned.items() if c})
+                            early.add(pid)
+                    early -= needed
                 if events is not None and kept is None:  # replay the policy's cache decisions
                     for op, pid in load_before.get(tid, []):
                         if op == "evict" and pid in where and pid not in needed:
@@ -274,7 +291,7 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                                 load(pid, needed | {q for q, c in pinned.items() if c})
                 for pid in sorted(needed):
                     if pid not in where:
-                        load(pid, needed | {q for q, c in pinned.items() if c})
+                        load(pid, needed | early | {q for q, c in pinned.items() if c})
                     last_use[pid] = len(ins)
                 if kept is not None:  # streamed group after its last use: out once its group has run
                     for pid in sorted(needed):
@@ -404,7 +421,8 @@ def _plan_send_waits(prog: Program) -> None:
 
 def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
                    param_bytes: Dict[str, int], budget: Dict[int, float], param_units: Dict[str, float],
-                   param_cap_bytes: Optional[Dict[int, int]] = None, fuse: bool = True) -> Dict[int, List[str]]:
+                   param_cap_bytes: Optional[Dict[int, int]] = None, fuse: bool = True,
+                   lookahead: int = 0) -> Tuple[Dict[int, List[str]], Dict[int, Dict[str, str]]]:
     """Steady-state residency for a repeating step: per rank, the parameter groups to keep
     resident; the rest are streamed (loaded before first use, evicted after last use).
 
@@ -416,7 +434,14 @@ def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
     whatever came last — for Llama-3-8B the 1.05 GB LM head, whose buffer then displaces ~1 GB
     of layers. Here groups are kept greedily by refill bytes per budget unit, largest first,
     so the streaming buffer is sized by the SMALL groups that remain.
+
+    ``lookahead`` = k > 0: a streamed group's load is issued at the first use of the streamed
+    group k places before it (second return value: rank -> {group: task}, for
+    :func:`build_programs`' ``load_at``), and the keep set is chosen with those longer
+    lifetimes. Returns (rank -> kept groups, rank -> load positions).
     """
+    import bisect
+
     import numpy as np
 
     tmap = {t.id: t for t in tasks}
@@ -433,6 +458,7 @@ def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
 
     caps = param_cap_bytes or {}
     out: Dict[int, List[str]] = {}
+    where_load: Dict[int, Dict[str, str]] = {}
     for rank in range(world):
         span: Dict[str, List[int]] = {}
         for tid in order:
@@ -443,30 +469,48 @@ def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 sp = span.setdefault(pid, [lo, hi])
                 sp[0], sp[1] = min(sp[0], lo), max(sp[1], hi)
         n = max(len(order), 1)
-        live_u, live_b = np.zeros(n), np.zeros(n)
         units = {pid: float(param_units.get(pid, 0.0)) for pid in span}
         nbytes = {pid: float(_aligned(param_bytes.get(pid, 0))) for pid in span}
-        for pid, (lo, hi) in span.items():
-            live_u[lo:hi + 1] += units[pid]
-            live_b[lo:hi + 1] += nbytes[pid]
         cap_u, cap_b = float(budget.get(rank, 0.0)), float(caps.get(rank, 1 << 50))
-        keep_u = keep_b = 0.0
-        kept: List[str] = []
         ratio = {q: float(param_bytes.get(q, 0)) / max(units[q], 1e-30) for q in span}
         top = max(ratio.values(), default=1.0) or 1.0
-        for pid in sorted(span, key=lambda q: (-round(ratio[q] / top, 6), -nbytes[q], q)):
-            lo, hi = span[pid]
-            tu, tb = live_u.copy(), live_b.copy()
-            tu[lo:hi + 1] -= units[pid]
-            tb[lo:hi + 1] -= nbytes[pid]
-            if keep_u + units[pid] + max(tu.max(), 0.0) <= cap_u + 1e-9 and \
-                    keep_b + nbytes[pid] + max(tb.max(), 0.0) <= cap_b:
-                kept.append(pid)
-                keep_u += units[pid]
-                keep_b += nbytes[pid]
-                live_u, live_b = tu, tb
+        prio = sorted(span, key=lambda q: (-round(ratio[q] / top, 6), -nbytes[q], q))
+
+        def choose(spans):
+            live_u, live_b = np.zeros(n), np.zeros(n)
+            for pid, (lo, hi) in spans.items():
+                live_u[lo:hi + 1] += units[pid]
+                live_b[lo:hi + 1] += nbytes[pid]
+            keep_u = keep_b = 0.0
+            kept: List[str] = []
+            for pid in prio:
+                lo, hi = spans[pid]
+                tu, tb = live_u.copy(), live_b.copy()
+                tu[lo:hi + 1] -= units[pid]
+                tb[lo:hi + 1] -= nbytes[pid]
+                if keep_u + units[pid] + max(tu.max(), 0.0) <= cap_u + 1e-9 and \
+                        keep_b + nbytes[pid] + max(tb.max(), 0.0) <= cap_b:
+                    kept.append(pid)
+                    keep_u += units[pid]
+                    keep_b += nbytes[pid]
+                    live_u, live_b = tu, tb
+            return kept
+
+        kept = choose(span)
+        if lookahead > 0:
+            # a streamed group is live from the first use of the streamed group `lookahead`
+            # places before it (its load is issued there); the streamed sequence is taken from
+            # the plain choice, then the keep set is re-chosen with the longer lifetimes
+            kset = set(kept)
+            firsts = sorted(span[q][0] for q in span if q not in kset)
+            ext = {}
+            for pid, (lo, hi) in span.items():
+                k = bisect.bisect_left(firsts, lo)  # streamed groups first used before this one
+                ext[pid] = [min(firsts[k - lookahead], lo) if k >= lookahead else lo, hi]
+            kept = choose(ext)
+            where_load[rank] = {q: order[ext[q][0]] for q in span if q not in set(kept) and ext[q][0] < span[q][0]}
         out[rank] = sorted(kept, key=lambda q: (span[q][0], q))
-    return out
+    return out, where_load
 
 
 def _aligned(nbytes) -> int:
@@ -478,7 +522,8 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
                           param_bytes: Dict[str, int], param_cap_bytes: Optional[Dict[int, int]] = None,
                           events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
                           fuse: bool = True, rounds: int = 3,
-                          planned: Optional[Tuple[Dict[int, float], Dict[str, float]]] = None) -> List[Program]:
+                          planned: Optional[Tuple[Dict[int, float], Dict[str, float]]] = None,
+                          lookahead: int = 0) -> List[Program]:
     """Programs for the repeating step. The cold lowering (empty arenas) plans every load at
     the offsets an empty arena gives; in steady state the arena instead holds whatever the
     previous step left, so many of those loads would overwrite resident groups and re-fill
@@ -487,7 +532,9 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
     bytes per step (every load of a warm program is a real copy).
 
     ``planned`` = (budget per rank, budget units per group): a policy whose memory model is
-    the repeating step (EFT) also offers the :func:`plan_keep_sets` residency as a candidate."""
+    the repeating step (EFT) also offers the :func:`plan_keep_sets` residency as a candidate;
+    when it wins and ``lookahead`` > 0, the programs issue its streamed loads that far ahead
+    (a copy stream overlaps them with the kernels; a few more bytes stream)."""
     progs = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, events, node_rank, fuse)
     # the cold lowering repeated as is (no start state) is a candidate too
     best, best_bytes = progs, sum(steady_fill_bytes(p, param_bytes) for p in progs)
@@ -501,20 +548,34 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
             break  # fixed point: the next round would lower the same programs
         progs = warm
     if planned is not None and best_bytes > 0:
-        keep = plan_keep_sets(tasks, placement, order, world, param_bytes, planned[0], planned[1],
-                              param_cap_bytes, fuse)
-        for _ in range(8):  # best-fit fragmentation of the streaming region: shed kept groups
-            try:
-                cand = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, None, node_rank,
-                                      fuse, keep=keep)
-            except RuntimeError:
-                keep = {r: k[:-1] for r, k in keep.items()}
-                continue
-            nbytes = sum(steady_fill_bytes(p, param_bytes) for p in cand)
-            if nbytes < best_bytes:
-                best, best_bytes = cand, nbytes
-            break
+        cand, nbytes = _planned_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, node_rank,
+                                         fuse, planned, 0)
+        if cand is not None and nbytes < best_bytes:
+            best, best_bytes = cand, nbytes
+            if lookahead > 0:  # the same residency with loads issued ahead for a copy stream
+                ahead, ab = _planned_programs(tasks, placement, order, world, param_bytes, param_cap_bytes,
+                                              node_rank, fuse, planned, lookahead)
+                # the longer lifetimes displace kept groups: worth it while the extra refill is
+                # small next to the kernel time it overlaps (Llama-3-8B: +4 % bytes)
+                if ahead is not None and ab <= AHEAD_MAX_EXTRA * nbytes:
+                    best = ahead
     return best
+
+
+def _planned_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, node_rank, fuse, planned,
+                      lookahead):
+    """(programs, steady-state fill bytes) of the planned keep set, or (None, 0)."""
+    keep, load_at = plan_keep_sets(tasks, placement, order, world, param_bytes, planned[0], planned[1],
+                                   param_cap_bytes, fuse, lookahead=lookahead)
+    for _ in range(8):  # best-fit fragmentation of the streaming region: shed kept groups
+        try:
+            progs = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, None, node_rank,
+                                   fuse, keep=keep, load_at=load_at)
+        except RuntimeError:
+            keep = {r: k[:-1] for r, k in keep.items()}
+            continue
+        return progs, sum(steady_fill_bytes(p, param_bytes) for p in progs)
+    return None, 0
 
 
 def steady_fill_bytes(prog: Program, param_bytes: Dict[str, int], steps: int = 2,

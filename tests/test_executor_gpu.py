@@ -63,23 +63,43 @@ def test_memory_capped_reloads_on_gpu():
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_memory_capped_reloads_with_prefetch(monkeypatch, graph):
-    """Refills hoisted onto the side copy stream (DLS_PREFETCH=1) give the same logits."""
+    """Refills hoisted onto the side copy stream (DLS_PREFETCH=1) give the same logits; the
+    step then stays eager (captured branches would run one after the other)."""
     from distributed_llm_scheduler_amd.parallel import executor as exmod
-    monkeypatch.setattr(exmod, "PREFETCH", True)
+    monkeypatch.setattr(exmod, "PREFETCH", "1")
     full = runtime.plan("mini-gpt2", world=1, seq=64)
     need = sum(runtime.make_store(full).nbytes(g) for g in full.groups) / 1e9
-    p = runtime.plan("mini-gpt2", world=1, seq=64, cap_gb=need * 0.5)
+    p = runtime.plan("mini-gpt2", world=1, seq=64, cap_gb=need * 0.5, scheduler="MRU_spec")
     store = runtime.make_store(p)
     ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=graph)
     assert ex._copy_stream is not None and ex._hoist
     for _ in range(2):
         st = ex.step()
-    if graph:
-        assert ex.capture()
-        ex.step()
-    else:
-        assert st.param_fills > 0
+    assert not ex.capture()
+    st = ex.step()
+    assert st.param_fills > 0
     torch.cuda.synchronize()
+    _check(p, ex, store, 0.03)
+
+
+def test_planned_residency_streams_ahead_on_gpu():
+    """EFT's planned keep set with streamed loads issued one streamed group ahead: the
+    default executor (DLS_PREFETCH=auto) fills them on the copy stream; same logits, and the
+    refill bytes are the planned ones."""
+    from distributed_llm_scheduler_amd.parallel.program import steady_fill_bytes
+
+    full = runtime.plan("mini-llama", world=1, seq=64)
+    need = sum(runtime.make_store(full).nbytes(g) for g in full.groups) / 1e9
+    p = runtime.plan("mini-llama", world=1, seq=64, cap_gb=need * 0.6)
+    pr = p.programs[0]
+    assert pr.residency == "planned" and pr.prefetch
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store)
+    assert ex._copy_stream is not None
+    for _ in range(3):
+        st = ex.step()
+    torch.cuda.synchronize()
+    assert st.bytes_filled == steady_fill_bytes(pr, p.param_bytes) > 0
     _check(p, ex, store, 0.03)
 
 
