@@ -32,6 +32,8 @@ from ..core.task import Task
 
 ALIGN = 256
 AHEAD_MAX_EXTRA = 1.10  # issuing streamed loads ahead may cost at most 10 % more refill bytes
+AHEAD_MAX_FILL_RATIO = 8.0  # ... and pays while refill time <= 8 x kernel time (_overlap_pays)
+HOST_LINK_BPS = 56e9  # host -> HBM refill rate, one MI355X (benchmarks/bench_h2d.py)
 
 
 @dataclass
@@ -557,9 +559,27 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
                                               node_rank, fuse, planned, lookahead)
                 # the longer lifetimes displace kept groups: worth it while the extra refill is
                 # small next to the kernel time it overlaps (Llama-3-8B: +4 % bytes)
-                if ahead is not None and ab <= AHEAD_MAX_EXTRA * nbytes:
+                if ahead is not None and ab <= AHEAD_MAX_EXTRA * nbytes and _overlap_pays(tasks, placement, ahead,
+                                                                                          param_bytes):
                     best = ahead
     return best
+
+
+def _overlap_pays(tasks, placement, progs, param_bytes) -> bool:
+    """Issue streamed loads ahead only while the refill time is within AHEAD_MAX_FILL_RATIO x
+    the rank's kernel time (the DAG's compute estimates): overlap can hide at most the kernel
+    time, and a copy-engine fill beside kernels runs ~5 % below the in-order pull kernel.
+    Measured on MI355X, Llama-3-8B (kernels ~9.7 ms) at 90 / 80 / 60 % cap: refill/kernel
+    ratio 1.6 / 5.3 / 12.5 -> 23.0 -> 20.4, 54.0 -> 51.4, 115.2 -> 118.2 ms per step."""
+    comp: Dict[int, float] = defaultdict(float)
+    for t in tasks:
+        if t.id in placement:
+            comp[placement[t.id]] += float(t.compute_time)
+    for pr in progs:
+        fill_s = steady_fill_bytes(pr, param_bytes) / HOST_LINK_BPS
+        if fill_s > AHEAD_MAX_FILL_RATIO * max(comp.get(pr.rank, 0.0), 1e-9):
+            return False
+    return True
 
 
 def _planned_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, node_rank, fuse, planned,
