@@ -965,6 +965,9 @@ using C31 = Cfg<192, 128, 2, 2, 2, 0, 1>;  // split rings: 2 x 24 KiB A + 3 x 16
 // tiles). Measured (Mixtral-8x7B grouped launches): C33 441 / 206 us for gate-up / down vs C31
 // 465 / 215; C32 (same rings, 4 waves) no faster than C31 — the wave count, not the ring
 // depth, moved it. A 192 x 256 tile (half the routed-row bytes per weight byte) ran > 550 us.
+// Role-split rings (half the waves DMA only W, 5-6 tiles deep; the other half only A, 2 deep;
+// 8 or 16 waves) were slower still: 537-545 / 254-268 us — not bytes in flight but the number of
+// DMA-issuing waves per stream bounds these launches.
 using C32 = Cfg<192, 128, 2, 2, 3, 0, 1>;
 using C33 = Cfg<192, 128, 4, 2, 3, 0, 1>;
 
