@@ -193,6 +193,8 @@ class DAGExecutor:
         self._plan_moe_batches()
         self._hoist: Dict[int, List[int]] = {}
         self._await: Dict[str, object] = {}  # group -> copy-stream event its first reader waits on
+        self._carry_at: Dict[int, List[int]] = {}  # instr -> next step's loads issued after it
+        self._carry: Dict[int, object] = {}  # next step's loads already issued -> their events
         self._copy_stream = None
         if self.gpu and (PREFETCH == "1" or (PREFETCH == "auto" and p.prefetch)) \
                 and any(i.op == "load" for i in p.instrs):
@@ -273,14 +275,27 @@ class DAGExecutor:
         """For every ``load`` at instruction i: the earliest point it may start — right after
         the last earlier instruction that touches an overlapping arena region (a kernel
         group using a parameter group resident there, or an earlier load into it). The
-        copy is issued there on the copy stream; the mapping switch stays at i."""
+        copy is issued there on the copy stream; the mapping switch stays at i.
+
+        Loads whose region is free from the step start (hoisted to -1) are carried over the
+        step boundary: the previous step issues them right after the LAST instruction that
+        touches their region (``_carry_at``), so the next step's first refills run under the
+        current step's tail kernels instead of stalling the next step's first kernel."""
         # groups resident from a warm start occupy their regions until evicted
         region: Dict[str, Tuple[int, int]] = {pid: (off, group_layout(self.store.groups[pid])[0])
                                               for pid, off in self.prog.start_resident.items()}
         touches: List[Tuple[int, List[Tuple[int, int]]]] = []
         for i, ins in enumerate(self.prog.instrs):
-            if ins.op == "load" and ins.peer >= 0:
-                continue  # fetched from a peer in the step's message order, never hoisted
+            if ins.op == "load" and ins.peer >= 0:  # fetched from a peer in the message order, never hoisted
+                off = self.prog.param_offset.get((i, ins.param))
+                if off is not None:
+                    size = group_layout(self.store.groups[ins.param])[0]
+                    region[ins.param] = (off, size)
+                    touches.append((i, [(off, size)]))
+                continue
+            if ins.op == "psend":  # reads the group's region
+                touches.append((i, [(ins.param_off, group_layout(self.store.groups[ins.param])[0])]))
+                continue
             if ins.op == "load":
                 off = self.prog.param_offset.get((i, ins.param))
                 if off is None:
@@ -301,6 +316,11 @@ class DAGExecutor:
                 regs = [region[q] for q in used if q in region]
                 if regs:
                     touches.append((i, regs))
+        for i in self._hoist.get(-1, []):  # cross-step: after the region's last toucher
+            off = self.prog.param_offset[(i, self.prog.instrs[i].param)]
+            size = group_layout(self.store.groups[self.prog.instrs[i].param])[0]
+            last = max(ti for ti, regs in touches if any(o < off + size and off < o + n for o, n in regs))
+            self._carry_at.setdefault(last, []).append(i)
 
     def _plan_stats_handoff(self) -> None:
         """Pair every folded norm with the GEMM that produces its input on this rank: the
@@ -810,11 +830,14 @@ class DAGExecutor:
         recv_work: Dict[str, Tuple[object, object]] = {}
         hoist = self._hoist if self._copy_stream is not None else None
         pending: Dict[int, object] = {}
-        if hoist and -1 in hoist:
+        if hoist:
+            pending, self._carry = self._carry, {}  # issued by the previous step's tail
+        if hoist and -1 in hoist and any(k not in pending for k in hoist[-1]):
             ev0 = torch.cuda.Event()
             ev0.record()
             for k in hoist[-1]:
-                self._prefetch(k, ev0, stats, pending, events)
+                if k not in pending:
+                    self._prefetch(k, ev0, stats, pending, events)
         for i, ins in enumerate(self.prog.instrs):
             if tr:
                 Roctx.push(f"{ins.op}:{ins.task or ins.param}")
@@ -879,6 +902,11 @@ class DAGExecutor:
                 elif run is not None:
                     run(ins)
                 stats.kernels += 1
+            if hoist and i in self._carry_at:  # the next step's first refills, under this tail
+                evc = torch.cuda.Event()
+                evc.record()
+                for k in self._carry_at[i]:
+                    self._prefetch(k, evc, stats, self._carry, events)
             if hoist and i in hoist:  # loads whose region is free from here on
                 ev = torch.cuda.Event()
                 ev.record()

@@ -272,12 +272,6 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             t = tmap[tid]
             if r == rank:
                 needed = set(t.params_needed)
-                if kept is not None:
-                    for pid in ahead.get(tid, ()):
-                        if pid not in where:
-                            load(pid, needed | early | {q for q, c in pinned.items() if c})
-                            early.add(pid)
-                    early -= needed
                 if events is not None and kept is None:  # replay the policy's cache decisions
                     for op, pid in load_before.get(tid, []):
                         if op == "evict" and pid in where and pid not in needed:
@@ -295,6 +289,12 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                     if pid not in where:
                         load(pid, needed | early | {q for q, c in pinned.items() if c})
                     last_use[pid] = len(ins)
+                if kept is not None:  # streamed groups issued ahead, after this task's own loads
+                    early -= needed
+                    for pid in ahead.get(tid, ()):
+                        if pid not in where:
+                            load(pid, needed | early | {q for q, c in pinned.items() if c})
+                            early.add(pid)
                 if kept is not None:  # streamed group after its last use: out once its group has run
                     for pid in sorted(needed):
                         uses_left[pid] -= 1
@@ -476,7 +476,8 @@ def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
         cap_u, cap_b = float(budget.get(rank, 0.0)), float(caps.get(rank, 1 << 50))
         ratio = {q: float(param_bytes.get(q, 0)) / max(units[q], 1e-30) for q in span}
         top = max(ratio.values(), default=1.0) or 1.0
-        prio = sorted(span, key=lambda q: (-round(ratio[q] / top, 6), -nbytes[q], q))
+        prio = _spread(sorted(span, key=lambda q: (-round(ratio[q] / top, 6), -nbytes[q], span[q][0], q)),
+                       key=lambda q: (round(ratio[q] / top, 6), nbytes[q]))
 
         def choose(spans):
             live_u, live_b = np.zeros(n), np.zeros(n)
@@ -513,6 +514,25 @@ def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
             where_load[rank] = {q: order[ext[q][0]] for q in span if q not in set(kept) and ext[q][0] < span[q][0]}
         out[rank] = sorted(kept, key=lambda q: (span[q][0], q))
     return out, where_load
+
+
+def _spread(items: List[str], key) -> List[str]:
+    """Reorder each run of equal-``key`` items (in step order) by the bit-reversed run index,
+    so any prefix of the run — the groups the greedy keeps — is spread evenly over the step,
+    and so are the streamed rest: refills then alternate with kernels all through the step
+    instead of bunching (e.g. the 32 equal attention out-projections of Llama-3-8B)."""
+    out: List[str] = []
+    i = 0
+    while i < len(items):
+        j = i
+        while j < len(items) and key(items[j]) == key(items[i]):
+            j += 1
+        run = items[i:j]
+        bits = max(1, (len(run) - 1).bit_length())
+        rev = lambda x: int(format(x, f"0{bits}b")[::-1], 2)  # noqa: E731
+        out += [run[k] for k in sorted(range(len(run)), key=rev)]
+        i = j
+    return out
 
 
 def _aligned(nbytes) -> int:
