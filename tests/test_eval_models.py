@@ -148,3 +148,60 @@ def test_arena_best_fit_and_coalescing():
     assert not c.resident("p0") and c.evictions == 1
     c.acquire("p0", 1000)
     assert c.reloads == 1
+
+
+def _hf_llama_state(cfg, store, moe: bool):
+    """Our parameter tensors under transformers' Llama / Mixtral (5.x) state-dict names."""
+    nh, nkv, D, F = cfg.n_head, cfg.kv_heads, cfg.head_dim, cfg.ffn
+    t = lambda n: store.tensor(n).float()  # noqa: E731
+    sd = {"model.embed_tokens.weight": t("tok_embeddings"), "model.norm.weight": t("norm.weight"),
+          "lm_head.weight": t("output.weight")}
+    for i in range(cfg.n_layer):
+        p, q = f"layers.{i}.", f"model.layers.{i}."
+        wqkv = t(p + "attention.wqkv")
+        sd[q + "self_attn.q_proj.weight"] = wqkv[:nh * D]
+        sd[q + "self_attn.k_proj.weight"] = wqkv[nh * D:(nh + nkv) * D]
+        sd[q + "self_attn.v_proj.weight"] = wqkv[(nh + nkv) * D:]
+        sd[q + "self_attn.o_proj.weight"] = t(p + "attention.wo")
+        sd[q + "input_layernorm.weight"] = t(p + "attention_norm.weight")
+        sd[q + "post_attention_layernorm.weight"] = t(p + "ffn_norm.weight")
+        if moe:
+            sd[q + "mlp.gate.weight"] = t(p + "moe.gate")
+            sd[q + "mlp.experts.gate_up_proj"] = torch.stack([t(p + f"moe.experts.{e}.w13")
+                                                              for e in range(cfg.n_experts)])
+            sd[q + "mlp.experts.down_proj"] = torch.stack([t(p + f"moe.experts.{e}.w2") for e in range(cfg.n_experts)])
+        else:
+            w13 = t(p + "feed_forward.w13")
+            sd[q + "mlp.gate_proj.weight"], sd[q + "mlp.up_proj.weight"] = w13[:F], w13[F:]
+            sd[q + "mlp.down_proj.weight"] = t(p + "feed_forward.w2")
+    return sd
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
+def test_reference_forward_is_hf_llama_mixtral(name):
+    """models.reference.llama_forward == transformers LlamaForCausalLM / MixtralForCausalLM with
+    the same weights (tiny configs, random init, no checkpoint or network): RMSNorm, GQA,
+    RoPE (half-split rotation, rope_theta), SwiGLU, Mixtral's top-2 routing with the
+    renormalised softmax gate and the untied LM head."""
+    transformers = pytest.importorskip("transformers")
+    from distributed_llm_scheduler_amd.models.llama import llama_param_groups
+
+    cfg = get_config(name)
+    moe = bool(cfg.n_experts)
+    kw = dict(vocab_size=cfg.vocab_size, hidden_size=cfg.n_embd, intermediate_size=cfg.ffn,
+              num_hidden_layers=cfg.n_layer, num_attention_heads=cfg.n_head, num_key_value_heads=cfg.kv_heads,
+              max_position_embeddings=cfg.n_positions, rms_norm_eps=cfg.norm_eps, rope_theta=cfg.rope_theta,
+              tie_word_embeddings=False, attention_dropout=0.0)
+    if moe:
+        hf_cfg = transformers.MixtralConfig(num_local_experts=cfg.n_experts, num_experts_per_tok=cfg.top_k, **kw)
+        model = transformers.MixtralForCausalLM(hf_cfg).eval()
+    else:
+        model = transformers.LlamaForCausalLM(transformers.LlamaConfig(**kw)).eval()
+    store = ParamStore(llama_param_groups(cfg), dtype=torch.float32, pin=False)
+    missing, unexpected = model.load_state_dict(_hf_llama_state(cfg, store, moe), strict=False)
+    assert not unexpected and not [k for k in missing if "rotary" not in k]
+    tok = torch.randint(0, cfg.vocab_size, (2, 16), generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        hf = model(tok).logits.float()
+    ref = reference.llama_forward(cfg, store, tok)
+    assert torch.allclose(hf, ref, atol=2e-4, rtol=2e-4), (hf - ref).abs().max()
