@@ -476,8 +476,10 @@ def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
         cap_u, cap_b = float(budget.get(rank, 0.0)), float(caps.get(rank, 1 << 50))
         ratio = {q: float(param_bytes.get(q, 0)) / max(units[q], 1e-30) for q in span}
         top = max(ratio.values(), default=1.0) or 1.0
+        # replicas (ranks with the same groups) keep different equal groups: each one's streamed
+        # groups are then resident on a peer, and plan_peer_fills fetches them over xGMI
         prio = _spread(sorted(span, key=lambda q: (-round(ratio[q] / top, 6), -nbytes[q], span[q][0], q)),
-                       key=lambda q: (round(ratio[q] / top, 6), nbytes[q]))
+                       key=lambda q: (round(ratio[q] / top, 6), nbytes[q]), shift=rank)
 
         def choose(spans):
             live_u, live_b = np.zeros(n), np.zeros(n)
@@ -516,11 +518,14 @@ def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
     return out, where_load
 
 
-def _spread(items: List[str], key) -> List[str]:
+def _spread(items: List[str], key, shift: int = 0) -> List[str]:
     """Reorder each run of equal-``key`` items (in step order) by the bit-reversed run index,
     so any prefix of the run — the groups the greedy keeps — is spread evenly over the step,
     and so are the streamed rest: refills then alternate with kernels all through the step
-    instead of bunching (e.g. the 32 equal attention out-projections of Llama-3-8B)."""
+    instead of bunching (e.g. the 32 equal attention out-projections of Llama-3-8B). ``shift``
+    rotates the run by that many items first: the last quarter of a bit-reversed order is the
+    items at 3 mod 4, so ranks 0..3 shifted by 0..3 stream disjoint quarters (a rotation by a
+    power-of-two fraction of the run would leave the kept set unchanged)."""
     out: List[str] = []
     i = 0
     while i < len(items):
@@ -528,6 +533,8 @@ def _spread(items: List[str], key) -> List[str]:
         while j < len(items) and key(items[j]) == key(items[i]):
             j += 1
         run = items[i:j]
+        r = shift % max(len(run), 1)
+        run = run[r:] + run[:r]
         bits = max(1, (len(run) - 1).bit_length())
         rev = lambda x: int(format(x, f"0{bits}b")[::-1], 2)  # noqa: E731
         out += [run[k] for k in sorted(range(len(run)), key=rev)]

@@ -310,6 +310,11 @@ def test_peer_parameter_fills_two_ranks(model, cap):
     p = runtime.plan(model, world=2, seq=16, batch=1, replicas=2, cap_gb=cap, cost_model="bytes")
     peers = sum(1 for pr in p.programs for i in pr.instrs if i.op == "load" and i.peer >= 0)
     assert peers > 0 and check_plan(p) == []
+    # EFT's planned keep sets differ between the replicas (program.plan_keep_sets shift), so
+    # each rank's streamed groups sit resident in the other's arena
+    assert all(pr.residency == "planned" for pr in p.programs)
+    k0, k1 = (set(pr.start_resident) for pr in p.programs)
+    assert {g.split("/", 1)[-1] for g in k0} != {g.split("/", 1)[-1] for g in k1}
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
