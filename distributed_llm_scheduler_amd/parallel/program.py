@@ -34,6 +34,9 @@ ALIGN = 256
 AHEAD_MAX_EXTRA = 1.10  # issuing streamed loads ahead may cost at most 10 % more refill bytes
 AHEAD_MAX_FILL_RATIO = 8.0  # ... and pays while refill time <= 8 x kernel time (_overlap_pays)
 HOST_LINK_BPS = 56e9  # host -> HBM refill rate, one MI355X (benchmarks/bench_h2d.py)
+# host (Python) work per kernel group of an eager step: Llama-3-8B 6.9 ms / 67 groups
+# (benchmarks/bench_host_overhead.py with DLS_HOST_PROFILE=1)
+EAGER_HOST_S_PER_GROUP = 1e-4
 
 
 @dataclass
@@ -552,7 +555,7 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
                           events: Optional[Sequence[tuple]] = None, node_rank: Optional[Dict[str, int]] = None,
                           fuse: bool = True, rounds: int = 3,
                           planned: Optional[Tuple[Dict[int, float], Dict[str, float]]] = None,
-                          lookahead: int = 0) -> List[Program]:
+                          lookahead: int = 0, force_ahead: bool = False) -> List[Program]:
     """Programs for the repeating step. The cold lowering (empty arenas) plans every load at
     the offsets an empty arena gives; in steady state the arena instead holds whatever the
     previous step left, so many of those loads would overwrite resident groups and re-fill
@@ -563,7 +566,8 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
     ``planned`` = (budget per rank, budget units per group): a policy whose memory model is
     the repeating step (EFT) also offers the :func:`plan_keep_sets` residency as a candidate;
     when it wins and ``lookahead`` > 0, the programs issue its streamed loads that far ahead
-    (a copy stream overlaps them with the kernels; a few more bytes stream)."""
+    (a copy stream overlaps them with the kernels; a few more bytes stream) — where that pays
+    (``_overlap_pays``), or always with ``force_ahead`` (``DLS_PREFETCH=1``)."""
     progs = build_programs(tasks, placement, order, world, param_bytes, param_cap_bytes, events, node_rank, fuse)
     # the cold lowering repeated as is (no start state) is a candidate too
     best, best_bytes = progs, sum(steady_fill_bytes(p, param_bytes) for p in progs)
@@ -586,8 +590,8 @@ def build_steady_programs(tasks: Sequence[Task], placement: Dict[str, int], orde
                                               node_rank, fuse, planned, lookahead)
                 # the longer lifetimes displace kept groups: worth it while the extra refill is
                 # small next to the kernel time it overlaps (Llama-3-8B: +4 % bytes)
-                if ahead is not None and ab <= AHEAD_MAX_EXTRA * nbytes and _overlap_pays(tasks, placement, ahead,
-                                                                                          param_bytes):
+                if ahead is not None and (force_ahead or (ab <= AHEAD_MAX_EXTRA * nbytes and
+                                                          _overlap_pays(tasks, placement, ahead, param_bytes))):
                     best = ahead
     return best
 
@@ -597,14 +601,17 @@ def _overlap_pays(tasks, placement, progs, param_bytes) -> bool:
     the rank's kernel time (the DAG's compute estimates): overlap can hide at most the kernel
     time, and a copy-engine fill beside kernels runs ~5 % below the in-order pull kernel.
     Measured on MI355X, Llama-3-8B (kernels ~9.7 ms) at 90 / 80 / 60 % cap: refill/kernel
-    ratio 1.6 / 5.3 / 12.5 -> 23.0 -> 20.4, 54.0 -> 51.4, 115.2 -> 118.2 ms per step."""
+    ratio 1.6 / 5.3 / 12.5 -> 23.0 -> 20.4, 54.0 -> 51.4, 115.2 -> 118.2 ms per step. The
+    overlapped step runs eagerly (no hipGraph), so the kernel time must also cover the host's
+    launch work (EAGER_HOST_S_PER_GROUP per kernel group), else the step turns host-bound."""
     comp: Dict[int, float] = defaultdict(float)
     for t in tasks:
         if t.id in placement:
             comp[placement[t.id]] += float(t.compute_time)
     for pr in progs:
         fill_s = steady_fill_bytes(pr, param_bytes) / HOST_LINK_BPS
-        if fill_s > AHEAD_MAX_FILL_RATIO * max(comp.get(pr.rank, 0.0), 1e-9):
+        c = comp.get(pr.rank, 0.0)
+        if fill_s > AHEAD_MAX_FILL_RATIO * max(c, 1e-9) or c < EAGER_HOST_S_PER_GROUP * pr.n_kernels:
             return False
     return True
 

@@ -125,9 +125,10 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         budget = {r: caps_gb[r] - max([tmem[tid] for tid, rr in place.items() if rr == r] or [0.0])
                   for r in range(world)}
         planned = (budget, {pid: sched.param_size(pid) for pid in param_bytes})
-    lookahead = 0 if os.environ.get("DLS_PREFETCH", "auto") == "0" else 1  # executor.PREFETCH
+    prefetch = os.environ.get("DLS_PREFETCH", "auto")  # executor.PREFETCH
     programs = build_steady_programs(tasks, place, order, world, param_bytes, caps, events=sched.events,
-                                     node_rank=node_rank, fuse=fuse, planned=planned, lookahead=lookahead)
+                                     node_rank=node_rank, fuse=fuse, planned=planned,
+                                     lookahead=0 if prefetch == "0" else 1, force_ahead=prefetch == "1")
     if world > 1 and os.environ.get("DLS_PEER_FILL", "1") != "0":
         plan_peer_fills(programs, tasks, param_bytes)  # refills from a peer's HBM over xGMI
     name = cls.name if placement == "scheduler" else placement

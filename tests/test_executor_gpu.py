@@ -82,11 +82,16 @@ def test_memory_capped_reloads_with_prefetch(monkeypatch, graph):
     _check(p, ex, store, 0.03)
 
 
-def test_planned_residency_streams_ahead_on_gpu():
-    """EFT's planned keep set with streamed loads issued one streamed group ahead: the
-    default executor (DLS_PREFETCH=auto) fills them on the copy stream; same logits, and the
+def test_planned_residency_streams_ahead_on_gpu(monkeypatch):
+    """EFT's planned keep set with streamed loads issued one streamed group ahead (forced with
+    DLS_PREFETCH=1: at these mini shapes the eager step would be host-bound, so the planner's
+    own choice is in-order): the executor fills them on the copy stream; same logits, and the
     refill bytes are the planned ones."""
+    from distributed_llm_scheduler_amd.parallel import executor as exmod
     from distributed_llm_scheduler_amd.parallel.program import steady_fill_bytes
+
+    monkeypatch.setenv("DLS_PREFETCH", "1")
+    monkeypatch.setattr(exmod, "PREFETCH", "1")
 
     full = runtime.plan("mini-llama", world=1, seq=64)
     need = sum(runtime.make_store(full).nbytes(g) for g in full.groups) / 1e9
