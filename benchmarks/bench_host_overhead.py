@@ -27,6 +27,10 @@ def main():
     for _ in range(3):
         ex.step()
     torch.cuda.synchronize()
+    if os.environ.get("DLS_CAPTURE") == "1":  # hipGraph (segments) as bench.py does
+        print("captured:", ex.capture(), "segments:", len(ex._segments), flush=True)
+        ex.step()
+        torch.cuda.synchronize()
     n = 10
     t0 = time.perf_counter()
     host = []

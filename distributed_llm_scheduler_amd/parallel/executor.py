@@ -103,7 +103,9 @@ class DAGExecutor:
         self.gpu = self.device.type == "cuda"
         self.cfg = model_cfg
         self.pg = pg
-        self.use_graph = use_graph and self.gpu and not program.has_comm
+        # whole-step hipGraph for comm-free programs without copy-stream refills; the others
+        # replay hipGraph SEGMENTS (runs of kernel groups) between their eager RCCL / copy steps
+        self.use_graph = use_graph and self.gpu
         self.seed = seed
         self.trace = trace  # roctx range per instruction (eager steps; a graph replay is one range)
         self.debug = debug  # canary guards after every arena + non-finite check of outputs, per step
@@ -193,6 +195,9 @@ class DAGExecutor:
         self._plan_moe_batches()
         self._hoist: Dict[int, List[int]] = {}
         self._await: Dict[str, object] = {}  # group -> copy-stream event its first reader waits on
+        self._segments: Dict[int, Tuple[int, object]] = {}  # segment start -> (end, hipGraph)
+        self._capture_plan: Optional[Dict[int, int]] = None  # set while capture_segments runs
+        self._seg_pool = None
         self._carry_at: Dict[int, List[int]] = {}  # instr -> next step's loads issued after it
         self._carry: Dict[int, object] = {}  # next step's loads already issued -> their events
         self._copy_stream = None
@@ -838,10 +843,34 @@ class DAGExecutor:
             for k in hoist[-1]:
                 if k not in pending:
                     self._prefetch(k, ev0, stats, pending, events)
-        for i, ins in enumerate(self.prog.instrs):
+        segs = self._segments if (events is None and not tr) else {}
+        n_ins = len(self.prog.instrs)
+        i = -1
+        while i + 1 < n_ins:
+            i += 1
+            ins = self.prog.instrs[i]
+            seg_end = None
+            if ins.op == "run" and (i in segs or (self._capture_plan and i in self._capture_plan)):
+                seg_end = segs[i][0] if i in segs else self._capture_plan[i]
+                for k in range(i, seg_end):  # everything the segment's runs wait for, before it
+                    self._pre_run(self.prog.instrs[k], recv_work, events)
+                if i in segs:
+                    segs[i][1].replay()
+                else:  # capture_segments: record this segment's kernels
+                    g = torch.cuda.CUDAGraph()
+                    # thread-local capture: RCCL's watchdog thread keeps querying its events
+                    with torch.cuda.graph(g, pool=self._seg_pool, capture_error_mode="thread_local"):
+                        for k in range(i, seg_end):
+                            self._issue_run(k, self.prog.instrs[k], stats, None)
+                    self._segments[i] = (seg_end, g)
+                stats.kernels += seg_end - i
+                i = seg_end - 1
+                ins = self.prog.instrs[i]
             if tr:
                 Roctx.push(f"{ins.op}:{ins.task or ins.param}")
-            if ins.op == "psend":
+            if seg_end is not None:
+                pass
+            elif ins.op == "psend":
                 self._psend(i, ins, stats)
             elif ins.op == "load" and ins.peer >= 0 and self._steps_done > 0:
                 self._peer_load(i, ins, stats)
@@ -877,30 +906,8 @@ class DAGExecutor:
                 stats.sends += 1
                 stats.bytes_sent += buf.numel() * buf.element_size()
             elif ins.op == "run":
-                for tid in ins.group:
-                    for pid in self.tasks[tid].params_needed:
-                        self._await_fill(pid)
-                        pw = self._param_recv.pop(pid, None)
-                        if pw is not None:
-                            pw.wait()  # the group arrives from a peer's HBM
-                    for d in self.tasks[tid].dependencies:
-                        rw = recv_work.pop(d, None)
-                        if rw is not None:
-                            rw[0].wait()
-                            if events is not None:
-                                events.append((d, "recv", rw[1], self._mark()))
-                self._wait_sends(ins)  # output region about to be overwritten: its sends must be done
-                run = self._run_group
-                if i in self._moe_batch:  # the layer's experts in one grouped launch pair
-                    run = lambda _ins, _i=i: self._run_moe_batch(_i, stats)  # noqa: E731
-                elif i in self._moe_skip:  # ran with its layer's batch
-                    run = None
-                if run is not None and events is not None:
-                    t0 = self._mark()
-                    run(ins)
-                    events.append((ins.task, "kernel", t0, self._mark()))
-                elif run is not None:
-                    run(ins)
+                self._pre_run(ins, recv_work, events)
+                self._issue_run(i, ins, stats, events)
                 stats.kernels += 1
             if hoist and i in self._carry_at:  # the next step's first refills, under this tail
                 evc = torch.cuda.Event()
@@ -928,6 +935,36 @@ class DAGExecutor:
             w.wait()
         self._param_recv = {}
         self._steps_done += 1
+
+    def _pre_run(self, ins, recv_work, events) -> None:
+        """What a run must wait for: copy-stream fills and peer receives of its parameter
+        groups, receives of its inputs, in-flight sends of the region it overwrites."""
+        for tid in ins.group:
+            for pid in self.tasks[tid].params_needed:
+                self._await_fill(pid)
+                pw = self._param_recv.pop(pid, None)
+                if pw is not None:
+                    pw.wait()  # the group arrives from a peer's HBM
+            for d in self.tasks[tid].dependencies:
+                rw = recv_work.pop(d, None)
+                if rw is not None:
+                    rw[0].wait()
+                    if events is not None:
+                        events.append((d, "recv", rw[1], self._mark()))
+        self._wait_sends(ins)  # output region about to be overwritten: its sends must be done
+
+    def _issue_run(self, i: int, ins, stats: StepStats, events) -> None:
+        run = self._run_group
+        if i in self._moe_batch:  # the layer's experts in one grouped launch pair
+            run = lambda _ins, _i=i: self._run_moe_batch(_i, stats)  # noqa: E731
+        elif i in self._moe_skip:  # ran with its layer's batch
+            run = None
+        if run is not None and events is not None:
+            t0 = self._mark()
+            run(ins)
+            events.append((ins.task, "kernel", t0, self._mark()))
+        elif run is not None:
+            run(ins)
 
     def _psend(self, i: int, ins, stats: StepStats) -> None:
         """Send a resident parameter group to a peer that re-fills it from this rank's HBM
@@ -1030,9 +1067,12 @@ class DAGExecutor:
         return tid in self._local_consumed
 
     def capture(self) -> bool:
-        """Capture the steady-state step into a hipGraph (comm-free programs only)."""
-        if not self.use_graph or self._copy_stream is not None:
-            return False  # refills overlap kernels only as eager streams
+        """Capture the steady-state step into a hipGraph: the whole step for a comm-free
+        program without copy-stream refills, else its kernel-group segments (capture_segments)."""
+        if not self.use_graph:
+            return False
+        if self._copy_stream is not None or self.prog.has_comm:
+            return self.capture_segments()
         torch.cuda.synchronize(self.device)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -1047,6 +1087,64 @@ class DAGExecutor:
         self._graph = g
         return True
 
+    def _plan_segments(self) -> List[Tuple[int, int]]:
+        """[start, end) ranges of consecutive ``run`` instructions that replay as one hipGraph.
+        Everything a run waits for (a copy-stream fill, a peer's parameter group, a received
+        activation, an in-flight send of its output region) happens eagerly BEFORE its segment,
+        so such a run starts a segment (waiting earlier inside one would delay the runs before
+        it); a prefetch issue point (the copy stream waits for the compute stream there) ends
+        one. Non-run instructions (loads, evictions, p2p) stay eager between segments."""
+        pre = set(sum(self._hoist.values(), [])) | set(sum(self._carry_at.values(), []))
+        fresh: set = set()  # groups / activations whose first reader must start a segment
+        received = set()
+        starts, ends = set(), set()
+        for i, ins in enumerate(self.prog.instrs):
+            if ins.op == "load" and (i in pre or ins.peer >= 0):
+                fresh.add(ins.param)
+            elif ins.op == "recv":
+                received.add(ins.task)
+            elif ins.op == "run":
+                needs = set()
+                deps = set()
+                for tid in ins.group:
+                    needs |= self.tasks[tid].params_needed
+                    deps |= set(self.tasks[tid].dependencies)
+                if needs & fresh or deps & received or ins.wait_sends:
+                    starts.add(i)
+                fresh -= needs
+                received -= deps
+                if i in self._hoist or i in self._carry_at:
+                    ends.add(i)
+        segs: List[Tuple[int, int]] = []
+        i, n = 0, len(self.prog.instrs)
+        while i < n:
+            if self.prog.instrs[i].op != "run":
+                i += 1
+                continue
+            j = i + 1
+            while j < n and self.prog.instrs[j].op == "run" and j not in starts and (j - 1) not in ends:
+                j += 1
+            segs.append((i, j))
+            i = j
+        return segs
+
+    def capture_segments(self) -> bool:
+        """Piecewise capture for programs that must stay eager around RCCL p2p or copy-stream
+        refills: one hipGraph per kernel-group segment (_plan_segments), sharing one memory
+        pool, captured in program order during a steady-state step (the host bookkeeping of
+        that step runs as usual; its segment kernels are recorded, not run)."""
+        self._segments = {}
+        segs = [(a, b) for a, b in self._plan_segments()]
+        if not segs:
+            return False
+        torch.cuda.synchronize(self.device)
+        self._capture_plan = {a: b for a, b in segs}
+        self._seg_pool = torch.cuda.graph_pool_handle()
+        self._step_body(StepStats())  # segments captured in order as the step reaches them
+        self._capture_plan = None
+        torch.cuda.synchronize(self.device)
+        return bool(self._segments)
+
     def refine_tuning(self, top: int = 3, reps: int = 20, min_gain: float = 0.01, force: bool = False) -> Dict:
         """GEMM config choice by WHOLE-STEP time: for every GEMM shape this rank runs (costliest
         first), try the microbenchmark's runner-up configs inside the captured hipGraph of the
@@ -1055,8 +1153,8 @@ class DAGExecutor:
         Persists the choices (ops/gemm_tuning.json). Returns {key: (old, new, step_ms)}."""
         from ..ops import tuning
 
-        if not (self.gpu and self.use_graph):
-            return {}
+        if not (self.gpu and self.use_graph) or self._copy_stream is not None or self.prog.has_comm:
+            return {}  # whole-step graphs only
 
         def step_ms():
             self._graph = None

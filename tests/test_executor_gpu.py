@@ -75,7 +75,9 @@ def test_memory_capped_reloads_with_prefetch(monkeypatch, graph):
     assert ex._copy_stream is not None and ex._hoist
     for _ in range(2):
         st = ex.step()
-    assert not ex.capture()
+    if graph:  # kernel-group segments replay as hipGraphs between the eager refills
+        assert ex.capture() and ex._segments and ex._graph is None
+    st = ex.step()
     st = ex.step()
     assert st.param_fills > 0
     torch.cuda.synchronize()
@@ -105,6 +107,14 @@ def test_planned_residency_streams_ahead_on_gpu(monkeypatch):
         st = ex.step()
     torch.cuda.synchronize()
     assert st.bytes_filled == steady_fill_bytes(pr, p.param_bytes) > 0
+    _check(p, ex, store, 0.03)
+    # the same with the kernel groups between refills replayed as hipGraph segments
+    assert ex.capture() and len(ex._segments) > 1
+    for _ in range(3):
+        st = ex.step()
+    torch.cuda.synchronize()
+    assert st.bytes_filled == steady_fill_bytes(pr, p.param_bytes)
+    assert st.kernels == pr.n_kernels
     _check(p, ex, store, 0.03)
 
 
