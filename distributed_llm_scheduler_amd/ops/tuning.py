@@ -126,18 +126,23 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
     return statistics.median(res)
 
 
+# csrc gemm_glds kKStep: K granularity per LDS-DMA config id (64; 128 / 256 for two / four K groups)
+_KSTEP = [64] * 16 + [128] * 4 + [256] * 2 + [64] * 3 + [128] * 4 + [64, 128, 64, 64, 64]
+# configs whose 48- / 144-column wave tiles cannot pair SwiGLU gate/up fragments
+SWIGLU_BAD = frozenset(range(22, 28))
+
+
 def kstep(cfg: int) -> int:
-    """K granularity of an LDS-DMA config (csrc gemm_glds kKStep): 64, or 128 / 256 for the
-    two / four K-group configs 16-19, 25-28, 30 / 20-21."""
+    """K granularity of an LDS-DMA config (csrc gemm_glds kKStep)."""
     c = cfg % PERSIST if cfg < REGSTAGE else 0
-    return 256 if c in (20, 21) else 128 if (16 <= c <= 19 or 25 <= c <= 28 or c == 30) else 64
+    return _KSTEP[c] if c < len(_KSTEP) else 64
 
 
 def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
     out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1), (LIB, 1)]
     for cfg in range(n_cfg):
         ks = kstep(cfg)
-        if 22 <= cfg <= 27 and "s" in tg:
+        if cfg in SWIGLU_BAD and "s" in tg:
             continue  # 48/144-column wave tiles cannot pair SwiGLU gate/up fragments
         for sk in ((1,) if "g" in tg else (1, 2, 3, 4, 6, 8)):  # grouped launches: no split-K
             if K % 64 or K % (ks * sk) or (sk > 1 and N % 8) or K // (ks * sk) < 2:

@@ -1145,12 +1145,15 @@ class DAGExecutor:
         torch.cuda.synchronize(self.device)
         return bool(self._segments)
 
-    def refine_tuning(self, top: int = 3, reps: int = 20, min_gain: float = 0.01, force: bool = False) -> Dict:
+    def refine_tuning(self, top: int = 3, reps: int = 20, min_gain: float = 0.01, force: bool = False,
+                      exhaustive: bool = False, log=None) -> Dict:
         """GEMM config choice by WHOLE-STEP time: for every GEMM shape this rank runs (costliest
         first), try the microbenchmark's runner-up configs inside the captured hipGraph of the
         real step and keep one only if the step gets faster by > ``min_gain``. The cold-weight
         microbenchmark misses the DAG's cache state and neighbour kernels; this does not.
-        Persists the choices (ops/gemm_tuning.json). Returns {key: (old, new, step_ms)}."""
+        ``exhaustive``: every valid (config, split-K <= 4) of the shape instead of the runner-ups
+        (``log(key, cand, ms)`` sees each timing). Persists the choices (ops/gemm_tuning.json).
+        Returns {key: (old, new, step_ms)}."""
         from ..ops import tuning
 
         if not (self.gpu and self.use_graph) or self._copy_stream is not None or self.prog.has_comm:
@@ -1187,11 +1190,21 @@ class DAGExecutor:
                     tuning.set_choice(M, N, K, tg, prev)
             cur = tuning.lookup(M, N, K, tg)
             best, best_ms = cur, base
-            for cand in tuning.runner_ups(M, N, K, tg, top + 1):
+            if exhaustive:
+                cands = [c for c in tuning.candidates(M, N, K, ops.ext().gemm_glds_num_configs(), tg)
+                         if c[1] <= 4 and (c[0] < tuning.REGSTAGE or c[0] == tuning.LIB)]
+            else:
+                cands = tuning.runner_ups(M, N, K, tg, top + 1)
+            for cand in cands:
                 if tuple(cand) == tuple(cur):
                     continue
                 tuning.set_choice(M, N, K, tg, cand)
-                ms = step_ms()
+                try:
+                    ms = step_ms()
+                except RuntimeError:  # a config this shape / epilogue cannot run
+                    continue
+                if log is not None:
+                    log(f"{M}x{N}x{K}{tg}", tuple(cand), ms)
                 if ms < best_ms * (1.0 - min_gain):
                     best, best_ms = tuple(cand), ms
             tuning.set_choice(M, N, K, tg, best)
