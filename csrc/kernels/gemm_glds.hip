@@ -170,7 +170,7 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                                int kbeg, int nk, int lane, int wave, int kgrp, int wm, int wn,
                                                bool ln_acc, f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
-                                               float (&st_q)[C::FM]) {
+                                               float (&st_q)[C::FM], const int* __restrict__ arows) {
   // `wave` is the wave's index in the whole block (all K groups issue DMA); instruction
   // gi = wave*PW + j loads 8 rows of K-tile gi / INSTR of the stage
   const bf16* src[C::PW];
@@ -183,7 +183,8 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
     const int gch = (lane & 7) ^ (row & 7);
     const int kofs = kbeg + sub * C::BK + gch * 8;
     if (row < C::BM) {
-      const int gm = min(m0 + row, M - 1);
+      int gm = min(m0 + row, M - 1);
+      if (arows) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
       src[j] = A + (size_t)gm * lda + kofs;
     } else {
       const int gn = min(n0 + row - C::BM, N - 1);
@@ -222,14 +223,15 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                                int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
                                                f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
-                                               float (&st_q)[C::FM], int fmv = C::FM) {
+                                               float (&st_q)[C::FM], int fmv, const int* __restrict__ arows) {
   static_assert(C::SB == C::SA + 1, "split rings: W ring is one deeper than A");
   const bf16* srcA[C::PWA];
   const bf16* srcB[C::PWB];
 #pragma unroll
   for (int j = 0; j < C::PWA; ++j) {
     const int row = 8 * (wave * C::PWA + j) + (lane >> 3);
-    const int gm = min(m0 + row, M - 1);
+    int gm = min(m0 + row, M - 1);
+    if (arows) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
     srcA[j] = A + (size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8;
   }
 #pragma unroll
@@ -311,10 +313,10 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
   if constexpr (C::BXS > 0)
     mainloop_split<C, WPOL, SKIP>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
-                                  st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)));
+                                  st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), ep.a_rows);
   else
     mainloop_joint<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
-                      st_q);
+                      st_q, ep.a_rows);
   if constexpr (C::KG > 1) {
     // sum the K groups' accumulators into group 0 (lane-contiguous 16-B records)
     __syncthreads();
@@ -670,15 +672,18 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
     const bf16* Wg = reinterpret_cast<const bf16*>(ep.grp_w[g]);
     bf16* Cg = ep.grp_c ? reinterpret_cast<bf16*>(ep.grp_c[g]) : Cp + (size_t)r0 * ldc;
-    const bf16* Ag = A + (size_t)r0 * lda;
+    // gathered A: the group's rows are tokens a_rows[r0 ..]; else rows r0.. of the sorted A
+    Epi eg = ep;
+    if (ep.a_rows) eg.a_rows = ep.a_rows + r0;
+    const bf16* Ag = ep.a_rows ? A : A + (size_t)r0 * lda;
     for (int t = 0; t * C::BM < Mr; ++t) {
       if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
       if (C::BXS > 0 && ep.w_stream)
         glds_tile<C, 0, kPolStream, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K,
-                                          act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep);
+                                          act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, eg);
       else
         glds_tile<C, 0>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act, alpha, 0, K, t,
-                        tn, ln_colsum, 0, ln_eps, ep);
+                        tn, ln_colsum, 0, ln_eps, eg);
     }
     return;
   }
@@ -1076,7 +1081,8 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
 }
 
 void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const int* offsets,
-                              const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s) {
+                              const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s,
+                              const int* a_rows) {
   cfg &= kGemmPersist - 1;
   if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
   with_cfg(cfg, [&](auto c) {
@@ -1087,7 +1093,7 @@ void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const in
       const char* e = std::getenv("DLS_EXPERT_NT");
       return e && e[0] == '0' ? 0 : 1;
     }();
-    const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs, w_stream};
+    const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs, w_stream, a_rows};
     const int tiles_n = (a.N + C::BN - 1) / C::BN;
     hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(n_groups * tiles_n), dim3(C::T), 0, s, (const bf16*)a.A,
                        a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0, nullptr, a.M, a.N, a.K, a.act,

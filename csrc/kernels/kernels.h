@@ -57,6 +57,9 @@ struct Epi {
   const unsigned long long* grp_c = nullptr;
   // grouped launch: weight DMA with the streaming (nt) cache policy (split-ring configs)
   int w_stream = 0;
+  // grouped launch: A row r of the expert-sorted order is row a_rows[r] of A (the token
+  // matrix) — the MoE permute folded into the DMA source addresses; nullptr -> A is sorted
+  const int* a_rows = nullptr;
 };
 
 int gemm_pick_config(int M, int N, int K);
@@ -82,7 +85,8 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
 // writes them either at the same rows of a.C (c_ptrs == nullptr) or compactly to rows
 // 0..min(count, a.compact_rows)-1 of c_ptrs[g]. No split-K; any LDS-DMA config.
 void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const int* offsets,
-                              const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s);
+                              const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s,
+                              const int* a_rows = nullptr);
 
 struct AttnArgs {
   const void* q; int ldq;   // bf16, row = token (b*S + s), head h at column h*D
@@ -121,6 +125,10 @@ void launch_moe_router(const void* logits, int M, int E, int topk, int32_t* topk
                        hipStream_t s);
 void launch_moe_align(const int32_t* topk_idx, int M, int topk, int E, int32_t* src_rows, int32_t* slot_of,
                       int32_t* offsets, hipStream_t s);
+// router + align in one workgroup (M * topk <= kRouteMaxAssign): same outputs as the pair
+constexpr int kRouteMaxAssign = 16384;
+void launch_moe_route(const void* logits, int M, int E, int topk, int32_t* topk_idx, float* topk_w,
+                      int32_t* src_rows, int32_t* slot_of, int32_t* offsets, hipStream_t s);
 void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int rows, int H, hipStream_t s);
 void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
                         int topk, int H, const int32_t* range, hipStream_t s);

@@ -87,6 +87,96 @@ __global__ __launch_bounds__(1024) void align_kernel(const int32_t* __restrict__
   if (tid == 0) offsets[E] = base_s;
 }
 
+// Router + align fused into ONE workgroup: per token the top-k experts (router_kernel's
+// selection: ties go to the lower expert index) and renormalised gates, then the counting sort
+// of the M*k assignments by expert in align_kernel's order (stable in assignment index i =
+// m*k + j), so the outputs equal the two-launch pair exactly. The experts of the assignments
+// stay in LDS; ranks within a 64-assignment wave come from one ballot per expert, wave
+// prefixes from an LDS table: two barriers per 1024 assignments instead of three per expert.
+__global__ __launch_bounds__(1024) void route_kernel(const bf16* __restrict__ logits, int M, int E, int topk,
+                                                     int32_t* __restrict__ idx, float* __restrict__ w,
+                                                     int32_t* __restrict__ src_rows, int32_t* __restrict__ slot_of,
+                                                     int32_t* __restrict__ offsets) {
+  __shared__ unsigned char es[kRouteMaxAssign];  // expert of each assignment (E <= 64)
+  __shared__ int base[MAX_E];                    // per expert: first slot of the current chunk
+  __shared__ int wcnt[16][MAX_E];                // per wave, per expert: assignments in the chunk
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = M * topk;
+  if (tid < MAX_E) base[tid] = 0;
+  __syncthreads();
+  for (int m = tid; m < M; m += 1024) {
+    float l[MAX_E];
+    for (int e = 0; e < E; ++e) l[e] = bf2f(logits[(size_t)m * E + e]);
+    int sel[MAX_K];
+    float val[MAX_K];
+    for (int j = 0; j < topk; ++j) {
+      int best = -1;
+      float bv = -INFINITY;
+      for (int e = 0; e < E; ++e) {
+        bool taken = false;
+        for (int q = 0; q < j; ++q) taken |= (sel[q] == e);
+        if (!taken && (best < 0 || l[e] > bv)) {
+          best = e;
+          bv = l[e];
+        }
+      }
+      sel[j] = best;
+      val[j] = bv;
+    }
+    float mx = val[0], sum = 0.f;
+    for (int j = 0; j < topk; ++j) {
+      val[j] = __expf(val[j] - mx);
+      sum += val[j];
+    }
+    for (int j = 0; j < topk; ++j) {
+      idx[m * topk + j] = sel[j];
+      w[m * topk + j] = val[j] / sum;
+      es[m * topk + j] = (unsigned char)sel[j];
+      atomicAdd(&base[sel[j]], 1);  // per-expert totals (order-free)
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {  // exclusive scan of the E <= 64 totals -> offsets, first slots
+    const int c = lane < E ? base[lane] : 0;
+    int x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane < E) {
+      offsets[lane] = x - c;
+      base[lane] = x - c;
+    }
+    if (lane == 63) offsets[E] = x;
+  }
+  __syncthreads();
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int i = c0 + tid;
+    const int e = i < n ? (int)es[i] : -1;
+    int rank = 0;
+    for (int q = 0; q < E; ++q) {
+      const unsigned long long b = __ballot(e == q);
+      if (lane == 0) wcnt[wave][q] = __popcll(b);
+      if (e == q) rank = __popcll(b & ((1ull << lane) - 1ull));
+    }
+    __syncthreads();
+    if (e >= 0) {
+      int slot = base[e] + rank;
+      for (int v = 0; v < wave; ++v) slot += wcnt[v][e];
+      src_rows[slot] = i / topk;
+      slot_of[i] = slot;
+    }
+    __syncthreads();
+    if (tid < E) {
+      int t = 0;
+      for (int v = 0; v < 16; ++v) t += wcnt[v][tid];
+      base[tid] += t;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void permute_kernel(const bf16* __restrict__ x, const int32_t* __restrict__ src,
                                                       bf16* __restrict__ out, int rows, int H) {
   const int lane = threadIdx.x & 63;
@@ -127,41 +217,48 @@ __global__ __launch_bounds__(256) void combine_kernel(const bf16* __restrict__ e
 // y[m] = r[m] + sum_j w[m,j] * E_{e}[slot[m,j] - off[e]],  e = idx[m,j]
 // Expert outputs are COMPACT: expert e's node wrote its routed rows (expert-sorted order)
 // to rows 0..count_e-1 of its own [M][H] buffer, wherever that buffer lives (a local arena
-// view or an xGMI receive buffer). One wave per token row, 16-B chunks per lane.
+// view or an xGMI receive buffer). One workgroup per token row: the routing words are
+// block-uniform (scalar loads), and each thread issues all k + 1 of its 16-B loads before the
+// arithmetic, so a 4096-wide row is 2 load batches per thread (a wave per row took 8 dependent
+// rounds: 15 us per Mixtral layer at 1 TB/s).
 __global__ __launch_bounds__(256) void gather_combine_kernel(const unsigned long long* __restrict__ eo_ptrs,
                                                              const int32_t* __restrict__ idx,
                                                              const int32_t* __restrict__ slot_of,
                                                              const int32_t* __restrict__ off,
                                                              const float* __restrict__ w, const bf16* __restrict__ r,
                                                              bf16* __restrict__ y, int M, int topk, int H, int E) {
-  const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (m >= M) return;
-  const bf16x8* src[8];
-  float g[8];
-  const int kk = topk < 8 ? topk : 8;
-  for (int j = 0; j < kk; ++j) {
+  const int m = blockIdx.x;
+  const bf16x8* src[MAX_K];
+  float g[MAX_K];
+  const int kk = topk < MAX_K ? topk : MAX_K;
+#pragma unroll
+  for (int j = 0; j < MAX_K; ++j) {
+    src[j] = nullptr;
+    g[j] = 0.f;
+    if (j >= kk) continue;
     const int e = idx[m * topk + j];
+    if (e < 0 || e >= E) continue;
     const int row = slot_of[m * topk + j] - off[e];
-    src[j] = (e >= 0 && e < E) ? reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(eo_ptrs[e]) +
-                                                                   (size_t)row * H)
-                               : nullptr;
+    src[j] = reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(eo_ptrs[e]) + (size_t)row * H);
     g[j] = w[m * topk + j];
   }
   bf16x8* yo = reinterpret_cast<bf16x8*>(y + (size_t)m * H);
   const bf16x8* ro = r ? reinterpret_cast<const bf16x8*>(r + (size_t)m * H) : nullptr;
-  for (int c = lane; c < H / 8; c += 64) {
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (ro) {
-      const bf16x8 v = ro[c];
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    bf16x8 v[MAX_K];
+    bf16x8 rv = {};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] = bf2f(v[e]);
-    }
-    for (int j = 0; j < kk; ++j) {
+    for (int j = 0; j < MAX_K; ++j)
+      if (src[j]) v[j] = src[j][c];
+    if (ro) rv = ro[c];
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = ro ? bf2f(rv[e]) : 0.f;
+#pragma unroll
+    for (int j = 0; j < MAX_K; ++j) {
       if (!src[j]) continue;
-      const bf16x8 v = src[j][c];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += g[j] * bf2f(v[e]);
+      for (int e = 0; e < 8; ++e) acc[e] += g[j] * bf2f(v[j][e]);
     }
     bf16x8 o;
 #pragma unroll
@@ -175,7 +272,7 @@ __global__ __launch_bounds__(256) void gather_combine_kernel(const unsigned long
 void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t* idx, const int32_t* slot_of,
                                const int32_t* off, const float* w, const void* r, void* y, int M, int topk, int H,
                                int E, hipStream_t s) {
-  hipLaunchKernelGGL(gather_combine_kernel, dim3((M + 3) / 4), dim3(256), 0, s, eo_ptrs, idx, slot_of, off, w,
+  hipLaunchKernelGGL(gather_combine_kernel, dim3(M), dim3(256), 0, s, eo_ptrs, idx, slot_of, off, w,
                      (const bf16*)r, (bf16*)y, M, topk, H, E);
 }
 
@@ -189,6 +286,12 @@ void launch_moe_align(const int32_t* topk_idx, int M, int topk, int E, int32_t* 
                       int32_t* offsets, hipStream_t s) {
   hipLaunchKernelGGL(align_kernel, dim3(1), dim3(1024), 0, s, topk_idx, M * topk, E, src_rows, slot_of, offsets,
                      topk);
+}
+
+void launch_moe_route(const void* logits, int M, int E, int topk, int32_t* topk_idx, float* topk_w,
+                      int32_t* src_rows, int32_t* slot_of, int32_t* offsets, hipStream_t s) {
+  hipLaunchKernelGGL(route_kernel, dim3(1), dim3(1024), 0, s, (const bf16*)logits, M, E, topk, topk_idx, topk_w,
+                     src_rows, slot_of, offsets);
 }
 
 void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int rows, int H, hipStream_t s) {

@@ -341,6 +341,22 @@ std::vector<at::Tensor> moe_align(const at::Tensor& idx, int64_t E) {
   return {src, slot, off};
 }
 
+// router + align in ONE launch (route_kernel): idx, w, src_rows, slot_of, offsets
+std::vector<at::Tensor> moe_route(const at::Tensor& logits, int64_t topk) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits must be contiguous [M][E]");
+  const int64_t M = logits.size(0), E = logits.size(1);
+  TORCH_CHECK(E <= 64 && topk >= 1 && topk <= 8 && topk <= E, "router supports E <= 64, 1 <= topk <= min(8, E)");
+  TORCH_CHECK(M * topk <= kRouteMaxAssign, "fused routing holds at most ", kRouteMaxAssign, " assignments");
+  auto iopt = logits.options().dtype(at::kInt);
+  auto idx = at::empty({M, topk}, iopt);
+  auto w = at::empty({M, topk}, logits.options().dtype(at::kFloat));
+  auto src = at::empty({M * topk}, iopt), slot = at::empty({M * topk}, iopt), off = at::empty({E + 1}, iopt);
+  launch_moe_route(logits.data_ptr(), (int)M, (int)E, (int)topk, idx.data_ptr<int32_t>(), w.data_ptr<float>(),
+                   src.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), off.data_ptr<int32_t>(), cur_stream());
+  return {idx, w, src, slot, off};
+}
+
 at::Tensor moe_permute(const at::Tensor& x, const at::Tensor& src_rows) {
   check_bf16(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "x must be contiguous [M][H]");
@@ -392,12 +408,21 @@ at::Tensor grouped_gemm(const at::Tensor& X, const at::Tensor& offsets, const at
 // rows' own positions, or (outs + out_ptrs) E compact outputs, rows 0..min(count, cap)-1 each.
 void gemm_grouped(const at::Tensor& x, const std::vector<at::Tensor>& weights, const at::Tensor& w_ptrs,
                   const at::Tensor& offsets, int64_t act, const c10::optional<at::Tensor>& out,
-                  const std::vector<at::Tensor>& outs, const c10::optional<at::Tensor>& out_ptrs, int64_t config) {
+                  const std::vector<at::Tensor>& outs, const c10::optional<at::Tensor>& out_ptrs, int64_t config,
+                  const c10::optional<at::Tensor>& a_rows) {
   const int64_t E = (int64_t)weights.size();
   check_bf16(x, "x");
   check_rows(x, "x");
   TORCH_CHECK(E > 0, "at least one expert");
-  const int64_t R = x.size(0), K = x.size(1), N = weights[0].size(0);
+  // a_rows (int32 [R], values < x.size(0)): x is the token matrix and sorted row r reads token
+  // a_rows[r] (the MoE permute folded into the GEMM's DMA source addresses)
+  const int* arp = nullptr;
+  if (a_rows.has_value()) {
+    TORCH_CHECK(a_rows->is_cuda() && a_rows->scalar_type() == at::kInt && a_rows->is_contiguous(),
+                "a_rows: contiguous int32 on the GPU");
+    arp = a_rows->data_ptr<int32_t>();
+  }
+  const int64_t R = a_rows.has_value() ? a_rows->numel() : x.size(0), K = x.size(1), N = weights[0].size(0);
   const bool sw = act == kActSwiglu;
   const int64_t NO = sw ? N / 2 : N;
   for (const auto& w : weights) {
@@ -443,7 +468,8 @@ void gemm_grouped(const at::Tensor& x, const std::vector<at::Tensor>& weights, c
     g.ldc = (int)out->stride(0);
   }
   launch_gemm_glds_grouped(g, cfg, (int)E, offsets.data_ptr<int32_t>(),
-                           reinterpret_cast<const unsigned long long*>(w_ptrs.data_ptr<int64_t>()), cp, cur_stream());
+                           reinterpret_cast<const unsigned long long*>(w_ptrs.data_ptr<int64_t>()), cp, cur_stream(),
+                           arp);
 }
 
 // experts: list of E compact [rows][H] bf16 outputs; ptrs: int64 [E] device tensor holding
@@ -543,11 +569,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_router", &moe_router);
   m.def("moe_gather_combine", &moe_gather_combine);
   m.def("moe_align", &moe_align);
+  m.def("moe_route", &moe_route);
   m.def("moe_permute", &moe_permute);
   m.def("moe_combine", &moe_combine, py::arg("expert_out"), py::arg("slot_of"), py::arg("weights"),
         py::arg("range") = py::none(), py::arg("out") = py::none());
   m.def("grouped_gemm", &grouped_gemm, py::arg("X"), py::arg("offsets"), py::arg("W"), py::arg("act") = 0);
   m.def("gemm_grouped", &gemm_grouped, py::arg("x"), py::arg("weights"), py::arg("w_ptrs"), py::arg("offsets"),
         py::arg("act") = 0, py::arg("out") = py::none(), py::arg("outs") = std::vector<at::Tensor>{},
-        py::arg("out_ptrs") = py::none(), py::arg("config") = -1);
+        py::arg("out_ptrs") = py::none(), py::arg("config") = -1, py::arg("a_rows") = py::none());
 }

@@ -62,9 +62,11 @@ def _stale(out: str, srcs) -> bool:
     return _newer(out, srcs)
 
 
-def _record(out: str, srcs) -> None:
+def _record(out: str, srcs, digest: str = None) -> None:
+    """Stamp ``out`` with the sources' digest — taken BEFORE the compile started (``digest``),
+    so a source edited while the compiler ran leaves the output stale, not falsely fresh."""
     with open(out + ".srchash.tmp", "w") as f:
-        f.write(_digest(srcs))
+        f.write(digest or _digest(srcs))
     os.replace(out + ".srchash.tmp", out + ".srchash")
 
 
@@ -115,6 +117,7 @@ def build_core(force: bool = False, verbose: bool = False) -> str:
 
 
 def _build_core(srcs, hdrs, pybind11, verbose) -> str:
+    d0 = _digest(srcs + hdrs)
     cmd = [
         os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
         "-Wall", "-Wno-sign-compare",
@@ -123,7 +126,7 @@ def _build_core(srcs, hdrs, pybind11, verbose) -> str:
     ]
     _run(cmd, verbose)
     os.replace(CORE_SO + ".tmp", CORE_SO)
-    _record(CORE_SO, srcs + hdrs)
+    _record(CORE_SO, srcs + hdrs, d0)
     return CORE_SO
 
 
@@ -156,6 +159,7 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
 
 def _build_ops(kern, hdrs, binding, force, verbose, jobs) -> str:
     os.makedirs(BUILD_DIR, exist_ok=True)
+    d0 = _digest(kern + hdrs + [binding])
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     inc, defs, libs = _torch_flags()
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
@@ -167,20 +171,26 @@ def _build_ops(kern, hdrs, binding, force, verbose, jobs) -> str:
     per_file = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
     def compile_kernel(src):
+        # objects are stamped by content too (an mtime check misses an edit made while an
+        # earlier compile of the same file was running)
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
-        if force or _newer(obj, [src] + hdrs):
+        if force or _stale(obj, [src] + hdrs):
+            d = _digest([src] + hdrs)
             _run([hipcc, *common, *per_file.get(os.path.basename(src), []), "-c", src, "-o", obj], verbose)
+            _record(obj, [src] + hdrs, d)
         return obj
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(compile_kernel, kern))
     bobj = os.path.join(BUILD_DIR, "ops_binding.o")
-    if force or _newer(bobj, [binding] + hdrs):
+    if force or _stale(bobj, [binding] + hdrs):
+        db = _digest([binding] + hdrs)
         _run([hipcc, "-O2", "-std=c++17", "-fPIC", *inc, *defs, f"-I{os.path.join(CSRC, 'kernels')}", f"-I{ROCM}/include",
               "-x", "c++", "-c", binding, "-o", bobj], verbose)
+        _record(bobj, [binding] + hdrs, db)
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, bobj, *libs, "-o", OPS_SO + ".tmp"], verbose)
     os.replace(OPS_SO + ".tmp", OPS_SO)
-    _record(OPS_SO, kern + hdrs + [binding])
+    _record(OPS_SO, kern + hdrs + [binding], d0)
     return OPS_SO
 
 

@@ -403,6 +403,15 @@ def moe_align(topk_idx, n_experts):
     return (order // k).to(torch.int32), slot_of.to(torch.int32), offsets.to(torch.int32)
 
 
+def moe_route(logits, topk, n_experts):
+    """Router + align of one MoE layer: (idx, gate, src_rows, slot_of, offsets). GPU: ONE
+    workgroup launch (route_kernel) with exactly the outputs of moe_router + moe_align."""
+    if _gpu(logits) and logits.shape[0] * topk <= 16384 and logits.shape[1] == n_experts:
+        return tuple(ext().moe_route(logits.contiguous(), int(topk)))
+    idx, gate = moe_router(logits, topk)
+    return (idx, gate) + moe_align(idx, n_experts)
+
+
 def moe_permute(x, src_rows):
     if _gpu(x):
         return ext().moe_permute(x.contiguous(), src_rows)
@@ -466,22 +475,26 @@ def moe_expert(h, router_logits, w_gate_up, w_down, expert, n_experts, top_k, ou
     return moe_combine(y, slot, gate, rng, out)
 
 
-def gemm_grouped(x, weights, offsets, act=None, out=None, outs=None, w_ptrs=None, out_ptrs=None, rows_hint=None):
+def gemm_grouped(x, weights, offsets, act=None, out=None, outs=None, w_ptrs=None, out_ptrs=None, rows_hint=None,
+                 a_rows=None):
     """Every expert of an MoE layer in ONE GEMM launch (GPU: LDS-DMA kernel, grid = experts x
     column tiles). Expert e multiplies the expert-sorted rows [offsets[e], offsets[e+1]) of
     ``x`` by ``weights[e]`` ([N][K]; SwiGLU: gate/up-interleaved, N/2 outputs) and writes them
     at the same rows of ``out``, or compactly to rows 0.. of ``outs[e]`` (at most its row
-    count). ``w_ptrs`` / ``out_ptrs``: cached int64 device tensors of the tensors' addresses
-    (built here when omitted — pass cached ones inside a hipGraph)."""
+    count). ``a_rows`` (int32 [R]): ``x`` is the TOKEN matrix and sorted row r is token
+    ``a_rows[r]`` (the permute happens in the kernel's loads). ``w_ptrs`` / ``out_ptrs``:
+    cached int64 device tensors of the tensors' addresses (built here when omitted — pass
+    cached ones inside a hipGraph)."""
     a = ACT[act] if not isinstance(act, int) else act
     E = len(weights)
     N, K = weights[0].shape
+    R = x.shape[0] if a_rows is None else a_rows.numel()
     if _gpu(x):
         if w_ptrs is None:
             w_ptrs = torch.tensor([w.data_ptr() for w in weights], dtype=torch.int64, device=x.device)
         if outs is not None and out_ptrs is None:
             out_ptrs = torch.tensor([o.data_ptr() for o in outs], dtype=torch.int64, device=x.device)
-        hint = rows_hint or max(1, x.shape[0] // E)
+        hint = rows_hint or max(1, R // E)
         # grouped variants ("g"): tuned as GROUPS experts of `hint` rows in one launch; until
         # tuned, the per-expert row-range choice ("r") stands in
         cfg, _ = tuning.lookup_fused(hint, N, K, ("s" if a == SWIGLU else "") + "g")
@@ -490,8 +503,10 @@ def gemm_grouped(x, weights, offsets, act=None, out=None, outs=None, w_ptrs=None
         if cfg >= tuning.REGSTAGE:
             cfg = -1
         ext().gemm_grouped(x, list(weights), w_ptrs, offsets, a, out, list(outs) if outs is not None else [],
-                           out_ptrs, cfg)
+                           out_ptrs, cfg, a_rows)
         return out if outs is None else outs
+    if a_rows is not None:
+        x = x[a_rows.long()]
     off = [int(v) for v in offsets.tolist()]
     for e in range(E):
         r0, r1 = off[e], off[e + 1]

@@ -80,6 +80,9 @@ STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
 PREFETCH = os.environ.get("DLS_PREFETCH", "auto")
 # one grouped launch pair per MoE layer for the experts co-located on this rank (GPU)
 MOE_BATCH = os.environ.get("DLS_MOE_BATCH", "1") != "0"
+# MoE routing in one launch (router + align, ops.moe_route) and the grouped gate/up GEMM
+# gathering its token rows itself (no permute kernel); 0 restores the separate launches
+MOE_FUSED_ROUTE = os.environ.get("DLS_MOE_FUSED_ROUTE", "1") != "0"
 # parameter refills: "pull" = the host-pull kernel reads the pinned group image over the host
 # link (benchmarks/bench_h2d.py: 50-56 GB/s from 2.4 MB up, 32 GB/s at 0.25 MB, on 32-64
 # workgroups), "dma" = hipMemcpyAsync (42-51 GB/s, 15 GB/s at 0.25 MB)
@@ -260,9 +263,13 @@ class DAGExecutor:
         tasks = sorted((self.tasks[self.prog.instrs[m].group[0]] for m in members), key=lambda t: t.op.attrs["expert"])
         a = tasks[0].op.attrs
         E, K = a["n_experts"], a["top_k"]
-        off = self._moe_route(tasks[0].op.inputs[1], E, K)[4]
-        xp = self._moe_permuted(tasks[0].op.inputs[0], tasks[0].op.inputs[1], E, K)
-        R, F = xp.shape[0], a["ffn"]
+        route = self._moe_route(tasks[0].op.inputs[1], E, K)
+        off, src = route[4], route[2]
+        if MOE_FUSED_ROUTE:  # tokens: the gate/up GEMM gathers its rows by src
+            x, rows = self._flat(self._x(tasks[0].op.inputs[0])), src
+        else:
+            x, rows = self._moe_permuted(tasks[0].op.inputs[0], tasks[0].op.inputs[1], E, K), None
+        R, F = src.numel(), a["ffn"]
         w13 = [self._prep(t.op.weights["w_gate_up"], None, None, interleave=True)[0] for t in tasks]
         w2 = [self._w(t.op.weights["w_down"]) for t in tasks]
         outs = [self._flat(self._views[t.id]) for t in tasks]
@@ -273,7 +280,7 @@ class DAGExecutor:
             cached = (ptrs, mk(w13), mk(w2), mk(outs))
             self._moe_bufs[i] = cached
         hbuf = self._scratch("moe_h", (R, F))
-        ops.gemm_grouped(xp, w13, off, act="swiglu", out=hbuf, w_ptrs=cached[1], rows_hint=max(1, R // E))
+        ops.gemm_grouped(x, w13, off, act="swiglu", out=hbuf, w_ptrs=cached[1], rows_hint=max(1, R // E), a_rows=rows)
         ops.gemm_grouped(hbuf, w2, off, outs=outs, w_ptrs=cached[2], out_ptrs=cached[3], rows_hint=max(1, R // E))
 
     def _plan_prefetch(self) -> None:
@@ -645,9 +652,12 @@ class DAGExecutor:
         key = ("route", r_name)
         r = self._moe_memo.get(key)
         if r is None:
-            idx, gate = ops.moe_router(self._flat(self._x(r_name)), top_k)
-            src, slot, off = ops.moe_align(idx, E)
-            r = (idx, gate, src, slot, off)
+            logits = self._flat(self._x(r_name))
+            if MOE_FUSED_ROUTE:
+                r = ops.moe_route(logits, top_k, E)  # one launch on GPU
+            else:
+                idx, gate = ops.moe_router(logits, top_k)
+                r = (idx, gate) + tuple(ops.moe_align(idx, E))
             self._moe_memo[key] = r
         return r
 

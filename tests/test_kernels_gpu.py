@@ -332,6 +332,49 @@ def test_gemm_grouped_experts(config):
         assert (outs[e][min(r1 - r0, cap):].cpu().float() == 7.0).all(), "rows past the expert's count were written"
 
 
+@pytest.mark.parametrize("M,E,k", [(300, 8, 2), (512, 8, 2), (1500, 8, 2), (200, 64, 8), (777, 16, 1)])
+def test_moe_route_fused_equals_router_align(M, E, k):
+    """The one-workgroup route kernel returns exactly what moe_router + moe_align return."""
+    g = torch.Generator().manual_seed(M + E)
+    logits = torch.stack([torch.randperm(E, generator=g) for _ in range(M)]).float().mul(0.25)
+    logits = (logits + 0.01 * torch.randn(M, E, generator=g)).to(torch.bfloat16).to(DEV)
+    idx, w = ops.moe_router(logits, k)
+    src, slot, off = ops.moe_align(idx, E)
+    fi, fw, fs, fsl, fo = ops.ext().moe_route(logits, k)
+    torch.cuda.synchronize()
+    assert torch.equal(fi, idx) and torch.equal(fw, w)
+    assert torch.equal(fo, off) and torch.equal(fs, src) and torch.equal(fsl, slot)
+
+
+@pytest.mark.parametrize("config", [-1, 3, 17, 30, 31, 33])
+def test_gemm_grouped_gathered_rows(config):
+    """Gate/up grouped GEMM reading its expert-sorted rows straight from the token matrix
+    (a_rows = src rows of the routing) equals the permute-then-GEMM path."""
+    M, E, k, H, F = 300, 8, 2, 256, 384
+    g = torch.Generator().manual_seed(5)
+    logits = torch.stack([torch.randperm(E, generator=g) for _ in range(M)]).float().to(torch.bfloat16).to(DEV)
+    idx, gate, src, slot, off = ops.moe_route(logits, k, E)
+    x = _rand(M, H, seed=31)
+    w13 = [ops.interleave_gate_up(_rand(2 * F, H, scale=0.05, seed=40 + e)) for e in range(E)]
+    R = src.numel()
+    h_ref = torch.zeros(R, F, dtype=torch.bfloat16, device=DEV)
+    h = torch.full((R, F), 3.0, dtype=torch.bfloat16, device=DEV)
+    ops.gemm_grouped(ops.moe_permute(x, src), w13, off, act="swiglu", out=h_ref)
+    ops.gemm_grouped(x, w13, off, act="swiglu", out=h, a_rows=src)
+    ext = ops.ext()
+    wp = torch.tensor([w.data_ptr() for w in w13], dtype=torch.int64, device=DEV)
+    h2 = torch.full((R, F), 3.0, dtype=torch.bfloat16, device=DEV)
+    ext.gemm_grouped(x, w13, wp, off, 4, h2, [], None, config, src)
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_ref)
+    xs = x.cpu()[src.cpu().long()]
+    o = off.tolist()
+    for e in range(E):
+        r0, r1 = o[e], o[e + 1]
+        if r1 > r0:
+            _close(h2[r0:r1].cpu(), ops.ref_linear(xs[r0:r1], w13[e].cpu(), act="swiglu").float(), 2e-2)
+
+
 def test_moe_gather_combine():
     M, E, k, H = 300, 8, 2, 256
     g = torch.Generator().manual_seed(90)

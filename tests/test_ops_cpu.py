@@ -24,3 +24,22 @@ def test_ranged_linear_cpu_only_touches_range():
     ops.linear(x, w, out=out, rows=torch.tensor([3, 6], dtype=torch.int32))
     assert (out[:3] == 7).all() and (out[6:] == 7).all()
     assert torch.allclose(out[3:6], x[3:6] @ w.t(), atol=1e-5)
+
+
+def test_moe_route_and_gathered_grouped_gemm_cpu():
+    """CPU fallbacks: moe_route == moe_router + moe_align, and a grouped GEMM reading its
+    expert-sorted rows through a_rows equals the permute-then-GEMM path."""
+    M, E, k, H, F = 40, 4, 2, 16, 8
+    g = torch.Generator().manual_seed(3)
+    logits = torch.stack([torch.randperm(E, generator=g) for _ in range(M)]).float().to(torch.bfloat16)
+    idx, gate, src, slot, off = ops.moe_route(logits, k, E)
+    ri, rg = ops.moe_router(logits, k)
+    rs, rsl, ro = ops.moe_align(ri, E)
+    assert torch.equal(idx, ri) and torch.equal(gate, rg)
+    assert torch.equal(src, rs) and torch.equal(slot, rsl) and torch.equal(off, ro)
+    x = torch.randn(M, H, generator=g).to(torch.bfloat16)
+    ws = [(torch.randn(F, H, generator=g) * 0.1).to(torch.bfloat16) for _ in range(E)]
+    R = src.numel()
+    a = ops.gemm_grouped(ops.moe_permute(x, src), ws, off, out=torch.zeros(R, F, dtype=torch.bfloat16))
+    b = ops.gemm_grouped(x, ws, off, out=torch.zeros(R, F, dtype=torch.bfloat16), a_rows=src)
+    assert torch.equal(a, b)
