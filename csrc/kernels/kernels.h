@@ -129,6 +129,11 @@ void launch_moe_align(const int32_t* topk_idx, int M, int topk, int E, int32_t* 
 constexpr int kRouteMaxAssign = 16384;
 void launch_moe_route(const void* logits, int M, int E, int topk, int32_t* topk_idx, float* topk_w,
                       int32_t* src_rows, int32_t* slot_of, int32_t* offsets, hipStream_t s);
+// router GEMM (logits = x Wg^T, bf16) + routing in one launch; false (nothing launched) when
+// the shape is outside its limits (E * H <= 32768, M * max(k, E) <= kRouteMaxAssign, E even, E <= 16)
+bool launch_moe_gate_route(const void* x, int ldx, const void* wg, int M, int H, int E, int topk, void* logits,
+                           int* ticket, int32_t* topk_idx, float* topk_w, int32_t* src_rows, int32_t* slot_of,
+                           int32_t* offsets, hipStream_t s);
 void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int rows, int H, hipStream_t s);
 void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
                         int topk, int H, const int32_t* range, hipStream_t s);

@@ -14,38 +14,57 @@ namespace {
 constexpr int MAX_E = 64;
 constexpr int MAX_K = 8;
 
+// top-k of one token's E logits: ties go to the lower expert index; gates = softmax over the
+// selected logits (== the full softmax renormalised over the top-k). The j loop is unrolled to
+// MAX_K so sel / val stay in registers, and taken experts are a bitmask: a runtime-indexed
+// float[E] / int[k] lived in scratch memory (272 B per lane).
+__device__ __forceinline__ void select_topk(const bf16* __restrict__ lrow, int E, int topk, int (&sel)[MAX_K],
+                                            float (&val)[MAX_K]) {
+  unsigned long long taken = 0ull;
+#pragma unroll
+  for (int j = 0; j < MAX_K; ++j) {
+    sel[j] = 0;
+    val[j] = 0.f;
+    if (j >= topk) continue;
+    int best = -1;
+    float bv = -INFINITY;
+    for (int e = 0; e < E; ++e) {
+      const float le = bf2f(lrow[e]);
+      if (!((taken >> e) & 1ull) && (best < 0 || le > bv)) {
+        best = e;
+        bv = le;
+      }
+    }
+    taken |= 1ull << best;
+    sel[j] = best;
+    val[j] = bv;
+  }
+  const float mx = val[0];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAX_K; ++j)
+    if (j < topk) {
+      val[j] = __expf(val[j] - mx);
+      s += val[j];
+    }
+#pragma unroll
+  for (int j = 0; j < MAX_K; ++j)
+    if (j < topk) val[j] /= s;
+}
+
 __global__ __launch_bounds__(256) void router_kernel(const bf16* __restrict__ logits, int M, int E, int topk,
                                                      int32_t* __restrict__ idx, float* __restrict__ w) {
   const int m = blockIdx.x * 256 + threadIdx.x;
   if (m >= M) return;
-  float l[MAX_E];
-  for (int e = 0; e < E; ++e) l[e] = bf2f(logits[(size_t)m * E + e]);
   int sel[MAX_K];
   float val[MAX_K];
-  for (int j = 0; j < topk; ++j) {
-    int best = -1;
-    float bv = -INFINITY;
-    for (int e = 0; e < E; ++e) {
-      bool taken = false;
-      for (int q = 0; q < j; ++q) taken |= (sel[q] == e);
-      if (!taken && (best < 0 || l[e] > bv)) {
-        best = e;
-        bv = l[e];
-      }
+  select_topk(logits + (size_t)m * E, E, topk, sel, val);
+#pragma unroll
+  for (int j = 0; j < MAX_K; ++j)
+    if (j < topk) {
+      idx[m * topk + j] = sel[j];
+      w[m * topk + j] = val[j];
     }
-    sel[j] = best;
-    val[j] = bv;
-  }
-  // softmax restricted to the selected experts (== full softmax renormalised over top-k)
-  float mx = val[0], s = 0.f;
-  for (int j = 0; j < topk; ++j) {
-    val[j] = __expf(val[j] - mx);
-    s += val[j];
-  }
-  for (int j = 0; j < topk; ++j) {
-    idx[m * topk + j] = sel[j];
-    w[m * topk + j] = val[j] / s;
-  }
 }
 
 // single workgroup, 1024 threads: per expert a block-wide exclusive scan of "routed to e"
@@ -87,52 +106,43 @@ __global__ __launch_bounds__(1024) void align_kernel(const int32_t* __restrict__
   if (tid == 0) offsets[E] = base_s;
 }
 
-// Router + align fused into ONE workgroup: per token the top-k experts (router_kernel's
-// selection: ties go to the lower expert index) and renormalised gates, then the counting sort
-// of the M*k assignments by expert in align_kernel's order (stable in assignment index i =
-// m*k + j), so the outputs equal the two-launch pair exactly. The experts of the assignments
-// stay in LDS; ranks within a 64-assignment wave come from one ballot per expert, wave
-// prefixes from an LDS table: two barriers per 1024 assignments instead of three per expert.
-__global__ __launch_bounds__(1024) void route_kernel(const bf16* __restrict__ logits, int M, int E, int topk,
-                                                     int32_t* __restrict__ idx, float* __restrict__ w,
-                                                     int32_t* __restrict__ src_rows, int32_t* __restrict__ slot_of,
-                                                     int32_t* __restrict__ offsets) {
-  __shared__ unsigned char es[kRouteMaxAssign];  // expert of each assignment (E <= 64)
-  __shared__ int base[MAX_E];                    // per expert: first slot of the current chunk
-  __shared__ int wcnt[16][MAX_E];                // per wave, per expert: assignments in the chunk
+// Router + align for one MoE layer inside ONE workgroup of NT threads: per token the top-k
+// experts and renormalised gates (select_topk), then the counting sort of the M*k assignments
+// by expert in align_kernel's order (stable in assignment index i = m*k + j), so the outputs
+// equal the router_kernel + align_kernel pair exactly. The experts of the assignments stay in
+// LDS; ranks within a 64-assignment wave come from one ballot per expert, wave prefixes from an
+// LDS table: two barriers per NT assignments instead of three per expert.
+template <int NT>
+__device__ __forceinline__ void route_block(const bf16* __restrict__ logits, int M, int E, int topk,
+                                            int32_t* __restrict__ idx, float* __restrict__ w,
+                                            int32_t* __restrict__ src_rows, int32_t* __restrict__ slot_of,
+                                            int32_t* __restrict__ offsets, unsigned char* es, int* base,
+                                            int (*wcnt)[MAX_E]) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = M * topk;
   if (tid < MAX_E) base[tid] = 0;
   __syncthreads();
-  for (int m = tid; m < M; m += 1024) {
-    float l[MAX_E];
-    for (int e = 0; e < E; ++e) l[e] = bf2f(logits[(size_t)m * E + e]);
+  for (int m = tid; m < M; m += NT) {
     int sel[MAX_K];
     float val[MAX_K];
-    for (int j = 0; j < topk; ++j) {
-      int best = -1;
-      float bv = -INFINITY;
-      for (int e = 0; e < E; ++e) {
-        bool taken = false;
-        for (int q = 0; q < j; ++q) taken |= (sel[q] == e);
-        if (!taken && (best < 0 || l[e] > bv)) {
-          best = e;
-          bv = l[e];
-        }
+    select_topk(logits + (size_t)m * E, E, topk, sel, val);
+#pragma unroll
+    for (int j = 0; j < MAX_K; ++j)
+      if (j < topk) {
+        idx[m * topk + j] = sel[j];
+        w[m * topk + j] = val[j];
+        es[m * topk + j] = (unsigned char)sel[j];
       }
-      sel[j] = best;
-      val[j] = bv;
-    }
-    float mx = val[0], sum = 0.f;
-    for (int j = 0; j < topk; ++j) {
-      val[j] = __expf(val[j] - mx);
-      sum += val[j];
-    }
-    for (int j = 0; j < topk; ++j) {
-      idx[m * topk + j] = sel[j];
-      w[m * topk + j] = val[j] / sum;
-      es[m * topk + j] = (unsigned char)sel[j];
-      atomicAdd(&base[sel[j]], 1);  // per-expert totals (order-free)
+  }
+  __syncthreads();
+  // per-expert totals: one ballot per expert per wave, one LDS add per (wave, expert) — an
+  // LDS atomic per assignment piles 128 same-address atomics on each expert's counter
+  for (int c0 = 0; c0 < n; c0 += NT) {
+    const int i = c0 + tid;
+    const int e = i < n ? (int)es[i] : -1;
+    for (int q = 0; q < E; ++q) {
+      const unsigned long long b = __ballot(e == q);
+      if (lane == 0 && b) atomicAdd(&base[q], __popcll(b));
     }
   }
   __syncthreads();
@@ -151,7 +161,7 @@ __global__ __launch_bounds__(1024) void route_kernel(const bf16* __restrict__ lo
     if (lane == 63) offsets[E] = x;
   }
   __syncthreads();
-  for (int c0 = 0; c0 < n; c0 += 1024) {
+  for (int c0 = 0; c0 < n; c0 += NT) {
     const int i = c0 + tid;
     const int e = i < n ? (int)es[i] : -1;
     int rank = 0;
@@ -170,11 +180,111 @@ __global__ __launch_bounds__(1024) void route_kernel(const bf16* __restrict__ lo
     __syncthreads();
     if (tid < E) {
       int t = 0;
-      for (int v = 0; v < 16; ++v) t += wcnt[v][tid];
+      for (int v = 0; v < NT / 64; ++v) t += wcnt[v][tid];
       base[tid] += t;
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(1024) void route_kernel(const bf16* __restrict__ logits, int M, int E, int topk,
+                                                     int32_t* __restrict__ idx, float* __restrict__ w,
+                                                     int32_t* __restrict__ src_rows, int32_t* __restrict__ slot_of,
+                                                     int32_t* __restrict__ offsets) {
+  __shared__ unsigned char es[kRouteMaxAssign];  // expert of each assignment (E <= 64)
+  __shared__ int base[MAX_E];                    // per expert: first slot of the current chunk
+  __shared__ int wcnt[16][MAX_E];                // per wave, per expert: assignments in the chunk
+  route_block<1024>(logits, M, E, topk, idx, w, src_rows, slot_of, offsets, es, base, wcnt);
+}
+
+// Router GEMM + routing in ONE launch (replaces a split-K GEMM, its reduce and the route
+// kernel: 6.2 + 5.8 + 8.3 us per Mixtral layer). A workgroup of 8 waves takes GR_TOK tokens;
+// wave v computes the logits of token v / GR_EW for experts (v % GR_EW) * EPW .. + EPW - 1
+// straight from global memory (fp32 dot products over 16-B chunks, one wave reduction per
+// expert): M / GR_TOK workgroups cover the chip, each wave loads its x row and its weight
+// rows in one round trip. The logits are published with agent-scope (write-through) stores
+// and every workgroup draws a ticket; the LAST one routes every token from the published
+// logits (route_block) and resets the ticket. No workgroup waits on another, and nothing is
+// fenced (a device-scope fence writes back this XCD's whole L2: 36 us for the launch).
+constexpr int GR_WAVES = 8;
+constexpr int GR_XV = 8;  // 16-B x chunks per lane (H <= 8 * 64 * 8 = 4096)
+template <int EPW, int GR_EW>  // experts per wave, waves per token (EPW * GR_EW >= E)
+__global__ __launch_bounds__(64 * GR_WAVES) void gate_route_kernel(
+    const bf16* __restrict__ x, int ldx, const bf16* __restrict__ wg, int M, int H, int E, int topk,
+    bf16* __restrict__ logits, int* __restrict__ ticket, int32_t* __restrict__ idx, float* __restrict__ w,
+    int32_t* __restrict__ src_rows, int32_t* __restrict__ slot_of, int32_t* __restrict__ offsets) {
+  constexpr int NT = 64 * GR_WAVES, GR_TOK = GR_WAVES / GR_EW;
+  __shared__ unsigned char es[kRouteMaxAssign];
+  __shared__ unsigned int lg[kRouteMaxAssign / 2];  // the last block's copy of all logits (bf16 pairs)
+  __shared__ int base[MAX_E];
+  __shared__ int wcnt[GR_WAVES][MAX_E];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hv = H / 8;
+  const int m = blockIdx.x * GR_TOK + wave / GR_EW, e0 = (wave % GR_EW) * EPW;
+  if (m < M && e0 < E) {  // wave-uniform
+    // one round trip: the token row and this wave's weight rows (clamped, not guarded: a
+    // branch per load serialises them)
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)m * ldx);
+    bf16x8 xv[GR_XV], wv[EPW][GR_XV];
+#pragma unroll
+    for (int u = 0; u < GR_XV; ++u) xv[u] = xr[min(u * 64 + lane, hv - 1)];
+#pragma unroll
+    for (int k = 0; k < EPW; ++k) {
+      const bf16x8* wr = reinterpret_cast<const bf16x8*>(wg + (size_t)min(e0 + k, E - 1) * H);
+#pragma unroll
+      for (int u = 0; u < GR_XV; ++u) wv[k][u] = wr[min(u * 64 + lane, hv - 1)];
+    }
+    float acc[EPW];
+#pragma unroll
+    for (int k = 0; k < EPW; ++k) acc[k] = 0.f;
+    __builtin_amdgcn_sched_barrier(0);  // every load above is issued before the first use
+#pragma unroll
+    for (int u = 0; u < GR_XV; ++u) {
+      const bool in = u * 64 + lane < hv;  // a select, not a branch (a break sinks the loads)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xf = in ? bf2f(xv[u][q]) : 0.f;
+#pragma unroll
+        for (int k = 0; k < EPW; ++k) acc[k] += xf * bf2f(wv[k][u][q]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EPW; k += 2) {
+      if (e0 + k >= E) break;
+      const float t0 = wave_sum(acc[k]), t1 = wave_sum(acc[k + 1]);
+      if (lane == 0) {
+        const unsigned int pr = (unsigned int)__builtin_bit_cast(unsigned short, f2bf(t0)) |
+                                ((unsigned int)__builtin_bit_cast(unsigned short, f2bf(t1)) << 16);
+        __hip_atomic_store(reinterpret_cast<unsigned int*>(logits) + ((size_t)m * E + e0 + k) / 2, pr,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's logits stores are complete
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == (int)gridDim.x - 1;
+    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
+  __syncthreads();
+  if (!last) return;  // block-uniform
+  // agent-scope loads: the other blocks' logits come from memory, never from a stale cache line
+  const int nl = M * E / 2;
+  for (int i0 = 0; i0 < nl; i0 += NT * 8) {
+    unsigned int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = __hip_atomic_load(reinterpret_cast<const unsigned int*>(logits) + min(i0 + u * NT + tid, nl - 1),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u * NT + tid < nl) lg[i0 + u * NT + tid] = v[u];
+  }
+  __syncthreads();
+  route_block<NT>(reinterpret_cast<const bf16*>(lg), M, E, topk, idx, w, src_rows, slot_of, offsets, es, base,
+                  wcnt);
 }
 
 __global__ __launch_bounds__(256) void permute_kernel(const bf16* __restrict__ x, const int32_t* __restrict__ src,
@@ -292,6 +402,24 @@ void launch_moe_route(const void* logits, int M, int E, int topk, int32_t* topk_
                       int32_t* src_rows, int32_t* slot_of, int32_t* offsets, hipStream_t s) {
   hipLaunchKernelGGL(route_kernel, dim3(1), dim3(1024), 0, s, (const bf16*)logits, M, E, topk, topk_idx, topk_w,
                      src_rows, slot_of, offsets);
+}
+
+bool launch_moe_gate_route(const void* x, int ldx, const void* wg, int M, int H, int E, int topk, void* logits,
+                           int* ticket, int32_t* topk_idx, float* topk_w, int32_t* src_rows, int32_t* slot_of,
+                           int32_t* offsets, hipStream_t s) {
+  if (H > 64 * 8 * GR_XV || M * topk > kRouteMaxAssign || M * E > kRouteMaxAssign || E % 2 || H % 8 || E > 16 ||
+      ldx % 8)
+    return false;
+  // 2 experts per wave: E = 8 -> 4 waves per token, 2 tokens per workgroup (256 workgroups
+  // for a 512-token batch); E <= 16 -> 8 waves per token
+#define DLS_GR(EPW, EW)                                                                                           \
+  hipLaunchKernelGGL((gate_route_kernel<EPW, EW>), dim3((M + GR_WAVES / EW - 1) / (GR_WAVES / EW)),               \
+                     dim3(64 * GR_WAVES), 0, s, (const bf16*)x, ldx, (const bf16*)wg, M, H, E, topk, (bf16*)logits, \
+                     ticket, topk_idx, topk_w, src_rows, slot_of, offsets)
+  if (E <= 8) DLS_GR(2, 4);
+  else DLS_GR(2, 8);
+#undef DLS_GR
+  return true;
 }
 
 void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int rows, int H, hipStream_t s) {

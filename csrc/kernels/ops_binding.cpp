@@ -357,6 +357,30 @@ std::vector<at::Tensor> moe_route(const at::Tensor& logits, int64_t topk) {
   return {idx, w, src, slot, off};
 }
 
+// router GEMM + routing in ONE launch (gate_route_kernel): logits (bf16 [M][E], written to
+// `logits`) and idx, w, src_rows, slot_of, offsets; an empty list when the shape is outside
+// the kernel's limits (the caller then runs the GEMM and moe_route)
+std::vector<at::Tensor> moe_gate_route(const at::Tensor& x, const at::Tensor& wg, int64_t topk, at::Tensor& logits) {
+  check_bf16(x, "x");
+  check_bf16(wg, "router weight");
+  check_bf16(logits, "logits");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && wg.dim() == 2 && wg.is_contiguous() && wg.size(1) == x.size(1),
+              "x [M][H] (rows contiguous), router weight contiguous [E][H]");
+  const int64_t M = x.size(0), H = x.size(1), E = wg.size(0);
+  TORCH_CHECK(logits.is_contiguous() && logits.numel() == M * E, "logits must be contiguous [M][E]");
+  TORCH_CHECK(topk >= 1 && topk <= 8 && topk <= E, "1 <= topk <= min(8, E)");
+  auto iopt = x.options().dtype(at::kInt);
+  auto idx = at::empty({M, topk}, iopt);
+  auto w = at::empty({M, topk}, x.options().dtype(at::kFloat));
+  auto src = at::empty({M * topk}, iopt), slot = at::empty({M * topk}, iopt), off = at::empty({E + 1}, iopt);
+  int* ticket = split_k_counters(x, 1);
+  if (!launch_moe_gate_route(x.data_ptr(), (int)x.stride(0), wg.data_ptr(), (int)M, (int)H, (int)E, (int)topk,
+                             logits.data_ptr(), ticket, idx.data_ptr<int32_t>(), w.data_ptr<float>(),
+                             src.data_ptr<int32_t>(), slot.data_ptr<int32_t>(), off.data_ptr<int32_t>(), cur_stream()))
+    return {};
+  return {idx, w, src, slot, off};
+}
+
 at::Tensor moe_permute(const at::Tensor& x, const at::Tensor& src_rows) {
   check_bf16(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "x must be contiguous [M][H]");
@@ -570,6 +594,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_gather_combine", &moe_gather_combine);
   m.def("moe_align", &moe_align);
   m.def("moe_route", &moe_route);
+  m.def("moe_gate_route", &moe_gate_route);
   m.def("moe_permute", &moe_permute);
   m.def("moe_combine", &moe_combine, py::arg("expert_out"), py::arg("slot_of"), py::arg("weights"),
         py::arg("range") = py::none(), py::arg("out") = py::none());

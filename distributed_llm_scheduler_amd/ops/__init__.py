@@ -412,6 +412,19 @@ def moe_route(logits, topk, n_experts):
     return (idx, gate) + moe_align(idx, n_experts)
 
 
+def moe_gate_route(x, w_gate, topk, logits):
+    """Router GEMM + routing of one MoE layer: ``logits`` (bf16 [M][E]) <- x @ w_gate^T and
+    returns (idx, gate, src_rows, slot_of, offsets). GPU: ONE launch (the last workgroup to
+    publish its logits routes every token) when the shape fits the kernel, else the GEMM and
+    moe_route."""
+    if _gpu(x):
+        r = ext().moe_gate_route(x, w_gate, int(topk), logits.view(x.shape[0], -1))
+        if r:
+            return tuple(r)
+    linear(x, w_gate, out=logits.view(x.shape[0], -1))
+    return moe_route(logits.view(x.shape[0], -1), topk, w_gate.shape[0])
+
+
 def moe_permute(x, src_rows):
     if _gpu(x):
         return ext().moe_permute(x.contiguous(), src_rows)

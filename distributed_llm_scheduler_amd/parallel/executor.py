@@ -220,6 +220,7 @@ class DAGExecutor:
         self._moe_skip: set = set()
         self._moe_batched_ids: set = set()
         self._moe_bufs: Dict[int, tuple] = {}
+        self._gate_route: Dict[str, Tuple[int, int]] = {}  # router task -> (E, top-k): GEMM + routing fused
         ins = self.prog.instrs
         if not self.gpu or not MOE_BATCH or any(i.op in ("evict", "send", "recv") for i in ins):
             return
@@ -254,6 +255,8 @@ class DAGExecutor:
                 self._moe_batch[i] = (members, [ld for ld in loads if ld < members[-1]])
                 self._moe_skip |= set(members[1:])
                 self._moe_batched_ids |= {ins[m].group[0] for m in members}
+                if MOE_FUSED_ROUTE:  # the layer's router node computes its logits AND the routing
+                    self._gate_route[t0.op.inputs[1]] = (E, t0.op.attrs["top_k"])
             i = j
 
     def _run_moe_batch(self, i: int, stats: StepStats) -> None:
@@ -741,6 +744,13 @@ class DAGExecutor:
             ops.add(self._x(head.op.inputs[0]), self._x(head.op.inputs[1]), out=out)
         elif k == "gelu":
             ops.gelu(self._x(src), out=out)
+        elif k == "linear" and head.id in self._gate_route and norm is None and residual is None \
+                and st_out is None and "b" not in W and not act:
+            # router of a batched MoE layer: logits + top-k + expert-sorted order in one launch,
+            # memoised for the layer's experts and combine (_moe_route)
+            E, K = self._gate_route[head.id]
+            self._moe_memo[("route", head.id)] = ops.moe_gate_route(self._flat(self._x(src)), self._w(W["w"]), K,
+                                                                    self._flat(out))
         elif k in ("linear", "lm_head"):
             self._gemm(self._flat(self._x(src)), W["w"], W.get("b"), norm, act=act, residual=residual,
                        out=self._flat(out), stats_out=st_out)

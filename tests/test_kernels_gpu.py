@@ -346,6 +346,24 @@ def test_moe_route_fused_equals_router_align(M, E, k):
     assert torch.equal(fo, off) and torch.equal(fs, src) and torch.equal(fsl, slot)
 
 
+@pytest.mark.parametrize("M,E,k,H", [(512, 8, 2, 4096), (300, 8, 2, 256), (100, 16, 4, 512), (77, 64, 2, 128)])
+def test_moe_gate_route_fused(M, E, k, H):
+    """Router GEMM + routing in one launch (last workgroup routes): logits match the fp32
+    reference, and the routing equals moe_route over those same logits. E = 64 takes the
+    GEMM + moe_route fallback."""
+    x = _rand(M, H, seed=7)
+    wg = _rand(E, H, scale=0.05, seed=8)
+    logits = torch.empty(M, E, dtype=torch.bfloat16, device=DEV)
+    for _ in range(3):  # repeated launches: the ticket must be reset by every last block
+        r = ops.moe_gate_route(x, wg, k, logits)
+    torch.cuda.synchronize()
+    _close(logits.cpu().float(), ops.ref_linear(x.cpu(), wg.cpu()).float(), 2e-2)
+    ref = ops.moe_route(logits, k, E)
+    torch.cuda.synchronize()
+    for a, b in zip(r, ref):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("config", [-1, 3, 17, 30, 31, 33])
 def test_gemm_grouped_gathered_rows(config):
     """Gate/up grouped GEMM reading its expert-sorted rows straight from the token matrix
