@@ -20,7 +20,9 @@ from distributed_llm_scheduler_amd.parallel.executor import synthetic_tokens
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 GPUs")]
 
-WORLD = 2
+
+def _needs(world):
+    return pytest.mark.skipif(torch.cuda.device_count() < world, reason=f"needs >= {world} GPUs")
 
 
 def _free_port():
@@ -31,11 +33,11 @@ def _free_port():
     return port
 
 
-def _init(rank, port):
+def _init(rank, world, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     torch.cuda.set_device(rank)
-    dist.init_process_group("nccl", rank=rank, world_size=WORLD, device_id=torch.device(f"cuda:{rank}"))
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{rank}"))
 
 
 def _ref_err(p, ex, store, rid=""):
@@ -46,34 +48,42 @@ def _ref_err(p, ex, store, rid=""):
     return (out - ref).abs().max().item(), ref.abs().max().item()
 
 
-def _p2p_worker(rank, port, q):
-    _init(rank, port)
+def _p2p_worker(rank, world, port, q):
+    """Ring round trip: every rank sends to rank + 1 and receives from rank - 1 (one xGMI link
+    per pair), then the values travel back; each rank checks what returned."""
+    _init(rank, world, port)
     try:
-        x = torch.arange(1 << 20, device="cuda", dtype=torch.float32).to(torch.bfloat16)
-        if rank == 0:
-            dist.send(x, 1)
-            back = torch.empty_like(x)
-            dist.recv(back, 1)
-            q.put(bool(torch.equal(back, x + 1)))
-        else:
-            y = torch.empty_like(x)
-            dist.recv(y, 0)
-            dist.send(y + 1, 0)
-            q.put(True)
+        x = torch.arange(1 << 20, device="cuda", dtype=torch.float32).to(torch.bfloat16) + rank
+        nxt, prv = (rank + 1) % world, (rank - 1) % world
+        got = torch.empty_like(x)
+        reqs = [dist.isend(x, nxt), dist.irecv(got, prv)]
+        for r in reqs:
+            r.wait()
+        back = torch.empty_like(x)
+        reqs = [dist.isend(got + 1, prv), dist.irecv(back, nxt)]
+        for r in reqs:
+            r.wait()
+        torch.cuda.synchronize()
+        q.put(bool(torch.equal(got, x - rank + prv)) and bool(torch.equal(back, x + 1)))
     finally:
         dist.destroy_process_group()
 
 
-def _dag_worker(rank, port, model, placement, tp, q):
-    _init(rank, port)
+def _dag_worker(rank, world, port, model, placement, tp, capture, q):
+    _init(rank, world, port)
     try:
         kw = dict(tp=tp, placement=placement) if tp > 1 else dict(placement=placement, replicas=1)
-        p = runtime.plan(model, world=WORLD, seq=64, batch=2, **kw)
+        p = runtime.plan(model, world=world, seq=64, batch=2, **kw)
         store = runtime.make_store(p)
         ex = runtime.make_executor(p, rank, torch.device(f"cuda:{rank}"), store, pg=dist.group.WORLD)
         for _ in range(2):
             st = ex.step()
         torch.cuda.synchronize()
+        if capture:  # hipGraph segments between the eager RCCL steps, then replayed steps
+            ex.capture()
+            for _ in range(2):
+                st = ex.step()
+            torch.cuda.synchronize()
         res = {"rank": rank, "sends": st.sends, "recvs": st.recvs, "errs": []}
         if p.placement.get("output_projection") == rank:
             res["errs"].append(_ref_err(p, ex, store))
@@ -82,11 +92,11 @@ def _dag_worker(rank, port, model, placement, tp, q):
         dist.destroy_process_group()
 
 
-def _spawn(target, *args):
+def _spawn(target, world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, port, *args, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
     for pr in procs:
         pr.start()
     for pr in procs:
@@ -95,18 +105,23 @@ def _spawn(target, *args):
     for pr in procs:
         if pr.is_alive():
             pr.kill()
-    assert codes == [0] * WORLD, codes
-    return [q.get(timeout=5) for _ in range(WORLD)]
+    assert codes == [0] * world, codes
+    return [q.get(timeout=5) for _ in range(world)]
 
 
-def test_rccl_p2p_round_trip():
-    assert all(_spawn(_p2p_worker))
+@pytest.mark.parametrize("world", [2, pytest.param(4, marks=_needs(4)), pytest.param(8, marks=_needs(8))])
+def test_rccl_p2p_ring_round_trip(world):
+    assert all(_spawn(_p2p_worker, world))
 
 
-@pytest.mark.parametrize("model,placement,tp", [("mini-gpt2", "pipeline", 1), ("mini-llama", "pipeline", 1),
-                                                ("mini-gpt2", "tensor", 2), ("mini-llama", "tensor", 2)])
-def test_two_gpu_dag_matches_reference(model, placement, tp):
-    res = _spawn(_dag_worker, model, placement, tp)
+@pytest.mark.parametrize("model,placement,tp,world,capture", [
+    ("mini-gpt2", "pipeline", 1, 2, False), ("mini-llama", "pipeline", 1, 2, False),
+    ("mini-gpt2", "tensor", 2, 2, False), ("mini-llama", "tensor", 2, 2, False),
+    ("mini-gpt2", "pipeline", 1, 2, True), ("mini-llama", "tensor", 2, 2, True),
+    pytest.param("mini-llama", "pipeline", 1, 4, True, marks=_needs(4)),
+    pytest.param("mini-gpt2", "pipeline", 1, 8, True, marks=_needs(8))])
+def test_multi_gpu_dag_matches_reference(model, placement, tp, world, capture):
+    res = _spawn(_dag_worker, world, model, placement, tp, capture)
     assert sum(r["sends"] for r in res) > 0 and sum(r["recvs"] for r in res) > 0
     errs = [e for r in res for e in r["errs"]]
     assert len(errs) == 1
