@@ -408,8 +408,9 @@ bool launch_moe_gate_route(const void* x, int ldx, const void* wg, int M, int H,
                            int* ticket, int32_t* topk_idx, float* topk_w, int32_t* src_rows, int32_t* slot_of,
                            int32_t* offsets, hipStream_t s) {
   if (H > 64 * 8 * GR_XV || M * topk > kRouteMaxAssign || M * E > kRouteMaxAssign || E % 2 || H % 8 || E > 16 ||
-      ldx % 8)
-    return false;
+      ldx % 8 || reinterpret_cast<uintptr_t>(x) % 16 || reinterpret_cast<uintptr_t>(wg) % 16 ||
+      reinterpret_cast<uintptr_t>(logits) % 4)
+    return false;  // 16-B vector loads, 4-B logits pair stores
   // 2 experts per wave: E = 8 -> 4 waves per token, 2 tokens per workgroup (256 workgroups
   // for a 512-token batch); E <= 16 -> 8 waves per token
 #define DLS_GR(EPW, EW)                                                                                           \
