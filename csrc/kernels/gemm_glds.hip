@@ -862,6 +862,122 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows_kernel(const float* __
   }
 }
 
+// Split-K reduce that ALSO normalises the rows for the next norm (the separate norm launch of
+// a K > 1024 norm — Llama / Mixtral hidden 4096 — disappears): one workgroup owns a row, keeps
+// its bf16-rounded outputs in registers, reduces their statistics across the workgroup and
+// writes norm(row) * w (+ b) — the norm kernel's arithmetic on the same rounded inputs.
+constexpr int RN_MAXV = 4;  // 8-column vectors per thread: N <= 256 * 8 * RN_MAXV
+// VPT vectors per thread, SK split-K slices known at compile time (0: runtime count): every
+// slab load of the row is issued before the first add (one memory round trip, not VPT x SK)
+template <int VPT, int SK>
+__global__ __launch_bounds__(256) void splitk_reduce_norm_kernel(const float* __restrict__ P, int splitk, int M,
+                                                                 int N, bf16* __restrict__ C, int ldc,
+                                                                 const bf16* __restrict__ bias,
+                                                                 const bf16* __restrict__ R, int ldr, int act,
+                                                                 float alpha, Epi ep, ReduceNorm nm,
+                                                                 bf16* __restrict__ Y, int ldy,
+                                                                 const bf16* __restrict__ nw,
+                                                                 const bf16* __restrict__ nb, int nmode, float neps) {
+  __shared__ float red[2][4];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t slab = (size_t)M * N;
+  const int nsk = SK > 0 ? SK : splitk;
+  float v[VPT][8];
+#pragma unroll
+  for (int u = 0; u < VPT; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+  if constexpr (SK > 0) {
+    f32x4 a[VPT][SK][2];
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int cl = min((u * 256 + tid) * 8, N - 8);  // clamped, not guarded
+#pragma unroll
+      for (int s2 = 0; s2 < SK; ++s2) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(P + s2 * slab + (size_t)m * N + cl);
+        a[u][s2][0] = p[0];
+        a[u][s2][1] = p[1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u)
+#pragma unroll
+      for (int s2 = 0; s2 < SK; ++s2)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[u][e] += a[u][s2][0][e];
+          v[u][e + 4] += a[u][s2][1][e];
+        }
+  } else {
+    for (int s2 = 0; s2 < nsk; ++s2) {
+#pragma unroll
+      for (int u = 0; u < VPT; ++u) {
+        const int cl = min((u * 256 + tid) * 8, N - 8);
+        const f32x4* p = reinterpret_cast<const f32x4*>(P + s2 * slab + (size_t)m * N + cl);
+        const f32x4 a0 = p[0], a1 = p[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[u][e] += a0[e];
+          v[u][e + 4] += a1[e];
+        }
+      }
+    }
+  }
+  float y[VPT][8];
+  float s1 = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    const int c = (u * 256 + tid) * 8;
+    const int cl = min(c, N - 8);
+    float x[8];
+    reduce_finalize(x, v[u], m, cl, bias, R, ldr, act, alpha, ep, nm);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = f2bf(x[e]);
+      y[u][e] = c < N ? bf2f(o[e]) : 0.f;
+      s1 += y[u][e];
+    }
+    if (c < N) *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + c) = o;
+  }
+  bf16x8 wv[VPT], bv[VPT];  // the norm's weights, requested before the two reductions
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    const int cl = min((u * 256 + tid) * 8, N - 8);
+    wv[u] = *reinterpret_cast<const bf16x8*>(nw + cl);
+    bv[u] = nb ? *reinterpret_cast<const bf16x8*>(nb + cl) : bf16x8{};
+  }
+  auto block_sum = [&](float t, int slot) {
+    t = wave_sum(t);
+    if (lane == 0) red[slot][wave] = t;
+    __syncthreads();
+    return red[slot][0] + red[slot][1] + red[slot][2] + red[slot][3];
+  };
+  const float inv_n = 1.0f / (float)N;
+  float mean = 0.f;
+  if (nmode == 1) mean = block_sum(s1, 0) * inv_n;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPT; ++u)
+    if ((u * 256 + tid) * 8 < N)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (y[u][e] - mean) * (y[u][e] - mean);
+  const float rstd = rsqrtf(block_sum(q, 1) * inv_n + neps);
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    const int c = (u * 256 + tid) * 8;
+    if (c >= N) continue;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = (y[u][e] - mean) * rstd * bf2f(wv[u][e]);
+      if (nb) t += bf2f(bv[u][e]);
+      o[e] = f2bf(t);
+    }
+    *reinterpret_cast<bf16x8*>(Y + (size_t)m * ldy + c) = o;
+  }
+}
+
 // resident blocks of a persistent launch: CUs x blocks per CU (occupancy query, cached)
 template <class C, int LN>
 int persistent_grid() {
@@ -877,7 +993,7 @@ int persistent_grid() {
 }
 
 template <class C>
-void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
+bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
             float ln_eps, const int* rows, bool persist) {
   // in-launch combine only while the last arriver's serial read of the other slices stays small
   // (cdna_hip_programming.md: ~1 us per 16 KB; Llama-3-8B's 256x128 split-4 tiles would read
@@ -911,6 +1027,23 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
 #undef DLS_K
   if (splitk > 1 && !ep.tile_sem) {
     const ReduceNorm nm{ln_colsum, a.ext_stats ? ln_mode : 0, ln_eps, a.K};
+    if (a.norm_out && !rows && a.act != kActSwiglu && a.N % 8 == 0 && a.N <= 256 * 8 * RN_MAXV) {
+#define DLS_RN(VPT, SK)                                                                                          \
+  hipLaunchKernelGGL((splitk_reduce_norm_kernel<VPT, SK>), dim3(a.M), dim3(256), 0, s, ws, splitk, a.M, a.N,        \
+                     (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, ep, nm,     \
+                     (bf16*)a.norm_out, a.ldn, (const bf16*)a.norm_w, (const bf16*)a.norm_b, a.norm_mode, a.norm_eps)
+      if (a.N <= 256 * 8 * 2) {
+        if (splitk == 2) DLS_RN(2, 2);
+        else if (splitk == 4) DLS_RN(2, 4);
+        else DLS_RN(2, 0);
+      } else {
+        if (splitk == 2) DLS_RN(4, 2);
+        else if (splitk == 4) DLS_RN(4, 4);
+        else DLS_RN(4, 0);
+      }
+#undef DLS_RN
+      return true;
+    }
     if (a.stats_out && !rows && a.act != kActSwiglu && (a.N / 8) % 64 != 0) {  // small rows: a wave per row
       hipLaunchKernelGGL(splitk_reduce_rows_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, ws, splitk, a.M, a.N,
                          (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, ep, nm);
@@ -921,6 +1054,7 @@ void launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
                          (const bf16*)a.bias, (const bf16*)a.R, a.ldr, a.act, a.alpha, rows, a.compact_rows, ep, nm);
     }
   }
+  return false;
 }
 
 using C0 = Cfg<256, 128, 4, 2, 3>;  // 8 waves, 64x64 per wave: large GEMMs
@@ -1064,7 +1198,7 @@ void gemm_glds_pick(int M, int N, int K, int* cfg, int* splitk) {
 
 size_t gemm_glds_workspace_bytes(int M, int N, int splitk) { return splitk > 1 ? (size_t)splitk * M * N * 4 : 0; }
 
-void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s, const float* ln_colsum,
+bool launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s, const float* ln_colsum,
                       int ln_mode, float ln_eps, const int* rows) {
   float* ws = static_cast<float*>(workspace);
   const bool persist = cfg >= kGemmPersist && !rows;
@@ -1077,7 +1211,11 @@ void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
   // the SwiGLU epilogue pairs 16-column gate/up fragments: wave tiles must be multiples of 32
   // columns (configs 22-27 have 48- / 144-column wave tiles)
   if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
-  with_cfg(cfg, [&](auto c) { launch<decltype(c)>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist); });
+  bool normed = false;
+  with_cfg(cfg, [&](auto c) {
+    normed = launch<decltype(c)>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist);
+  });
+  return normed;
 }
 
 void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const int* offsets,

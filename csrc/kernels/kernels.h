@@ -41,6 +41,15 @@ struct GemmArgs {
   float* stats_out = nullptr;
   const float* ext_stats = nullptr;
   int* tile_sem = nullptr;  // split-K: >= tiles_m*tiles_n zeroed counters -> combine inside the GEMM launch
+  // post-norm of the FINAL output rows for the next (unfolded) norm: norm_out[M][ldn] =
+  // norm(C) * norm_w (+ norm_b); norm_mode 1 LayerNorm, 2 RMSNorm. Split-K launches do it in
+  // their row-owning reduce (no separate norm launch); launch_gemm_glds reports whether it did.
+  void* norm_out = nullptr;
+  const void* norm_w = nullptr;
+  const void* norm_b = nullptr;
+  int norm_mode = 0;
+  float norm_eps = 1e-5f;
+  int ldn = 0;
 };
 
 // epilogue extras carried down to the tile code
@@ -77,7 +86,8 @@ size_t gemm_glds_workspace_bytes(int M, int N, int splitk);
 // W pre-scaled by the norm gain, ln_colsum[n] = sum_k W[n][k], bias = bias + W.ln_bias)
 // rows (device int32[2], optional): only rows [rows[0], rows[1]) of A/C/R take part (M is then
 // the maximum row count, sizing the grid) — an MoE expert's routed rows without a host sync.
-void launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s,
+// returns true when the launch also wrote a.norm_out (a split-K GEMM's row-owning reduce)
+bool launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, hipStream_t s,
                       const float* ln_colsum = nullptr, int ln_mode = 0, float ln_eps = 1e-5f,
                       const int* rows = nullptr);
 // Grouped MoE-expert GEMM: E groups in ONE launch (grid = E x column tiles). Group g multiplies
@@ -143,9 +153,11 @@ void launch_grouped_gemm(const void* X, const int32_t* offsets, const void* W, v
 
 // y[m] = r[m] + sum_j w[m,j] * expert_{idx[m,j]}[slot[m,j] - off[idx[m,j]]] over compact per-expert
 // outputs whose base addresses are the device array eo_ptrs[E]; topk <= 8
+// yn (optional, H <= 8192): also write norm(y) * nw (+ nb) for the next norm (nmode 1 LayerNorm, 2 RMSNorm)
 void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t* idx, const int32_t* slot_of,
                                const int32_t* off, const float* w, const void* r, void* y, int M, int topk, int H,
-                               int E, hipStream_t s);
+                               int E, hipStream_t s, void* yn = nullptr, const void* nw = nullptr,
+                               const void* nb = nullptr, int nmode = 0, float neps = 1e-5f);
 
 // dst (HBM) <- src (pinned host memory, device-accessible address); bytes % 16 == 0, both
 // 16-byte aligned; at most `blocks` workgroups of 256 lanes pull over the host link

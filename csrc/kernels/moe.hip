@@ -331,49 +331,113 @@ __global__ __launch_bounds__(256) void combine_kernel(const bf16* __restrict__ e
 // block-uniform (scalar loads), and each thread issues all k + 1 of its 16-B loads before the
 // arithmetic, so a 4096-wide row is 2 load batches per thread (a wave per row took 8 dependent
 // rounds: 15 us per Mixtral layer at 1 TB/s).
+constexpr int GC_MAXV = 4;  // 8-column vectors per thread: H <= 256 * 8 * GC_MAXV
+// KK expert slots (>= top-k; unused slots and unrouted experts read a valid row with weight 0)
+// and VPT vectors per thread at compile time: every load of the row is issued before the
+// first use, with no branch around any of them (a null-checked load per expert made the
+// compiler wait a full memory latency per load)
+template <int KK, int VPT>
 __global__ __launch_bounds__(256) void gather_combine_kernel(const unsigned long long* __restrict__ eo_ptrs,
                                                              const int32_t* __restrict__ idx,
                                                              const int32_t* __restrict__ slot_of,
                                                              const int32_t* __restrict__ off,
                                                              const float* __restrict__ w, const bf16* __restrict__ r,
-                                                             bf16* __restrict__ y, int M, int topk, int H, int E) {
-  const int m = blockIdx.x;
-  const bf16x8* src[MAX_K];
-  float g[MAX_K];
-  const int kk = topk < MAX_K ? topk : MAX_K;
+                                                             bf16* __restrict__ y, int M, int topk, int H, int E,
+                                                             bf16* __restrict__ yn, const bf16* __restrict__ nw,
+                                                             const bf16* __restrict__ nb, int nmode, float neps) {
+  __shared__ float red[2][4];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16* rrow = r ? r + (size_t)m * H : nullptr;
+  const bf16* src[KK];
+  float g[KK];
+  const bf16* any_row = nullptr;
 #pragma unroll
-  for (int j = 0; j < MAX_K; ++j) {
+  for (int j = 0; j < KK; ++j) {
     src[j] = nullptr;
     g[j] = 0.f;
-    if (j >= kk) continue;
+    if (j >= topk) continue;
     const int e = idx[m * topk + j];
     if (e < 0 || e >= E) continue;
-    const int row = slot_of[m * topk + j] - off[e];
-    src[j] = reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(eo_ptrs[e]) + (size_t)row * H);
+    src[j] = reinterpret_cast<const bf16*>(eo_ptrs[e]) + (size_t)(slot_of[m * topk + j] - off[e]) * H;
     g[j] = w[m * topk + j];
+    any_row = src[j];
+  }
+  if (!any_row) any_row = rrow ? rrow : y + (size_t)m * H;  // a row every load may read
+#pragma unroll
+  for (int j = 0; j < KK; ++j)
+    if (!src[j]) src[j] = any_row;  // weight 0
+  const bf16* rsrc = rrow ? rrow : any_row;
+  const float rg = rrow ? 1.f : 0.f;
+  const int nv = H / 8;
+  bf16x8 v[VPT][KK], rv[VPT];
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    const int cl = min(u * 256 + tid, nv - 1);  // clamped loads, guarded stores
+#pragma unroll
+    for (int j = 0; j < KK; ++j) v[u][j] = reinterpret_cast<const bf16x8*>(src[j])[cl];
+    rv[u] = reinterpret_cast<const bf16x8*>(rsrc)[cl];
   }
   bf16x8* yo = reinterpret_cast<bf16x8*>(y + (size_t)m * H);
-  const bf16x8* ro = r ? reinterpret_cast<const bf16x8*>(r + (size_t)m * H) : nullptr;
-  for (int c = threadIdx.x; c < H / 8; c += 256) {
-    bf16x8 v[MAX_K];
-    bf16x8 rv = {};
+  float yv[VPT][8];
+  float s1 = 0.f;
 #pragma unroll
-    for (int j = 0; j < MAX_K; ++j)
-      if (src[j]) v[j] = src[j][c];
-    if (ro) rv = ro[c];
+  for (int u = 0; u < VPT; ++u) {
+    const int c = u * 256 + tid;
     float acc[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = ro ? bf2f(rv[e]) : 0.f;
+    for (int e = 0; e < 8; ++e) acc[e] = rg * bf2f(rv[u][e]);
 #pragma unroll
-    for (int j = 0; j < MAX_K; ++j) {
-      if (!src[j]) continue;
+    for (int j = 0; j < KK; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += g[j] * bf2f(v[j][e]);
-    }
+      for (int e = 0; e < 8; ++e) acc[e] += g[j] * bf2f(v[u][j][e]);
     bf16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
-    yo[c] = o;
+    for (int e = 0; e < 8; ++e) {
+      o[e] = f2bf(acc[e]);
+      yv[u][e] = c < nv ? bf2f(o[e]) : 0.f;
+      s1 += yv[u][e];
+    }
+    if (c < nv) yo[c] = o;
+  }
+  if (!yn) return;  // block-uniform
+  // post-norm for the next (unfolded) norm: this workgroup owns the whole row; its weights are
+  // requested before the two reductions
+  bf16x8 wv[VPT], bv[VPT];
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    const int cl = min(u * 256 + tid, nv - 1);
+    wv[u] = reinterpret_cast<const bf16x8*>(nw)[cl];
+    bv[u] = nb ? reinterpret_cast<const bf16x8*>(nb)[cl] : bf16x8{};
+  }
+  auto block_sum = [&](float t, int slot) {
+    t = wave_sum(t);
+    if (lane == 0) red[slot][wave] = t;
+    __syncthreads();
+    return red[slot][0] + red[slot][1] + red[slot][2] + red[slot][3];
+  };
+  const float inv_h = 1.0f / (float)H;
+  float mean = 0.f;
+  if (nmode == 1) mean = block_sum(s1, 0) * inv_h;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < VPT; ++u)
+    if (u * 256 + tid < nv)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (yv[u][e] - mean) * (yv[u][e] - mean);
+  const float rstd = rsqrtf(block_sum(q, 1) * inv_h + neps);
+  bf16x8* yno = reinterpret_cast<bf16x8*>(yn + (size_t)m * H);
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    const int c = u * 256 + tid;
+    if (c >= nv) continue;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = (yv[u][e] - mean) * rstd * bf2f(wv[u][e]);
+      if (nb) t += bf2f(bv[u][e]);
+      o[e] = f2bf(t);
+    }
+    yno[c] = o;
   }
 }
 
@@ -381,9 +445,24 @@ __global__ __launch_bounds__(256) void gather_combine_kernel(const unsigned long
 
 void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t* idx, const int32_t* slot_of,
                                const int32_t* off, const float* w, const void* r, void* y, int M, int topk, int H,
-                               int E, hipStream_t s) {
-  hipLaunchKernelGGL(gather_combine_kernel, dim3(M), dim3(256), 0, s, eo_ptrs, idx, slot_of, off, w,
-                     (const bf16*)r, (bf16*)y, M, topk, H, E);
+                               int E, hipStream_t s, void* yn, const void* nw, const void* nb, int nmode,
+                               float neps) {
+#define DLS_GC(KK, VPT)                                                                                            \
+  hipLaunchKernelGGL((gather_combine_kernel<KK, VPT>), dim3(M), dim3(256), 0, s, eo_ptrs, idx, slot_of, off, w,      \
+                     (const bf16*)r, (bf16*)y, M, topk, H, E, (bf16*)yn, (const bf16*)nw, (const bf16*)nb, nmode, \
+                     neps)
+#define DLS_GC_K(VPT)          \
+  if (topk <= 1) DLS_GC(1, VPT); \
+  else if (topk <= 2) DLS_GC(2, VPT); \
+  else if (topk <= 4) DLS_GC(4, VPT); \
+  else DLS_GC(8, VPT)
+  if (H <= 256 * 8 * 2) {
+    DLS_GC_K(2);
+  } else {
+    DLS_GC_K(4);
+  }
+#undef DLS_GC_K
+#undef DLS_GC
 }
 
 void launch_moe_router(const void* logits, int M, int E, int topk, int32_t* topk_idx, float* topk_w,

@@ -68,7 +68,9 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                 const c10::optional<at::Tensor>& rows, bool compact_rows,
                 const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin, int64_t rope_S,
                 int64_t rope_D, int64_t rope_cols, const c10::optional<at::Tensor>& stats_out,
-                const c10::optional<at::Tensor>& ext_stats) {
+                const c10::optional<at::Tensor>& ext_stats, const c10::optional<at::Tensor>& norm_out,
+                const c10::optional<at::Tensor>& norm_w, const c10::optional<at::Tensor>& norm_b, int64_t norm_mode,
+                double norm_eps) {
   check_bf16(a_in, "A");
   check_bf16(w, "W");
   at::Tensor a = as2d(a_in);
@@ -117,6 +119,35 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   GemmArgs g{a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0), c.data_ptr(), (int)c.stride(0),
              bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1,
              (compact_rows && rows.has_value()) ? (int)c.size(0) : 0};
+  // post-norm for the next (unfolded) norm: a split-K launch writes it from its row-owning
+  // reduce; every other path runs the norm kernel on the output right after the GEMM
+  at::Tensor y_n;
+  if (norm_out.has_value()) {
+    TORCH_CHECK(norm_mode == 1 || norm_mode == 2, "norm_mode: 1 LayerNorm, 2 RMSNorm");
+    TORCH_CHECK(!swiglu && !rows.has_value() && c.is_contiguous(), "post-norm needs a full, contiguous output");
+    y_n = as2d(*norm_out);
+    check_bf16(y_n, "norm_out");
+    TORCH_CHECK(y_n.is_contiguous() && y_n.size(0) == M && y_n.size(1) == N, "norm_out must be contiguous [M][N]");
+    TORCH_CHECK(norm_w.has_value() && norm_w->is_contiguous() && norm_w->numel() == N, "norm_w [N]");
+    check_bf16(*norm_w, "norm_w");
+    TORCH_CHECK(norm_mode == 2 || (norm_b.has_value() && norm_b->is_contiguous() && norm_b->numel() == N),
+                "LayerNorm post-norm needs norm_b [N]");
+    g.norm_out = y_n.data_ptr();
+    g.ldn = (int)N;
+    g.norm_w = norm_w->data_ptr();
+    g.norm_b = norm_mode == 1 ? norm_b->data_ptr() : nullptr;
+    g.norm_mode = (int)norm_mode;
+    g.norm_eps = (float)norm_eps;
+  }
+  auto post_norm = [&](bool done) {
+    if (!norm_out.has_value() || done) return;
+    if (norm_mode == 2)
+      launch_rmsnorm(c.data_ptr(), nullptr, nullptr, g.norm_w, y_n.data_ptr(), (int)M, (int)N, (float)norm_eps,
+                     cur_stream());
+    else
+      launch_layernorm(c.data_ptr(), nullptr, nullptr, g.norm_w, g.norm_b, y_n.data_ptr(), (int)M, (int)N,
+                       (float)norm_eps, cur_stream());
+  };
   TORCH_CHECK(!compact_rows || (rows.has_value() && !residual.has_value()), "compact_rows needs rows and no residual");
   auto check_stats = [&](const at::Tensor& t, const char* name) {
     TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == 2 * M, name,
@@ -161,6 +192,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   if (config >= kRegStage || !glds_ok) {
     g.config = config >= kRegStage ? (int)(config - kRegStage) : -1;
     launch_gemm_bf16(g, cur_stream());
+    post_norm(false);
     return c;
   }
   int cfg = (int)config, sk = (int)splitk;
@@ -179,10 +211,12 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   at::Tensor ws;
   if (sk > 1) {
     ws = at::empty({(int64_t)gemm_glds_workspace_bytes((int)M, (int)N, sk) / 4}, a.options().dtype(at::kFloat));
-    if (kSplitKFixup && !rowp) g.tile_sem = split_k_counters(a, (M + 63) / 64 * ((N + 63) / 64));
+    // (a post-norm wants the row-owning reduce kernel, not the in-launch combine)
+    if (kSplitKFixup && !rowp && !norm_out.has_value())
+      g.tile_sem = split_k_counters(a, (M + 63) / 64 * ((N + 63) / 64));
   }
-  launch_gemm_glds(g, cfg, sk, sk > 1 ? ws.data_ptr() : nullptr, cur_stream(), csp, (int)ln_mode, (float)ln_eps,
-                   rowp);
+  post_norm(launch_gemm_glds(g, cfg, sk, sk > 1 ? ws.data_ptr() : nullptr, cur_stream(), csp, (int)ln_mode,
+                             (float)ln_eps, rowp));
   return c;
 }
 
@@ -500,7 +534,9 @@ void gemm_grouped(const at::Tensor& x, const std::vector<at::Tensor>& weights, c
 // their addresses (built once by the caller and cached — hipGraph-safe)
 at::Tensor moe_gather_combine(const std::vector<at::Tensor>& experts, const at::Tensor& ptrs, const at::Tensor& idx,
                               const at::Tensor& slot_of, const at::Tensor& offsets, const at::Tensor& w,
-                              const c10::optional<at::Tensor>& residual, at::Tensor& out) {
+                              const c10::optional<at::Tensor>& residual, at::Tensor& out,
+                              const c10::optional<at::Tensor>& norm_out, const c10::optional<at::Tensor>& norm_w,
+                              const c10::optional<at::Tensor>& norm_b, int64_t norm_mode, double norm_eps) {
   const int64_t E = (int64_t)experts.size();
   TORCH_CHECK(E > 0 && ptrs.scalar_type() == at::kLong && ptrs.numel() == E && ptrs.is_cuda(), "ptrs: int64 [E]");
   const int64_t M = out.size(0), H = out.size(1), k = idx.size(1);
@@ -520,9 +556,28 @@ at::Tensor moe_gather_combine(const std::vector<at::Tensor>& experts, const at::
     TORCH_CHECK(residual->is_contiguous() && residual->numel() == M * H, "residual [M][H]");
     rp = residual->data_ptr();
   }
+  void* yn = nullptr;
+  const void *nwp = nullptr, *nbp = nullptr;
+  if (norm_out.has_value()) {  // post-norm of the combined rows for the next norm
+    TORCH_CHECK(norm_mode == 1 || norm_mode == 2, "norm_mode: 1 LayerNorm, 2 RMSNorm");
+    TORCH_CHECK(H <= 8192, "post-norm rows hold at most 8192 columns");
+    check_bf16(*norm_out, "norm_out");
+    check_bf16(*norm_w, "norm_w");
+    TORCH_CHECK(norm_out->is_contiguous() && norm_out->numel() == M * H && norm_w.has_value() &&
+                    norm_w->is_contiguous() && norm_w->numel() == H,
+                "norm_out contiguous [M][H], norm_w [H]");
+    TORCH_CHECK(norm_mode == 2 || (norm_b.has_value() && norm_b->is_contiguous() && norm_b->numel() == H),
+                "LayerNorm post-norm needs norm_b [H]");
+    yn = norm_out->data_ptr();
+    nwp = norm_w->data_ptr();
+    nbp = norm_mode == 1 ? norm_b->data_ptr() : nullptr;
+  } else {
+    TORCH_CHECK(H <= 8192, "gather-combine rows hold at most 8192 columns");
+  }
   launch_moe_gather_combine(reinterpret_cast<const unsigned long long*>(ptrs.data_ptr<int64_t>()),
                             idx.data_ptr<int32_t>(), slot_of.data_ptr<int32_t>(), offsets.data_ptr<int32_t>(),
-                            w.data_ptr<float>(), rp, out.data_ptr(), (int)M, (int)k, (int)H, (int)E, cur_stream());
+                            w.data_ptr<float>(), rp, out.data_ptr(), (int)M, (int)k, (int)H, (int)E, cur_stream(), yn,
+                            nwp, nbp, (int)norm_mode, (float)norm_eps);
   return out;
 }
 
@@ -566,7 +621,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("splitk") = 0, py::arg("ln_colsum") = py::none(), py::arg("ln_mode") = 0, py::arg("ln_eps") = 1e-5,
         py::arg("rows") = py::none(), py::arg("compact_rows") = false, py::arg("rope_cos") = py::none(),
         py::arg("rope_sin") = py::none(), py::arg("rope_S") = 1, py::arg("rope_D") = 2, py::arg("rope_cols") = 0,
-        py::arg("stats_out") = py::none(), py::arg("ext_stats") = py::none());
+        py::arg("stats_out") = py::none(), py::arg("ext_stats") = py::none(), py::arg("norm_out") = py::none(),
+        py::arg("norm_w") = py::none(), py::arg("norm_b") = py::none(), py::arg("norm_mode") = 0,
+        py::arg("norm_eps") = 1e-5);
   m.attr("REGSTAGE") = kRegStage;
   m.attr("PERSIST") = kGemmPersist;
   m.def("gemm_pick_config", &gemm_pick_config);
@@ -591,7 +648,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out") = py::none(), py::arg("zero") = py::none());
   m.def("rope_", &rope_);
   m.def("moe_router", &moe_router);
-  m.def("moe_gather_combine", &moe_gather_combine);
+  m.def("moe_gather_combine", &moe_gather_combine, py::arg("experts"), py::arg("ptrs"), py::arg("idx"),
+        py::arg("slot_of"), py::arg("offsets"), py::arg("w"), py::arg("residual"), py::arg("out"),
+        py::arg("norm_out") = py::none(), py::arg("norm_w") = py::none(), py::arg("norm_b") = py::none(),
+        py::arg("norm_mode") = 0, py::arg("norm_eps") = 1e-5);
   m.def("moe_align", &moe_align);
   m.def("moe_route", &moe_route);
   m.def("moe_gate_route", &moe_gate_route);

@@ -195,8 +195,22 @@ def ref_rope_(qkv, S, n_head, n_kv_head, head_dim, k_col, cos_t, sin_t):
 
 # --------------------------------------------------------------------- dispatchers
 
+def _post_norm_args(post_norm):
+    """(out, w, b, kind, eps) -> kwargs of the native post-norm (kind "layernorm" / "rmsnorm")."""
+    y, nw, nb, kind, eps = post_norm
+    return dict(norm_out=y, norm_w=nw, norm_b=nb if kind == "layernorm" else None,
+                norm_mode=1 if kind == "layernorm" else 2, norm_eps=float(eps))
+
+
+def _post_norm_ref(src, post_norm):
+    y, nw, nb, kind, eps = post_norm
+    s2 = src.reshape(-1, src.shape[-1])
+    r = ref_layernorm(s2, nw, nb, eps) if kind == "layernorm" else ref_rmsnorm(s2, nw, eps)
+    y.view(r.shape).copy_(r)
+
+
 def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=None, rows_hint=None,
-           compact=False, rope=None, stats_out=None):
+           compact=False, rope=None, stats_out=None, post_norm=None):
     """``act(alpha * x @ w^T + bias) + residual`` — one MFMA GEMM kernel with the whole
     epilogue fused on GPU. ``act="swiglu"`` takes a gate/up-interleaved weight
     (:func:`interleave_gate_up`) and returns the N/2-wide ``silu(gate) * up``. ``rows``
@@ -206,7 +220,9 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
     (at most ``out.shape[0]`` rows). ``rope=(cos, sin, S, D, cols)`` rotates output columns
     [0, cols) in the epilogue (q/k rows pair-interleaved, :func:`rope_pair_perm`). ``stats_out``
     (GPU, fp32 [M, 2], zeroed by the caller): accumulate each output row's (sum, sum of
-    squares) for the next folded norm (:func:`linear_norm` ``ext_stats``)."""
+    squares) for the next folded norm (:func:`linear_norm` ``ext_stats``). ``post_norm =
+    (y, w, b, "rmsnorm" | "layernorm", eps)``: also write the NEXT norm of the output rows into
+    ``y`` (a split-K launch does it in its row-owning reduce, saving the norm launch)."""
     a = ACT[act] if not isinstance(act, int) else act
     n_out = w.shape[0] // 2 if a == SWIGLU else w.shape[0]
     if _gpu(x):
@@ -214,7 +230,8 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
         M = x.numel() // x.shape[-1]
         cfg, sk = tuning.lookup(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
         if cfg == tuning.LIB:
-            if a == 0 and residual is None and rows is None and rope is None and stats_out is None:
+            if a == 0 and residual is None and rows is None and rope is None and stats_out is None \
+                    and post_norm is None:
                 # a PLAIN GEMM (no fused epilogue) whose tuned choice is the vendor library
                 # (hipBLASLt via torch); every fused-epilogue GEMM stays on the HIP kernels
                 x2 = x.reshape(M, x.shape[-1])
@@ -229,7 +246,8 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
             cfg, sk = tuning.lookup_fused(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
         rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
         y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact),
-                       rc, rs_, int(rS), int(rD), int(rcols), stats_out, None)
+                       rc, rs_, int(rS), int(rD), int(rcols), stats_out, None,
+                       **(_post_norm_args(post_norm) if post_norm is not None else {}))
         return y.view(shp) if out is None else out
     if rows is not None:
         r0, r1 = (int(v) for v in rows.tolist())
@@ -246,7 +264,9 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
     y = ref_linear(x, w, bias, act, residual, alpha, rope=rope)
     if out is not None:
         out.copy_(y)
-        return out
+        y = out
+    if post_norm is not None:
+        _post_norm_ref(y, post_norm)
     return y
 
 
@@ -447,7 +467,7 @@ def moe_combine(expert_out, slot_of, weights, slot_range=None, out=None):
     return out.copy_(y) if out is not None else y
 
 
-def moe_gather_combine(experts, idx, slot_of, offsets, gate, residual=None, out=None, ptrs=None):
+def moe_gather_combine(experts, idx, slot_of, offsets, gate, residual=None, out=None, ptrs=None, post_norm=None):
     """``out[m] = residual[m] + sum_j gate[m,j] * experts[e][slot[m,j] - offsets[e]]``, e = idx[m,j],
     over COMPACT per-expert outputs (expert e's routed rows at rows 0..count_e-1 of its
     buffer). ``ptrs``: cached int64 device tensor of the expert buffers' addresses (GPU)."""
@@ -458,7 +478,8 @@ def moe_gather_combine(experts, idx, slot_of, offsets, gate, residual=None, out=
         o2 = out.view(M, -1)
         return ext().moe_gather_combine([t.reshape(-1, o2.shape[1]) for t in experts], ptrs, idx, slot_of,
                                         offsets, gate.contiguous(), None if residual is None else
-                                        residual.reshape(M, -1), o2)
+                                        residual.reshape(M, -1), o2,
+                                        **(_post_norm_args(post_norm) if post_norm is not None else {}))
     H = out.shape[-1]
     acc = residual.reshape(M, H).float().clone() if residual is not None else torch.zeros(M, H)
     off = offsets.long()
@@ -470,6 +491,8 @@ def moe_gather_combine(experts, idx, slot_of, offsets, gate, residual=None, out=
             if sel.numel():
                 acc[sel] += gate.reshape(M, k)[sel, j, None].float() * experts[ee].reshape(-1, H)[row[sel]].float()
     out.view(M, H).copy_(acc.to(out.dtype))
+    if post_norm is not None:
+        _post_norm_ref(out, post_norm)
     return out
 
 

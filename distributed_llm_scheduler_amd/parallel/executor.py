@@ -83,6 +83,9 @@ MOE_BATCH = os.environ.get("DLS_MOE_BATCH", "1") != "0"
 # MoE routing in one launch (router + align, ops.moe_route) and the grouped gate/up GEMM
 # gathering its token rows itself (no permute kernel); 0 restores the separate launches
 MOE_FUSED_ROUTE = os.environ.get("DLS_MOE_FUSED_ROUTE", "1") != "0"
+# an unfolded norm (K > FOLD_MAX_K) computed by the block that produces its input: the split-K
+# reduce of the residual GEMM (or the MoE combine) owns whole rows and writes norm(row) too
+POST_NORM = os.environ.get("DLS_POST_NORM", "1")  # "0" off, "1" every producer, "gemm" residual GEMMs only
 # parameter refills: "pull" = the host-pull kernel reads the pinned group image over the host
 # link (benchmarks/bench_h2d.py: 50-56 GB/s from 2.4 MB up, 32 GB/s at 0.25 MB, on 32-64
 # workgroups), "dma" = hipMemcpyAsync (42-51 GB/s, 15 GB/s at 0.25 MB)
@@ -208,6 +211,60 @@ class DAGExecutor:
                 and any(i.op == "load" for i in p.instrs):
             self._plan_prefetch()
             self._copy_stream = torch.cuda.Stream(self.device)
+        self._post_norm: Dict[int, Task] = {}  # producer run -> the next norm it also writes
+        self._norm_given: Dict[int, str] = {}  # consumer run -> its norm task, already written
+        self._pn: Optional[Task] = None        # set by _issue_run for the run in flight
+        self._pn_given: Optional[str] = None   # its consumer: the norm its producer wrote (if it did)
+        self._pn_done: Optional[str] = None    # the norm the last producer actually wrote
+        if POST_NORM not in ("0", False) and self._copy_stream is None and not p.has_comm:
+            self._plan_post_norm()
+
+    def _plan_post_norm(self) -> None:
+        """Pair each norm that the next group would run as its own pass (its width is above
+        FOLD_MAX_K on GPU, so it is not folded into the consumer GEMM) with the group that
+        produces its input right before it: a residual block (attention / SwiGLU MLP, whose
+        split-K residual GEMM reduces whole rows) or the MoE combine (a workgroup per row).
+        That producer writes the normalised rows too — into the norm's own output when the
+        norm is a group of its own (Mixtral's post-attention norm feeds the router and the
+        experts), else into the consumer's norm scratch buffer. Only runs with nothing but
+        parameter loads / evictions between them (no kernel can touch the scratch rows); the
+        producer writes the norm only while the norm's weights are resident (every steady-state
+        step; a first step that loads them later lets the consumer run the norm itself)."""
+        ins = self.prog.instrs
+        norms = ("layernorm", "rmsnorm")
+        runs = [i for i, x in enumerate(ins) if x.op == "run"]
+        for i, j in zip(runs, runs[1:]):
+            P, Q = ins[i], ins[j]
+            if any(ins[k].op not in ("load", "evict") for k in range(i + 1, j)):
+                continue
+            pg = [self.tasks[t] for t in P.group]
+            qg = [self.tasks[t] for t in Q.group]
+            N = qg[0]
+            if N.op is None or N.op.kind not in norms or not N.op.inputs or N.op.inputs[0] != pg[-1].id:
+                continue
+            width = N.op.out_shape[-1]
+            if self.gpu and (width <= FOLD_MAX_K or width > 8192 or N.op.inputs[0] in self._ext_stats):
+                continue  # folded into the consumer GEMM, or wider than a reduce row holds
+            head = pg[1] if (pg[0].op.kind in norms and len(pg) > 1) else pg[0]
+            block = len(pg) > 1 and pg[-1].op.kind == "residual" and head.op.kind in ("attention", "swiglu_mlp")
+            combine = len(pg) == 1 and head.op.kind == "moe_combine" and POST_NORM != "gemm"
+            if not (block or combine) or (len(qg) == 1 and N.id not in self._views):
+                continue
+            self._post_norm[i] = N
+            self._norm_given[j] = N.id
+
+    def _post_norm_out(self, out2d: torch.Tensor):
+        """(y, w, b, kind, eps) for ops' ``post_norm`` when the run in flight feeds a norm
+        (``out2d``: the producer's output rows, which the post-norm reads whole)."""
+        N = self._pn
+        if N is None or not out2d.is_contiguous():
+            return None
+        W = N.op.weights
+        if any(W[k] not in self._wflat for k in ("w", "b") if k in W):
+            return None  # the norm's weights arrive after this run (first step): it runs itself
+        y = self._flat(self._views[N.id]) if N.id in self._views else self._scratch("norm", out2d.shape)
+        self._pn_done = N.id
+        return (y, self._w(W["w"]), self._w(W["b"]) if "b" in W else None, N.op.kind, N.op.attrs.get("eps", 1e-5))
 
     def _plan_moe_batches(self) -> None:
         """Every expert node of one MoE layer that sits on this rank, back to back in the
@@ -624,6 +681,9 @@ class DAGExecutor:
             W, cs, bd = self._prep(w_name, norm, b_name, interleave=sw, rope_perm=rope_perm)
             return ops.linear_norm(x, W, cs, bd, norm.op.kind, norm.op.attrs.get("eps", 1e-5), act=act,
                                    residual=residual, out=out, rope=rope, ext_stats=ext)
+        if norm is not None and self._pn_given == norm.id:  # x's producer wrote the normalised rows
+            x = self._scratch("norm", x.shape)
+            norm = None
         if norm is not None:
             nw = self._w(norm.op.weights["w"])
             xn = self._scratch("norm", x.shape)
@@ -703,7 +763,8 @@ class DAGExecutor:
         if ptrs is None and self.gpu:
             ptrs = torch.tensor([b.data_ptr() for b in bufs], dtype=torch.int64, device=self.device)
             self._moe_ptrs[key] = ptrs
-        ops.moe_gather_combine(bufs, idx, slot, off, gate, residual=self._x(res_name), out=out, ptrs=ptrs)
+        ops.moe_gather_combine(bufs, idx, slot, off, gate, residual=self._x(res_name), out=out, ptrs=ptrs,
+                               post_norm=self._post_norm_out(self._flat(out)))
 
     def _run_group(self, ins) -> None:
         grp = [self.tasks[t] for t in ins.group]
@@ -735,6 +796,8 @@ class DAGExecutor:
                     wpe = wpe[c * S:(c + 1) * S]
             zero = self._stats_slab if self._zero_in_embedding else None
             ops.embedding(tok, self._w(W["wte"]), wpe, S, out=self._flat(out), zero=zero)
+        elif k in ("layernorm", "rmsnorm") and self._pn_given == head.id:
+            pass  # written by the producer of its input (_plan_post_norm)
         elif k == "layernorm":
             ops.layernorm(self._flat(self._x(src)), self._w(W["w"]), self._w(W["b"]), a.get("eps", 1e-5),
                           out=self._flat(out))
@@ -772,7 +835,7 @@ class DAGExecutor:
             ops.attention(qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:], B, S, nh, nkv,
                           D, causal=a.get("causal", True), out=o)
             ops.linear(o, self._w(W["w_o"]), self._w(W["b_o"]) if "b_o" in W else None, residual=residual,
-                       out=self._flat(out), stats_out=st_out)
+                       out=self._flat(out), stats_out=st_out, post_norm=self._post_norm_out(self._flat(out)))
         elif k == "qkv_proj":
             # sequence chunk c's QKV rows (RoPE at its absolute positions c*Sc ..)
             x = self._flat(self._x(src))
@@ -810,7 +873,8 @@ class DAGExecutor:
             M, F = x.shape[0], a["ffn"]
             h = self._ws(0, (M, F))
             self._gemm(x, W["w_gate_up"], None, norm, act="swiglu", out=h)  # SwiGLU in the epilogue
-            ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out), stats_out=st_out)
+            ops.linear(h, self._w(W["w_down"]), residual=residual, out=self._flat(out), stats_out=st_out,
+                       post_norm=self._post_norm_out(self._flat(out)))
         elif k == "moe_expert":
             self._moe_expert(head, self._flat(out))
         elif k == "moe_combine":
@@ -840,6 +904,7 @@ class DAGExecutor:
         tr = self.trace
         self._pending_sends = {}
         self._moe_memo = {}
+        self._pn_done = None
         if self.prog.start_resident:  # warm-started program: its start groups are resident
             first = not self._started
             for pid, off in self.prog.start_resident.items():
@@ -974,6 +1039,16 @@ class DAGExecutor:
         self._wait_sends(ins)  # output region about to be overwritten: its sends must be done
 
     def _issue_run(self, i: int, ins, stats: StepStats, events) -> None:
+        given = self._norm_given.get(i)
+        self._pn, self._pn_given = self._post_norm.get(i), (given if given == self._pn_done else None)
+        if given is not None:
+            self._pn_done = None
+        try:
+            self._issue_run_body(i, ins, stats, events)
+        finally:
+            self._pn = self._pn_given = None
+
+    def _issue_run_body(self, i: int, ins, stats: StepStats, events) -> None:
         run = self._run_group
         if i in self._moe_batch:  # the layer's experts in one grouped launch pair
             run = lambda _ins, _i=i: self._run_moe_batch(_i, stats)  # noqa: E731

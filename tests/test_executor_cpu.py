@@ -331,3 +331,26 @@ def test_peer_parameter_fills_two_ranks(model, cap):
     assert len(errs) == 2
     for err, scale in errs:
         assert err < 0.02 * scale
+
+
+@pytest.mark.parametrize("model", ["tiny-llama", "tiny-mixtral"])
+def test_post_norm_written_by_producer(monkeypatch, model):
+    """A norm the next group would run as its own pass is written by the block producing its
+    input (residual GEMM / MoE combine) — the norm's own output for a standalone norm group, the
+    consumer's scratch for a lead norm. Same outputs as running the norms, and equal to the
+    fp32 reference; the first step (weights loaded later) runs the norms itself."""
+    from distributed_llm_scheduler_amd.parallel import executor as exm
+
+    outs = {}
+    for on in (False, True):
+        monkeypatch.setattr(exm, "POST_NORM", "1" if on else "0")
+        p = runtime.plan(model, world=1, seq=16)
+        store = runtime.make_store(p)
+        ex = runtime.make_executor(p, 0, torch.device("cpu"), store)
+        assert bool(ex._post_norm) == on
+        for _ in range(2):
+            ex.step()
+        err, scale = _ref_check(p, ex, store)
+        assert err < 0.03 * scale, (err, scale)
+        outs[on] = ex.output("output_projection").clone()
+    assert torch.equal(outs[False], outs[True])

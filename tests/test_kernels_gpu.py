@@ -493,3 +493,44 @@ def test_host_pull_copies_exact_bytes(nbytes, blocks):
     torch.cuda.synchronize()
     assert torch.equal(dst[:nbytes].cpu(), src)
     assert bool((dst[nbytes:] == 0xA5).all())
+
+
+@pytest.mark.parametrize("mode", ["rmsnorm", "layernorm"])
+@pytest.mark.parametrize("config,splitk", [(0, 4), (14, 4), (0, 2), (3, 1), (100, 1)])
+def test_gemm_post_norm(mode, config, splitk):
+    """A residual GEMM that also writes the next norm of its output rows: split-K launches do it
+    in the row-owning reduce, the others with the norm kernel after the GEMM. The output equals
+    the plain GEMM's bit for bit; the normalised rows match the norm kernel on that output."""
+    M, N, K = 512, 4096, 1024
+    x = _rand(M, K, seed=60)
+    w = _rand(N, K, scale=0.03, seed=61)
+    res = _rand(M, N, seed=62)
+    nw = (1 + 0.2 * _rand(N, seed=63).float()).to(torch.bfloat16)
+    nb = _rand(N, scale=0.1, seed=64) if mode == "layernorm" else None
+    plain = ops.ext().gemm(x, w, None, res, 0, 1.0, None, config, splitk)
+    yn = torch.full((M, N), 9.0, dtype=torch.bfloat16, device=DEV)
+    out = ops.ext().gemm(x, w, None, res, 0, 1.0, None, config, splitk, norm_out=yn, norm_w=nw, norm_b=nb,
+                         norm_mode=1 if mode == "layernorm" else 2, norm_eps=1e-5)
+    ref_n = ops.layernorm(plain, nw, nb) if mode == "layernorm" else ops.rmsnorm(plain, nw)
+    torch.cuda.synchronize()
+    assert torch.equal(out, plain)
+    _close(yn.cpu().float(), ref_n.cpu().float(), 2e-2)
+
+
+def test_moe_gather_combine_post_norm():
+    M, E, k, H = 300, 8, 2, 4096
+    g = torch.Generator().manual_seed(91)
+    logits = torch.randn(M, E, generator=g).to(torch.bfloat16).to(DEV)
+    idx, gate, src, slot, off = ops.moe_route(logits, k, E)
+    experts = [(torch.randn(M, H, generator=g) * 0.5).to(torch.bfloat16).to(DEV) for _ in range(E)]
+    res = torch.randn(M, H, generator=g).to(torch.bfloat16).to(DEV)
+    nw = (1 + 0.2 * _rand(H, seed=92).float()).to(torch.bfloat16)
+    out = torch.empty(M, H, dtype=torch.bfloat16, device=DEV)
+    yn = torch.empty(M, H, dtype=torch.bfloat16, device=DEV)
+    ops.moe_gather_combine(experts, idx, slot, off, gate, residual=res, out=out, post_norm=(yn, nw, None, "rmsnorm", 1e-5))
+    plain = torch.empty_like(out)
+    ops.moe_gather_combine(experts, idx, slot, off, gate, residual=res, out=plain)
+    ref_n = ops.rmsnorm(plain, nw)
+    torch.cuda.synchronize()
+    assert torch.equal(out, plain)
+    _close(yn.cpu().float(), ref_n.cpu().float(), 2e-2)
