@@ -165,7 +165,9 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
 }
 
 // Joint rings (BXS == 0): A and W rows of a K-tile share one stage and one DMA batch.
-template <class C>
+// GATHER: A row r is row arows[r] of A (MoE token gather) — a compile-time switch: a runtime
+// null check in every launch's prologue cost the GPT-2 GEMMs ~5 %.
+template <class C, bool GATHER = false>
 __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                                int kbeg, int nk, int lane, int wave, int kgrp, int wm, int wn,
@@ -184,7 +186,7 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
     const int kofs = kbeg + sub * C::BK + gch * 8;
     if (row < C::BM) {
       int gm = min(m0 + row, M - 1);
-      if (arows) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
+      if constexpr (GATHER) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
       src[j] = A + (size_t)gm * lda + kofs;
     } else {
       const int gn = min(n0 + row - C::BM, N - 1);
@@ -218,7 +220,7 @@ constexpr int kPolStream = 2;  // gfx950 CPol NT (streaming) bit of the DMA's au
 // Split rings (BXS > 0): issue order B0 [A0 B1] [A1 B2] ... — iteration t issues
 // A(t + SA - 1) then B(t + SB - 1). Waiting for A(t) then leaves a = min(SA-2, nk-1-t)
 // later A tiles and b = min(a + 1, nk-1-t) later W tiles in flight (B(t) precedes A(t)).
-template <class C, int WPOL = 0, bool SKIP = false>
+template <class C, int WPOL = 0, bool SKIP = false, bool GATHER = false>
 __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                                int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
@@ -231,7 +233,7 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
   for (int j = 0; j < C::PWA; ++j) {
     const int row = 8 * (wave * C::PWA + j) + (lane >> 3);
     int gm = min(m0 + row, M - 1);
-    if (arows) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
+    if constexpr (GATHER) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
     srcA[j] = A + (size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8;
   }
 #pragma unroll
@@ -283,7 +285,7 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 // they come from ep.ext_stats).
 // WPOL: cache policy of the split rings' weight DMA (0 default, kPolStream = nt for weights
 // read exactly once per step, e.g. MoE experts far larger than the MALL)
-template <class C, int LN, int WPOL = 0, bool SKIP = false>
+template <class C, int LN, int WPOL = 0, bool SKIP = false, bool GATHER = false>
 __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                           const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
                                           const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
@@ -312,10 +314,10 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
   if constexpr (C::BXS > 0)
-    mainloop_split<C, WPOL, SKIP>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
+    mainloop_split<C, WPOL, SKIP, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
                                   st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), ep.a_rows);
   else
-    mainloop_joint<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
+    mainloop_joint<C, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
                       st_q, ep.a_rows);
   if constexpr (C::KG > 1) {
     // sum the K groups' accumulators into group 0 (lane-contiguous 16-B records)
@@ -676,15 +678,22 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     Epi eg = ep;
     if (ep.a_rows) eg.a_rows = ep.a_rows + r0;
     const bf16* Ag = ep.a_rows ? A : A + (size_t)r0 * lda;
-    for (int t = 0; t * C::BM < Mr; ++t) {
-      if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
-      if (C::BXS > 0 && ep.w_stream)
-        glds_tile<C, 0, kPolStream, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K,
-                                          act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, eg);
-      else
-        glds_tile<C, 0>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act, alpha, 0, K, t,
-                        tn, ln_colsum, 0, ln_eps, eg);
+#define DLS_GROUPED_WALK(GA)                                                                                      \
+  for (int t = 0; t * C::BM < Mr; ++t) {                                                                           \
+    if (t) raw_barrier(); /* every wave is done reading the staging buffers of the previous tile */                \
+    if (C::BXS > 0 && ep.w_stream)                                                                                 \
+      glds_tile<C, 0, kPolStream, true, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, \
+                                            act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, eg);                    \
+    else                                                                                                           \
+      glds_tile<C, 0, 0, false, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act,   \
+                                    alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, eg);                                 \
+  }
+    if (ep.a_rows) {
+      DLS_GROUPED_WALK(true)
+    } else {
+      DLS_GROUPED_WALK(false)
     }
+#undef DLS_GROUPED_WALK
     return;
   }
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
