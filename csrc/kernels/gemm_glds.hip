@@ -292,7 +292,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
                                           float* __restrict__ part, int M, int Mmax, int N, int K, int act,
                                           float alpha, int ks, int kslice, int tm, int tn,
                                           const float* __restrict__ ln_colsum, int ln_mode, float ln_eps,
-                                          const Epi& ep) {
+                                          const Epi& ep, const int* __restrict__ arows = nullptr) {
   const RopeArgs& rope = ep.rope;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kgrp = wave / C::NW, wq = wave % C::NW;  // K group, wave within the group
@@ -315,10 +315,10 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
   if constexpr (C::BXS > 0)
     mainloop_split<C, WPOL, SKIP, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
-                                  st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), ep.a_rows);
+                                  st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), arows);
   else
     mainloop_joint<C, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
-                      st_q, ep.a_rows);
+                      st_q, arows);
   if constexpr (C::KG > 1) {
     // sum the K groups' accumulators into group 0 (lane-contiguous 16-B records)
     __syncthreads();
@@ -674,21 +674,23 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
     const bf16* Wg = reinterpret_cast<const bf16*>(ep.grp_w[g]);
     bf16* Cg = ep.grp_c ? reinterpret_cast<bf16*>(ep.grp_c[g]) : Cp + (size_t)r0 * ldc;
-    // gathered A: the group's rows are tokens a_rows[r0 ..]; else rows r0.. of the sorted A
-    Epi eg = ep;
-    if (ep.a_rows) eg.a_rows = ep.a_rows + r0;
-    const bf16* Ag = ep.a_rows ? A : A + (size_t)r0 * lda;
+    // gathered A: the group's rows are tokens a_rows[r0 ..]; else rows r0.. of the sorted A.
+    // The gather map travels in the `part` argument, unused by grouped launches (no split-K):
+    // a new Epi field would change every GEMM launch's argument layout
+    const int* a_rows = reinterpret_cast<const int*>(part);
+    const int* ag = a_rows ? a_rows + r0 : nullptr;
+    const bf16* Ag = a_rows ? A : A + (size_t)r0 * lda;
 #define DLS_GROUPED_WALK(GA)                                                                                      \
   for (int t = 0; t * C::BM < Mr; ++t) {                                                                           \
     if (t) raw_barrier(); /* every wave is done reading the staging buffers of the previous tile */                \
     if (C::BXS > 0 && ep.w_stream)                                                                                 \
       glds_tile<C, 0, kPolStream, true, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, \
-                                            act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, eg);                    \
+                                            act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep, ag);                \
     else                                                                                                           \
       glds_tile<C, 0, 0, false, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act,   \
-                                    alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, eg);                                 \
+                                    alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep, ag);                             \
   }
-    if (ep.a_rows) {
+    if (a_rows) {
       DLS_GROUPED_WALK(true)
     } else {
       DLS_GROUPED_WALK(false)
@@ -1240,10 +1242,11 @@ void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const in
       const char* e = std::getenv("DLS_EXPERT_NT");
       return e && e[0] == '0' ? 0 : 1;
     }();
-    const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs, w_stream, a_rows};
+    const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs, w_stream};
     const int tiles_n = (a.N + C::BN - 1) / C::BN;
     hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(n_groups * tiles_n), dim3(C::T), 0, s, (const bf16*)a.A,
-                       a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0, nullptr, a.M, a.N, a.K, a.act,
+                       a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0,
+                       const_cast<float*>(reinterpret_cast<const float*>(a_rows)), a.M, a.N, a.K, a.act,
                        a.alpha, 1, tiles_n, 1, a.K, nullptr, 0, 1e-5f, offsets, a.compact_rows, ep);
   });
 }

@@ -66,9 +66,6 @@ struct Epi {
   const unsigned long long* grp_c = nullptr;
   // grouped launch: weight DMA with the streaming (nt) cache policy (split-ring configs)
   int w_stream = 0;
-  // grouped launch: A row r of the expert-sorted order is row a_rows[r] of A (the token
-  // matrix) — the MoE permute folded into the DMA source addresses; nullptr -> A is sorted
-  const int* a_rows = nullptr;
 };
 
 int gemm_pick_config(int M, int N, int K);
