@@ -354,3 +354,24 @@ def test_post_norm_written_by_producer(monkeypatch, model):
         assert err < 0.03 * scale, (err, scale)
         outs[on] = ex.output("output_projection").clone()
     assert torch.equal(outs[False], outs[True])
+
+
+@pytest.mark.parametrize("sched", ["EFT", "MRU_spec"])
+def test_post_norm_under_memory_cap(sched):
+    """Post-norm pairs with parameter loads / evictions between producer and consumer: the
+    producer writes the norm only while the norm's weights are resident, else the consumer runs
+    it; repeated capped steps stay equal to the fp32 reference."""
+    from distributed_llm_scheduler_amd.models import registry
+    from distributed_llm_scheduler_amd.models.params import group_layout
+
+    _, groups, _ = registry.build("tiny-llama", batch=1, seq=16)
+    total = sum(group_layout(g)[0] for g in groups.values()) / 1e9
+    p = runtime.plan("tiny-llama", world=1, scheduler=sched, seq=16, cap_gb=total * 0.6)
+    assert p.completed == p.total and p.programs[0].counts().get("evict", 0) > 0
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, "cpu", store, debug=True)
+    assert ex._post_norm
+    for _ in range(3):
+        ex.step()
+    err, scale = _ref_check(p, ex, store)
+    assert err < 0.03 * scale, (err, scale)
