@@ -196,3 +196,27 @@ def test_post_norm_written_by_producer_on_gpu(monkeypatch, model, graph):
         ex.step()
     torch.cuda.synchronize()
     _check(p, ex, store, 0.03)
+
+
+@pytest.mark.parametrize("model", ["mini-llama", "mini-mixtral"])
+def test_post_norm_under_memory_cap_on_gpu(monkeypatch, model):
+    """Post-norm pairs with parameter refills between producer and consumer (no prefetch
+    stream: the pairs stay planned): capped steps still match the fp32 reference."""
+    from distributed_llm_scheduler_amd.parallel import executor as exm
+
+    monkeypatch.setattr(exm, "POST_NORM", "1")
+    monkeypatch.setattr(exm, "PREFETCH", "0")
+    monkeypatch.setattr(exm, "FOLD_MAX_K", 64)
+    monkeypatch.setattr(exm, "HANDOFF_MAX_K", 64)
+    full = runtime.plan(model, world=1, seq=64)
+    need = sum(runtime.make_store(full).nbytes(g) for g in full.groups) / 1e9
+    p = runtime.plan(model, world=1, seq=64, cap_gb=need * 0.6)
+    assert p.completed == p.total
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=False)
+    assert ex._post_norm
+    for _ in range(3):
+        st = ex.step()
+    assert st.param_fills > 0
+    torch.cuda.synchronize()
+    _check(p, ex, store, 0.03)
