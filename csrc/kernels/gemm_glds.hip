@@ -69,10 +69,11 @@ __device__ __forceinline__ void rope_pairs(float* v, int row, int col, const Rop
 // consecutive 64-deep K-tiles and group g multiplies tile g of every stage (intra-block
 // split-K: KG x the waves — and DMA issuers — per CU on a skinny grid, no reduce kernel; the
 // groups' accumulators are summed through LDS before the epilogue).
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0, int KG_ = 1>
+// RING_ = 1: the 256x256 half-tile ring main loop (mainloop_ring) instead of whole-K-tile stages
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0, int KG_ = 1, int RING_ = 0>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_, BXS = BXS_;
-  static constexpr int KG = KG_;
+  static constexpr int KG = KG_, RING = RING_;
   static constexpr int BK = 64, CH = 8;
   static constexpr int NW = WM * WN, T = 64 * NW * KG;
   static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
@@ -92,6 +93,8 @@ struct Cfg {
   static_assert(LDS_UNITS * 16 <= 163840, "LDS budget");
   static_assert(KG == 1 || (BXS == 0 && PRIO == 0), "K groups use the joint ring");
   static_assert(KG == 1 || NW * 64 * FM * FN * 16 <= LDS_UNITS * 16, "K-group reduction must fit the LDS");
+  static_assert(!RING || (BM == 256 && BN == 256 && WM == 2 && WN == 4 && STAGES == 2 && KG == 1 && BXS == 0),
+                "the ring main loop is written for 256x256 tiles, 8 waves as 2 x 4, 8 x 16 KiB slots");
 };
 
 // split rings: wait until at most a*PWA + b*PWB DMA instructions are outstanding, with
@@ -215,6 +218,156 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
   }
 }
 
+// Half-tile ring (256 x 256 tiles, 8 waves as 2 (M) x 4 (N), wave tile 128 x 64).
+//
+// Why: with whole 64-KiB K-tiles double-buffered (C8) the next tile is issued in one burst
+// and waited for with vmcnt(0) one K-tile later; on the GPT-2 LM head every K-tile then
+// stalls on the DMA (one 256-tile round of 256x256x768 tiles: 49 us = 2.1 TFLOP/s per CU,
+// benchmarks/bench_lmhead.py). Here a K-tile is four 16-KiB HALF-tiles (A rows 0-127,
+// A rows 128-255, W rows 0-127, W rows 128-255) in 8 slots (two K-tiles), and the wave's
+// 128 x 64 output is computed as four quadrants (64 x 32, 16 MFMAs each) in the order
+//   q0 (A top, W left)  q1 (A top, W right)  q2 (A bottom, W right)  q3 (A bottom, W left)
+// so a K-tile's W halves are last read in q1 and its A halves in q2: K-tile t+2's W halves
+// are issued into them at q2 of K-tile t and its A halves at q3 — four to six quadrant
+// phases before they are read, with two to three K-tiles' worth of DMA in flight at all
+// times instead of one burst per K-tile.
+// Synchronisation (cdna_hip_programming.md §5, "Read a staged buffer one phase AFTER the
+// wait that retires it"; RAW / WAR):
+//  * q0 of K-tile t: every wave waits (counted vmcnt: only K-tile t+1's 8 DMA instructions
+//    may still be outstanding) and then joins the barrier -> t's slots are complete for all;
+//  * q2 / q3: a barrier before the DMA issue — every wave has finished (lgkmcnt-waited,
+//    consumed by its MFMAs) the reads of the slots being re-filled (W after q1, A after q2).
+// Each wave's fragment reads of a quadrant are all issued before its 16 MFMAs.
+template <class C>
+__device__ __forceinline__ void mainloop_ring(bf16x8* smem, const bf16* __restrict__ A, int lda,
+                                              const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
+                                              int kbeg, int nk, int lane, int wave, int wm, int wn,
+                                              f32x4 (&acc)[C::FM][C::FN]) {
+  constexpr int SLOT = 128 * 8;  // bf16x8 units per 16-KiB half-tile slot (128 rows x 128 B)
+  // this thread's two DMA pieces of every half-tile: rows 8 * (2 * wave + j) + lane / 8
+  const bf16* srcA[2][2];
+  const bf16* srcB[2][2];
+  int dst[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = 8 * (2 * wave + j) + (lane >> 3);
+    const int gch = (lane & 7) ^ (r & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      srcA[h][j] = A + (size_t)min(m0 + h * 128 + r, M - 1) * lda + kbeg + gch * 8;
+      srcB[h][j] = W + (size_t)min(n0 + h * 128 + r, N - 1) * ldw + kbeg + gch * 8;
+    }
+    dst[j] = (2 * wave + j) * 64;
+  }
+  // slot of half-tile kind hk (0 A0, 1 A1, 2 W0, 3 W1) of K-tile t
+  auto slot = [&](int t, int hk) { return smem + ((t & 1) * 4 + hk) * SLOT; };
+  auto issue = [&](int t, int hk) {
+    const bf16* const* src = hk < 2 ? srcA[hk] : srcB[hk - 2];
+    bf16x8* st = slot(t, hk);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * C::BK),
+                                       (__attribute__((address_space(3))) void*)(st + dst[j]), 16, 0, 0);
+  };
+  // prologue: K-tiles 0 and 1 (W halves first: issue order inside a K-tile does not matter
+  // for the counted waits, which retire whole K-tiles)
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    if (t < nk) {
+      issue(t, 2);
+      issue(t, 3);
+      issue(t, 0);
+      issue(t, 1);
+    }
+  const int ah = wm;            // the wave's A half (rows 128 * wm ..)
+  const int bh = 2 + (wn >> 1);  // its W half
+  const int brow0 = (wn & 1) * 64;
+  bf16x8 af[2][4], bl[2][2], br[2][2];
+  for (int t = 0; t < nk; ++t) {
+    // ---- q0: K-tile t complete; A top + W left
+    if (t + 1 < nk) wait_vm<8>();
+    else wait_vm<0>();
+    raw_barrier();
+    const bf16x8* sa = slot(t, ah);
+    const bf16x8* sb = slot(t, bh);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = i * 16 + (lane & 15);
+        af[kk][i] = sa[row * C::CH + (chunk ^ (row & 7))];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = brow0 + j * 16 + (lane & 15);
+        bl[kk][j] = sb[row * C::CH + (chunk ^ (row & 7))];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16x16x32(bl[kk][j], af[kk][i], acc[i][j]);
+    // ---- q1: A top + W right
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = brow0 + 32 + j * 16 + (lane & 15);
+        br[kk][j] = sb[row * C::CH + (chunk ^ (row & 7))];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16x16x32(br[kk][j], af[kk][i], acc[i][2 + j]);
+    // ---- q2: every wave is past its q1 reads -> K-tile t+2's W halves go into t's W slots
+    raw_barrier();
+    if (t + 2 < nk) {
+      issue(t + 2, 2);
+      issue(t + 2, 3);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 64 + i * 16 + (lane & 15);
+        af[kk][i] = sa[row * C::CH + (chunk ^ (row & 7))];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16x16x32(br[kk][j], af[kk][i], acc[4 + i][2 + j]);
+    // ---- q3: every wave is past its q2 reads -> K-tile t+2's A halves; A bottom + W left
+    // (both already in registers)
+    raw_barrier();
+    if (t + 2 < nk) {
+      issue(t + 2, 0);
+      issue(t + 2, 1);
+    }
+    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16x16x32(bl[kk][j], af[kk][i], acc[4 + i][j]);
+    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+}
+
 constexpr int kPolStream = 2;  // gfx950 CPol NT (streaming) bit of the DMA's aux operand
 
 // Split rings (BXS > 0): issue order B0 [A0 B1] [A1 B2] ... — iteration t issues
@@ -313,7 +466,9 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   float st_s[C::FM], st_q[C::FM];
 #pragma unroll
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
-  if constexpr (C::BXS > 0)
+  if constexpr (C::RING && !SKIP && !GATHER)  // (grouped expert launches keep the joint ring)
+    mainloop_ring<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, acc);
+  else if constexpr (C::BXS > 0)
     mainloop_split<C, WPOL, SKIP, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
                                   st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), arows);
   else
@@ -1120,6 +1275,9 @@ using C31 = Cfg<192, 128, 2, 2, 2, 0, 1>;  // split rings: 2 x 24 KiB A + 3 x 16
 // DMA-issuing waves per stream bounds these launches.
 using C32 = Cfg<192, 128, 2, 2, 3, 0, 1>;
 using C33 = Cfg<192, 128, 4, 2, 3, 0, 1>;
+// 256 x 256 with the half-tile ring main loop (mainloop_ring): LM heads and the large GEMMs
+using C34 = Cfg<256, 256, 2, 4, 2, 0, 0, 1, 1>;
+using C35 = Cfg<256, 256, 2, 4, 2, 1, 0, 1, 1>;
 
 struct Shape {
   int bm, bn;
@@ -1129,11 +1287,11 @@ constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64
                              {256, 256}, {256, 256}, {256, 128}, {128, 128}, {64, 64},   {64, 64},
                              {128, 64},  {64, 128},  {64, 64},   {64, 64},   {64, 96},   {32, 144},
                              {32, 48},   {64, 96},   {32, 144},  {32, 48},   {128, 128}, {192, 128},
-                             {192, 128}, {192, 128}, {192, 128}, {192, 128}};
+                             {192, 128}, {192, 128}, {192, 128}, {192, 128}, {256, 256}, {256, 256}};
 constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
                           64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128, 128,
-                          64, 128, 64, 64, 64};
-constexpr int kNumCfg = 34;
+                          64, 128, 64, 64, 64, 64, 64};
+constexpr int kNumCfg = 36;
 static_assert(kNumCfg <= kGemmPersist, "config ids must stay below the persistent-launch flag");
 
 // call f(Cfg{}) for config id cfg (unknown ids: C3)
@@ -1173,6 +1331,8 @@ void with_cfg(int cfg, F&& f) {
     case 31: f(C31{}); break;
     case 32: f(C32{}); break;
     case 33: f(C33{}); break;
+    case 34: f(C34{}); break;
+    case 35: f(C35{}); break;
     default: f(C3{}); break;
   }
 }

@@ -261,6 +261,15 @@ __global__ __launch_bounds__(64 * GR_WAVES) void gate_route_kernel(
       }
     }
   }
+  // Hand-off (MI355X_MICROARCH.md, "Valid forms", first row of the sc1 table — measured on
+  // gfx950 / ROCm 7.2, not an architectural guarantee): every logit is stored write-through
+  // (agent-scope relaxed 4-B store = global_store sc1), each storing wave drains its stores,
+  // ONE lane per workgroup adds to the unsharded ticket after the workgroup barrier, and only
+  // the workgroup whose add returns gridDim-1 reads the logits — with sc1 loads (agent-scope
+  // relaxed), so no L1 line can be stale. A release/acquire fence pair would write back and
+  // invalidate this XCD's caches per workgroup (36 us per launch measured with
+  // __threadfence); tests/test_kernels_gpu.py::test_moe_gate_route_many_blocks checks the
+  // hand-off at the largest M (1024 workgroups) with fresh logits every launch, under uneven load.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's logits stores are complete
   __syncthreads();
   if (tid == 0) {
@@ -350,24 +359,30 @@ __global__ __launch_bounds__(256) void gather_combine_kernel(const unsigned long
   const bf16* rrow = r ? r + (size_t)m * H : nullptr;
   const bf16* src[KK];
   float g[KK];
+  bool ok[KK];  // slot j holds a routed expert row (padding slots j >= topk and invalid experts do not)
   const bf16* any_row = nullptr;
 #pragma unroll
   for (int j = 0; j < KK; ++j) {
     src[j] = nullptr;
     g[j] = 0.f;
+    ok[j] = false;
     if (j >= topk) continue;
     const int e = idx[m * topk + j];
     if (e < 0 || e >= E) continue;
     src[j] = reinterpret_cast<const bf16*>(eo_ptrs[e]) + (size_t)(slot_of[m * topk + j] - off[e]) * H;
     g[j] = w[m * topk + j];
+    ok[j] = true;
     any_row = src[j];
   }
-  if (!any_row) any_row = rrow ? rrow : y + (size_t)m * H;  // a row every load may read
+  // a row every unused load may read: a routed row, the residual, or row 0 of expert 0's buffer
+  // (allocated memory) — never the uninitialised output row; what such a load returns is
+  // discarded by a select below (0 * NaN would not be)
+  if (!any_row) any_row = rrow ? rrow : reinterpret_cast<const bf16*>(eo_ptrs[0]);
 #pragma unroll
   for (int j = 0; j < KK; ++j)
-    if (!src[j]) src[j] = any_row;  // weight 0
+    if (!src[j]) src[j] = any_row;
   const bf16* rsrc = rrow ? rrow : any_row;
-  const float rg = rrow ? 1.f : 0.f;
+  const bool has_r = rrow != nullptr;
   const int nv = H / 8;
   bf16x8 v[VPT][KK], rv[VPT];
 #pragma unroll
@@ -385,11 +400,11 @@ __global__ __launch_bounds__(256) void gather_combine_kernel(const unsigned long
     const int c = u * 256 + tid;
     float acc[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = rg * bf2f(rv[u][e]);
+    for (int e = 0; e < 8; ++e) acc[e] = has_r ? bf2f(rv[u][e]) : 0.f;
 #pragma unroll
     for (int j = 0; j < KK; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += g[j] * bf2f(v[u][j][e]);
+      for (int e = 0; e < 8; ++e) acc[e] += ok[j] ? g[j] * bf2f(v[u][j][e]) : 0.f;
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {

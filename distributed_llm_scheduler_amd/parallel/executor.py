@@ -129,7 +129,11 @@ class DAGExecutor:
         self._img_override: Dict[str, torch.Tensor] = {}         # pid -> pinned image
         self._derived_named: Dict[str, tuple] = {}                # weight -> (colsum, bias')
         self._tensor_home: Dict[str, Tuple[str, int]] = {}        # weight -> (pid, byte offset in group)
+        self._refills_memo: Optional[bool] = None
         self._valid: List[Tuple[int, int, str]] = []  # param arena regions holding data
+        # group -> (offset, bytes) its views in _params / _wflat point at; a fill that overwrites
+        # any part of that region unmaps the group (its views would read another group's bytes)
+        self._region: Dict[str, Tuple[int, int]] = {}
         self._inputs: Dict[str, torch.Tensor] = {}
         self._scratch_bufs: Dict[str, torch.Tensor] = {}
         self._moe_memo: Dict[tuple, object] = {}
@@ -204,6 +208,7 @@ class DAGExecutor:
         self._segments: Dict[int, Tuple[int, object]] = {}  # segment start -> (end, hipGraph)
         self._capture_plan: Optional[Dict[int, int]] = None  # set while capture_segments runs
         self._seg_pool = None
+        self._cap_stream = None  # side stream segment captures run on (_capture_segment)
         self._carry_at: Dict[int, List[int]] = {}  # instr -> next step's loads issued after it
         self._carry: Dict[int, object] = {}  # next step's loads already issued -> their events
         self._copy_stream = None
@@ -260,8 +265,11 @@ class DAGExecutor:
         if N is None or not out2d.is_contiguous():
             return None
         W = N.op.weights
-        if any(W[k] not in self._wflat for k in ("w", "b") if k in W):
-            return None  # the norm's weights arrive after this run (first step): it runs itself
+        if not all(self._resident(q) for q in N.params_needed):
+            # the norm's weight group is not mapped with valid bytes right now (it is loaded
+            # after this run, e.g. the first step or a cold-lowered capped program): the
+            # consumer runs the norm itself
+            return None
         y = self._flat(self._views[N.id]) if N.id in self._views else self._scratch("norm", out2d.shape)
         self._pn_done = N.id
         return (y, self._w(W["w"]), self._w(W["b"]) if "b" in W else None, N.op.kind, N.op.attrs.get("eps", 1e-5))
@@ -513,6 +521,31 @@ class DAGExecutor:
             views[spec.name] = self.param_slab[off + sub:off + sub + 2 * n].view(self.dtype).view(spec.shape)
         return off, total, layout, views
 
+    def _map(self, pid: str, off: int, total: int, views) -> None:
+        """Point the group's tensor names at its views in the arena region [off, off+total)."""
+        self._params[pid] = views
+        self._wflat.update(views)
+        self._region[pid] = (off, total)
+
+    def _unmap(self, pid: str) -> None:
+        for name in self._params.pop(pid, {}):
+            self._wflat.pop(name, None)
+        self._region.pop(pid, None)
+
+    def _overwrite(self, off: int, total: int, pid: str) -> None:
+        """Region [off, off+total) is about to receive group ``pid``: every OTHER group mapped
+        over any part of it loses its mapping and its validity (a later reader must load it
+        again; a stale view would silently read ``pid``'s bytes)."""
+        self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
+        for q, (o, n) in list(self._region.items()):
+            if q != pid and o < off + total and off < o + n:
+                self._unmap(q)
+
+    def _resident(self, pid: str) -> bool:
+        """Is group ``pid`` mapped AND do its arena bytes currently hold it?"""
+        r = self._region.get(pid)
+        return r is not None and (r[0], r[1], pid) in self._valid
+
     def _fill(self, off, total, layout, views, pid, stats: StepStats, dma: bool = False) -> bool:
         """Copy the group into its arena region unless the region already holds it. ``dma``:
         through the copy engines even when refills are pulled by a kernel (a copy overlapping
@@ -520,7 +553,7 @@ class DAGExecutor:
         until the copy ends — Llama-3-8B FFN 0.20 -> 0.60 ms beside a 16-block pull)."""
         if (off, total, pid) in self._valid:
             return False  # region still holds this group (steady-state residency)
-        self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
+        self._overwrite(off, total, pid)
         for spec, _ in layout:  # these weights are original again: drop stale folded-norm state
             if spec.name not in self._derived_named:
                 self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
@@ -565,18 +598,17 @@ class DAGExecutor:
 
     def _load(self, instr_index: int, pid: str, stats: StepStats) -> None:
         off, total, layout, views = self._group_views(instr_index, pid)
-        self._params[pid] = views
-        self._wflat.update(views)
         if (off, total, pid) in self._valid:
+            self._map(pid, off, total, views)
             return  # region still holds this group (steady-state residency)
         self._fill(off, total, layout, views, pid, stats)
+        self._map(pid, off, total, views)
 
     def _evict(self, pid: str) -> None:
         """The policy dropped the group: its bytes count as gone (a later load re-fills it even
         if the region was not reused meanwhile), so the executed refill traffic is exactly the
         policy's evict/reload decisions."""
-        for name in self._params.pop(pid, {}):
-            self._wflat.pop(name, None)
+        self._unmap(pid)
         if not VICTIM_REUSE:
             self._valid = [r for r in self._valid if r[2] != pid]
 
@@ -644,12 +676,24 @@ class DAGExecutor:
                 self._persist_transform(w_name, W, d)
         return W, d[0], d[1]
 
+    def _refills(self) -> bool:
+        """Does this rank's program re-fill any parameter group after its first step (steady-state
+        host refills, or groups received from a peer)?"""
+        if self._refills_memo is None:
+            from .program import steady_fill_bytes
+            pb = {pid: group_layout(g)[0] for pid, g in self.store.groups.items()}
+            self._refills_memo = (steady_fill_bytes(self.prog, pb) > 0
+                                  or any(i.op == "load" and i.peer >= 0 for i in self.prog.instrs))
+        return self._refills_memo
+
     def _persist_transform(self, w_name: str, W: torch.Tensor, d: tuple) -> None:
         """Write the transformed weight into a private copy of its group's host image (pinned
         on GPU; once, in an eager step). Every later refill — from the host image, or from a
         peer that holds the group in the same form — then carries the transformed bytes."""
         if self.gpu and torch.cuda.is_current_stream_capturing():
             return
+        if not self._refills():
+            return  # nothing is ever re-filled: a private (pinned) host image would be dead weight
         if not self._tensor_home:
             for gid, grp in self.store.groups.items():
                 for spec, sub in group_layout(grp)[1]:
@@ -911,8 +955,7 @@ class DAGExecutor:
                 o, total, layout, views = self._views_at(off, pid)
                 if first:  # one-time fill before the first step
                     self._fill(o, total, layout, views, pid, stats)
-                self._params[pid] = views
-                self._wflat.update(views)
+                self._map(pid, o, total, views)
         self._started = True
         if self._stats_slab is not None and not self._zero_in_embedding:
             self._stats_slab.zero_()
@@ -942,12 +985,7 @@ class DAGExecutor:
                 if i in segs:
                     segs[i][1].replay()
                 else:  # capture_segments: record this segment's kernels
-                    g = torch.cuda.CUDAGraph()
-                    # thread-local capture: RCCL's watchdog thread keeps querying its events
-                    with torch.cuda.graph(g, pool=self._seg_pool, capture_error_mode="thread_local"):
-                        for k in range(i, seg_end):
-                            self._issue_run(k, self.prog.instrs[k], stats, None)
-                    self._segments[i] = (seg_end, g)
+                    self._segments[i] = (seg_end, self._capture_segment(i, seg_end, stats))
                 stats.kernels += seg_end - i
                 i = seg_end - 1
                 ins = self.prog.instrs[i]
@@ -961,8 +999,7 @@ class DAGExecutor:
                 self._peer_load(i, ins, stats)
             elif ins.op == "load" and hoist is not None and i in pending:
                 off, total, layout, views = self._group_views(i, ins.param)
-                self._params[ins.param] = views
-                self._wflat.update(views)
+                self._map(ins.param, off, total, views)
                 done = pending.pop(i)
                 if done is not None:  # the compute stream waits at the group's first reader
                     self._await[ins.param] = done
@@ -1081,9 +1118,8 @@ class DAGExecutor:
         """Load a parameter group by receiving it from the peer that holds it."""
         self._wait_sends(ins)
         off, total, layout, views = self._group_views(i, ins.param)
-        self._params[ins.param] = views
-        self._wflat.update(views)
-        self._valid = [r for r in self._valid if r[0] + r[1] <= off or off + total <= r[0]]
+        self._overwrite(off, total, ins.param)
+        self._map(ins.param, off, total, views)
         for spec, _ in layout:
             if spec.name not in self._derived_named:
                 self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
@@ -1222,6 +1258,29 @@ class DAGExecutor:
             segs.append((i, j))
             i = j
         return segs
+
+    def _capture_segment(self, i: int, seg_end: int, stats: StepStats):
+        """Record runs [i, seg_end) into a hipGraph WITHOUT a device-wide synchronize
+        (``torch.cuda.graph`` synchronizes on entry, which would make every eager isend /
+        irecv / parameter send posted earlier in this step host-blocking — two ranks exchanging
+        in opposite directions could then wait on each other at capture). The capture runs on
+        a side stream ordered after the compute stream; the compute stream waits for it."""
+        g = torch.cuda.CUDAGraph()
+        cur = torch.cuda.current_stream(self.device)
+        if self._cap_stream is None:
+            self._cap_stream = torch.cuda.Stream(self.device)
+        cs = self._cap_stream
+        cs.wait_stream(cur)
+        with torch.cuda.stream(cs):
+            # thread-local capture mode: RCCL's watchdog thread keeps querying its events
+            g.capture_begin(pool=self._seg_pool, capture_error_mode="thread_local")
+            try:
+                for k in range(i, seg_end):
+                    self._issue_run(k, self.prog.instrs[k], stats, None)
+            finally:
+                g.capture_end()
+        cur.wait_stream(cs)
+        return g
 
     def capture_segments(self) -> bool:
         """Piecewise capture for programs that must stay eager around RCCL p2p or copy-stream

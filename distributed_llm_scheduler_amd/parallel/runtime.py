@@ -64,6 +64,10 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         shard-sum / residual / embedding / head nodes on GPU 0 (tensor parallelism).
       * ``"sequence"``  — with ``sp > 1``: sequence chunk c of every node on GPU c % world
         (context parallelism; the K/V edges between chunks are the cross-GPU transfers).
+      * ``"expert"``    — MoE models: expert e of every layer on GPU e % world, everything
+        else of request r on its home GPU r % world (expert parallelism: the router ->
+        expert edges carry each expert's routed token rows, the expert -> combine edges its
+        compact outputs).
     The fixed placements still go through the scheduler's memory accounting (tasks that
     do not fit fail exactly as in the policies).
 
@@ -106,7 +110,7 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         sched, schedule = _resume(resume, args, sched)
     elif placement == "scheduler":
         schedule = sched.schedule()
-    elif placement in ("replica", "pipeline", "tensor", "sequence"):
+    elif placement in ("replica", "pipeline", "tensor", "sequence", "expert"):
         schedule = _fixed_schedule(tasks, world, sched, placement, cfg)
     else:
         raise ValueError(f"unknown placement {placement!r}")
@@ -216,9 +220,11 @@ def _fixed_schedule(tasks: Sequence[Task], world: int, sched, mode: str, cfg) ->
     nodes = list(sched.nodes.values())
     L = cfg.n_layer
     for t in tasks:
-        if mode == "replica":
+        if mode in ("replica", "expert"):
             rep = int(t.id.split("/")[0][1:]) if "/" in t.id else 0
             r = rep % world
+            if mode == "expert" and t.op is not None and t.op.kind == "moe_expert":
+                r = t.op.attrs["expert"] % world
         elif mode in ("tensor", "sequence"):
             tag = "tp" if mode == "tensor" else "sp"
             sfx = t.id.rsplit(".", 1)[-1] if "." in t.id.split("/")[-1] else ""

@@ -53,3 +53,52 @@ def test_bench_two_ranks_gloo():
                   "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *ARGS])
     assert len(lines) == 1  # rank 0 only
     _check(lines[0], 2)
+
+
+def _torchrun(n, args):
+    return _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+                 "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n), *args])
+
+
+MINI = ["--seq", "16", "--steps", "1", "--warmup", "1", "--no-extras"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("config", ["gpt2m_cap", "llama_pipeline", "mixtral_expert"])
+def test_bench_baseline_multi_gpu_configs(world, config):
+    """BASELINE.json configs 3-5 as bench.py commands, at mini scale over 2 / 4 / 8 gloo ranks:
+    ONE request DAG spanning the GPUs (--replicas 1) or pipeline micro-batches, each printing one
+    JSON line with tasks completed and real cross-GPU edges / bytes.
+      3: GPT-2-medium across 2 GPUs under an artificial cap  (--cap-gb, --replicas 1)
+      4: Llama-3-8B pipeline placement                       (--placement pipeline)
+      5: Mixtral-8x7B experts across GPUs                     (--placement expert --replicas 1)"""
+    args = {
+        # the reference's policy under a cap that binds (evictions + re-fills) spreads the DAG
+        "gpt2m_cap": ["--model", "tiny-gpt2", "--replicas", "1", "--cap-gb", "0.0001", "--cost-model", "bytes",
+                      "--scheduler", "MRU_spec"],
+        "llama_pipeline": ["--model", "tiny-llama", "--placement", "pipeline"],
+        "mixtral_expert": ["--model", "tiny-mixtral", "--placement", "expert", "--replicas", "1"],
+    }[config]
+    lines = _torchrun(world, args + MINI)
+    assert len(lines) == 1
+    ln = lines[0]
+    assert ln["n_gpus"] == world and ln["rccl_world"] == world and len(ln["per_rank_ms"]) == world
+    assert ln["tasks_completed"] == ln["tasks_total"] > 0
+    assert ln["cross_gpu_edges"] > 0 and ln["cross_gpu_bytes"] > 0, "the DAG must span GPUs"
+    assert ln["value"] == max(ln["per_rank_ms"])
+
+
+@pytest.mark.timeout(600)
+def test_bench_extras_two_ranks():
+    """Default extras over 2 gloo ranks: the executed 80 % regime (MRU_spec / EFT / DFS) and the
+    strong-scaling pipeline run with cross-GPU edges."""
+    lines = _torchrun(2, ["--model", "tiny-gpt2", "--seq", "16", "--steps", "1", "--warmup", "1",
+                          "--extra-steps", "1", "--strong-mb", "4"])
+    ln = lines[0]
+    cap = ln["capped"]
+    assert cap["memory_regime"] == 0.8 and cap["cost_model"] == "reference"
+    for s in ("MRU_spec", "EFT", "DFS"):
+        assert cap[s]["ms_per_step"] > 0 and cap[s]["tasks_total"] > 0
+    assert cap["MRU_spec"]["tasks_completed"] == cap["MRU_spec"]["tasks_total"]
+    assert ln["strong"]["cross_gpu_edges"] > 0 and ln["strong"]["micro_batches"] == 4

@@ -375,3 +375,53 @@ def test_post_norm_under_memory_cap(sched):
         ex.step()
     err, scale = _ref_check(p, ex, store)
     assert err < 0.03 * scale, (err, scale)
+
+
+@pytest.mark.parametrize("model,sched,frac", [("tiny-mixtral", "EFT", 0.35), ("tiny-mixtral", "EFT", 0.6),
+                                              ("tiny-mixtral", "MRU_spec", 0.8), ("tiny-llama", "EFT", 0.7),
+                                              ("tiny-llama", "MRU_spec", 0.8)])
+def test_post_norm_never_reads_stale_weights(model, sched, frac):
+    """Cold-lowered capped programs (every step planned from an empty arena, residency
+    'trace') load the norm's weight group BETWEEN the producer P and the consumer Q of a
+    post-norm pair, and an earlier load can land on the region the group held in the previous
+    step. The producer may write the norm only while the group's mapped bytes are really its
+    own: every post-norm the producer writes uses weights equal to the store's, for 3 steps,
+    and the outputs match the fp32 reference."""
+    from distributed_llm_scheduler_amd.models import registry
+    from distributed_llm_scheduler_amd.models.params import group_layout
+    from distributed_llm_scheduler_amd.parallel.executor import DAGExecutor
+
+    _, groups, _ = registry.build(model, batch=1, seq=16)
+    total = sum(group_layout(g)[0] for g in groups.values()) / 1e9
+    p = runtime.plan(model, world=1, scheduler=sched, seq=16, cap_gb=total * frac, residency="trace")
+    assert p.completed == p.total and p.programs[0].residency == "cold"
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, "cpu", store)
+    ins = p.programs[0].instrs
+    between = 0
+    for i, N in ex._post_norm.items():
+        j = next(j for j, q in ex._norm_given.items() if q == N.id)
+        between += any(ins[k].op == "load" and ins[k].param in N.params_needed for k in range(i + 1, j))
+    assert between > 0, "no post-norm pair with its norm group loaded between producer and consumer"
+    written = []
+    orig = DAGExecutor._post_norm_out
+
+    def checked(self, out2d):
+        r = orig(self, out2d)
+        if r is not None:
+            W = self._pn.op.weights
+            for k in ("w", "b"):
+                if k in W:
+                    assert torch.equal(self._w(W[k]), store.tensor(W[k]).to(self._w(W[k]).dtype)), \
+                        f"post-norm of {self._pn.id} would read stale {k}"
+            written.append(self._pn.id)
+        return r
+
+    ex._post_norm_out = checked.__get__(ex)
+    for _ in range(3):
+        ex.step()
+    err, scale = _ref_check(p, ex, store)
+    assert err < 0.03 * scale, (err, scale)
+    for q, (o, n) in ex._region.items():  # no two mapped groups share arena bytes
+        for q2, (o2, n2) in ex._region.items():
+            assert q == q2 or o + n <= o2 or o2 + n2 <= o, (q, q2)

@@ -49,7 +49,8 @@ def test_gemm_identity_asymmetric():
                                            (16, 1), (17, 1), (18, 1), (19, 1), (16, 2), (17, 3), (80, 1),
                                            (20, 1), (21, 1), (21, 3), (22, 1), (23, 1), (24, 1),
                                            (25, 1), (26, 1), (27, 1), (22, 4), (24, 2), (27, 3), (28, 1), (28, 2),
-                                           (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2)])
+                                           (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2),
+                                           (34, 1), (35, 1), (34, 2), (34, 3), (98, 1)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
@@ -364,6 +365,31 @@ def test_moe_gate_route_fused(M, E, k, H):
         assert torch.equal(a, b)
 
 
+def test_moe_gate_route_many_blocks():
+    """The one-launch router hands the logits of 1024 workgroups to the last arriver without a
+    fence (sc1 stores / ticket / sc1 loads): at the largest M the fused kernel takes, with new
+    logits every launch (the last block's L1 still holds the previous launch's lines) and a GEMM
+    on another stream loading the chip unevenly, the routing equals moe_route over the logits
+    written."""
+    M, E, k, H = 2048, 8, 2, 1024
+    wg = _rand(E, H, scale=0.05, seed=8)
+    logits = torch.empty(M, E, dtype=torch.bfloat16, device=DEV)
+    side = torch.cuda.Stream()
+    a, b = _rand(4096, 4096, seed=1), _rand(4096, 4096, seed=2)
+    for it in range(8):
+        x = _rand(M, H, seed=100 + it)
+        with torch.cuda.stream(side):
+            torch.matmul(a, b)
+        r = ops.moe_gate_route(x, wg, k, logits)
+        torch.cuda.synchronize()
+        assert r is not None
+        ref = ops.moe_route(logits, k, E)
+        torch.cuda.synchronize()
+        for u, v in zip(r, ref):
+            assert torch.equal(u, v), f"launch {it}: routing differs from the published logits"
+        _close(logits.cpu().float(), ops.ref_linear(x.cpu(), wg.cpu()).float(), 2e-2)
+
+
 @pytest.mark.parametrize("config", [-1, 3, 17, 30, 31, 33])
 def test_gemm_grouped_gathered_rows(config):
     """Gate/up grouped GEMM reading its expert-sorted rows straight from the token matrix
@@ -418,6 +444,34 @@ def test_moe_gather_combine():
     _close(y.cpu().float(), exp, 1e-2)
 
 
+def test_moe_gather_combine_no_nan_from_unused_rows():
+    """Top-3 (padded expert slots) and no residual: the padding slots and every row past an
+    expert's routed count hold Inf, the output buffer holds NaN before the launch — none of it
+    may leak into the combined rows (unused loads are discarded by select, not weighted by 0)."""
+    M, E, k, H = 257, 8, 3, 512
+    g = torch.Generator().manual_seed(91)
+    logits = torch.randn(M, E, generator=g).to(torch.bfloat16)
+    idx, gate = ops.moe_router(logits, k)
+    src, slot, off = ops.moe_align(idx, E)
+    counts = (off[1:] - off[:-1]).tolist()
+    experts = []
+    for e in range(E):
+        t = torch.randn(M, H, generator=g).to(torch.bfloat16)
+        t[counts[e]:] = float("inf")
+        experts.append(t)
+    exp = torch.zeros(M, H)
+    for m in range(M):
+        for j in range(k):
+            e = int(idx[m, j])
+            exp[m] += float(gate[m, j]) * experts[e][int(slot[m * k + j]) - int(off[e])].float()
+    out = torch.full((M, H), float("nan"), dtype=torch.bfloat16, device=DEV)
+    y = ops.moe_gather_combine([t.to(DEV) for t in experts], idx.to(DEV), slot.to(DEV), off.to(DEV), gate.to(DEV),
+                               residual=None, out=out)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(y.float()).all())
+    _close(y.cpu().float(), exp, 1e-2)
+
+
 @pytest.mark.parametrize("config,splitk", [(-1, 0), (3, 1), (0, 2), (3, 4), (8, 1)])
 def test_gemm_rope_epilogue(config, splitk):
     B, S, nh, nkv, D, H = 2, 128, 4, 2, 128, 512
@@ -443,7 +497,7 @@ def test_gemm_rope_epilogue(config, splitk):
 
 
 @pytest.mark.parametrize("N", [768, 4096])
-@pytest.mark.parametrize("config,splitk", [(3, 1), (3, 3), (0, 1), (8, 2), (100, 1)])
+@pytest.mark.parametrize("config,splitk", [(3, 1), (3, 3), (0, 1), (8, 2), (100, 1), (34, 1), (34, 2)])
 def test_gemm_emits_row_stats(config, splitk, N):
     M, K = 300, 768
     x, w = _rand(M, K, seed=100), _rand(N, K, scale=0.05, seed=101)
@@ -458,7 +512,8 @@ def test_gemm_emits_row_stats(config, splitk, N):
 
 
 @pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
-@pytest.mark.parametrize("config,splitk,act", [(3, 1, 0), (3, 4, 1), (0, 2, 0), (8, 1, 0), (12, 2, 0), (3, 1, 4)])
+@pytest.mark.parametrize("config,splitk,act", [(3, 1, 0), (3, 4, 1), (0, 2, 0), (8, 1, 0), (12, 2, 0), (3, 1, 4),
+                                               (34, 1, 0), (34, 2, 1), (35, 1, 0)])
 def test_gemm_folded_norm_external_stats(mode, config, splitk, act):
     M, N, K = 256, 1024, 2048
     x = _rand(M, K, scale=2.0, seed=110) + 0.3

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--marker", default="embedding_kernel")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--per-dispatch", action="store_true",
+                    help="also list every dispatch of the last step in order (duration, gap to the previous end)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -52,6 +54,17 @@ def main():
     print(f"{'kernel':60s} {'grid/block':>22s} {'calls':>6s} {'mean_us':>9s} {'us/step':>9s} {'%':>5s}")
     for (k, g), (n, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:a.top]:
         print(f"{k:60s} {g:>22s} {n / nst:6.1f} {t / n:9.2f} {t / nst:9.1f} {100 * t / busy:5.1f}")
+    if a.per_dispatch:
+        last = rows[starts[-2]:starts[-1]] if len(starts) >= 2 else sel
+        print(f"\nlast step, {len(last)} dispatches in order:")
+        print(f"{'#':>3s} {'kernel':60s} {'grid/block':>22s} {'us':>8s} {'gap_us':>7s}")
+        prev = None
+        for i, r in enumerate(last):
+            s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            gap = (s0 - prev) / 1e3 if prev is not None else 0.0
+            prev = e0
+            g = f'{r["Grid_Size_X"]}x{r["Grid_Size_Y"]}x{r["Grid_Size_Z"]}/{r["Workgroup_Size_X"]}'
+            print(f"{i:3d} {short(r['Kernel_Name']):60s} {g:>22s} {(e0 - s0) / 1e3:8.2f} {gap:7.2f}")
 
 
 if __name__ == "__main__":
