@@ -74,6 +74,15 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 // in blocks of 16 (W' rows 32c..32c+15 = gate 16c.., 32c+16..32c+31 = up 16c..); output N/2 wide
 enum DlsAct : int { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_SILU = 2, ACT_RELU = 3, ACT_SWIGLU = 4 };
 
+// compile-time activation (epilogues instantiated per activation: no per-value branch)
+template <int ACT>
+__device__ __forceinline__ float act_c(float v) {
+  if constexpr (ACT == ACT_GELU_TANH) return gelu_tanh(v);
+  else if constexpr (ACT == ACT_SILU) return silu(v);
+  else if constexpr (ACT == ACT_RELU) return fmaxf(v, 0.f);
+  else return v;
+}
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {
     case ACT_GELU_TANH: return gelu_tanh(v);

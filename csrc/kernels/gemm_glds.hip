@@ -18,8 +18,15 @@
 //    to a workspace slab and a vectorised reduce kernel applies the fused epilogue.
 //  * XCD-aware tile order (T1): the blocks of one weight panel share an XCD's L2.
 #include <cstdlib>
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
+
+// In-kernel phase stamps for diagnostic builds (benchmarks/gemm_stamps.hip defines it before
+// including this file); empty in the library.
+#ifndef DLS_STAMP
+#define DLS_STAMP(k)
+#endif
 
 namespace {
 
@@ -452,6 +459,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   const int wm = wq / C::WN, wn = wq % C::WN;
   const int m0 = tm * C::BM, n0 = tn * C::BN;
   if (m0 >= M) return;  // whole block idle (uniform: before any barrier)
+  DLS_STAMP(0)
   const int kbeg = ks * kslice;
   const int nk = kslice / (C::BK * C::KG);
 
@@ -474,6 +482,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   else
     mainloop_joint<C, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
                       st_q, arows);
+  DLS_STAMP(1)
   if constexpr (C::KG > 1) {
     // sum the K groups' accumulators into group 0 (lane-contiguous 16-B records)
     __syncthreads();
@@ -698,48 +707,75 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
                 "store pass: every wave makes the same number of passes (shuffles stay wave-uniform)");
   bf16* img = reinterpret_cast<bf16*>(smem);
   __syncthreads();  // every wave is done with the staging buffers (and the norm statistics)
+  // The activation / folded-norm / RoPE choice is made ONCE per tile and the fragment pass is
+  // instantiated per combination: a runtime switch per output value (apply_act) unrolled over
+  // the 128 values per lane of a 256 x 256 tile compiled to ~25k instructions of branches
+  // around inlined GeLU / SiLU bodies, and the instruction fetches of jumping through them made
+  // this pass take 19.5 us per tile on MI355X (benchmarks/gemm_stamps.hip) — 3x the main loop
+  // of the GPT-2 LM head.
+  auto image_pass = [&](auto act_tag, auto ln_tag, auto rope_tag) {
+    constexpr int ACT = decltype(act_tag)::value;
+    constexpr bool LNM = decltype(ln_tag)::value, ROPE = decltype(rope_tag)::value;
 #pragma unroll
-  for (int j = 0; j < C::FN; ++j) {
-    if (kgrp != 0) break;  // K group 0 holds the summed tile
-    const int cl = wn * C::WTN + j * 16 + g4;  // local column of this lane's 4 values
-    const int col = n0 + cl;
-    const bool full = col + 3 < N;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    float csv[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(W') of the 4 columns (folded norm)
-    if (bias) {
+    for (int j = 0; j < C::FN; ++j) {
+      if (kgrp != 0) break;  // K group 0 holds the summed tile
+      const int cl = wn * C::WTN + j * 16 + g4;  // local column of this lane's 4 values
+      const int col = n0 + cl;
+      const bool full = col + 3 < N;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      float csv[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(W') of the 4 columns (folded norm)
+      if (bias) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
-    }
-    if (ln_mode != 0) {
-      if (full && (N % 4 == 0)) {
-        const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_colsum + col);
+        for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
+      }
+      if constexpr (LNM) {
+        if (full && (N % 4 == 0)) {
+          const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_colsum + col);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) csv[e] = c4[e];
-      } else {
+          for (int e = 0; e < 4; ++e) csv[e] = c4[e];
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) csv[e] = col + e < N ? ln_colsum[col + e] : 0.f;
+          for (int e = 0; e < 4; ++e) csv[e] = col + e < N ? ln_colsum[col + e] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int rl = wm * C::WTM + i * 16 + r16;
+        float v[4];
+        if constexpr (LNM) {
+          // W.LN(x) = rstd * (W' x - mu * colsum(W')) + (bias + W b), W' = W * ln_w (host-derived)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act_c<ACT>(ln_rs[i] * (acc[i][j][e] - ln_mu[i] * csv[e]) + bv[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act_c<ACT>(alpha * acc[i][j][e] + bv[e]);
+        }
+        if constexpr (ROPE) rope_pairs<4>(v, m0 + rl, col, rope);
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<bf16x4*>(img + rl * BNP * 8 + (((cl >> 3) ^ (rl & 7)) << 3) + (cl & 7)) = o;
       }
     }
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      const int rl = wm * C::WTM + i * 16 + r16;
-      float v[4];
-      if (ln_mode != 0) {
-        // W.LN(x) = rstd * (W' x - mu * colsum(W')) + (bias + W b), W' = W * ln_w (host-derived)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(ln_rs[i] * (acc[i][j][e] - ln_mu[i] * csv[e]) + bv[e], act);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(alpha * acc[i][j][e] + bv[e], act);
-      }
-      if (rope.cols) rope_pairs<4>(v, m0 + rl, col, rope);
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-      *reinterpret_cast<bf16x4*>(img + rl * BNP * 8 + (((cl >> 3) ^ (rl & 7)) << 3) + (cl & 7)) = o;
+  };
+  using B0 = std::integral_constant<bool, false>;
+  using B1 = std::integral_constant<bool, true>;
+  auto by_ln = [&](auto act_tag, auto rope_tag) {
+    if (ln_mode != 0) image_pass(act_tag, B1{}, rope_tag);
+    else image_pass(act_tag, B0{}, rope_tag);
+  };
+  if (rope.cols) {
+    by_ln(std::integral_constant<int, ACT_NONE>{}, B1{});  // RoPE epilogues carry no activation
+  } else {
+    switch (act) {
+      case ACT_GELU_TANH: by_ln(std::integral_constant<int, ACT_GELU_TANH>{}, B0{}); break;
+      case ACT_SILU: by_ln(std::integral_constant<int, ACT_SILU>{}, B0{}); break;
+      case ACT_RELU: by_ln(std::integral_constant<int, ACT_RELU>{}, B0{}); break;
+      default: by_ln(std::integral_constant<int, ACT_NONE>{}, B0{}); break;
     }
   }
   __syncthreads();
+  DLS_STAMP(2)
   const bool v16 = ((reinterpret_cast<uintptr_t>(Cp) | ((uintptr_t)ldc * 2)) & 15) == 0 &&
                    (!R || ((reinterpret_cast<uintptr_t>(R) | ((uintptr_t)ldr * 2)) & 15) == 0);
   const bf16x8* img8 = reinterpret_cast<const bf16x8*>(img);
@@ -791,6 +827,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
       }
     }
   }
+  DLS_STAMP(3)
 }
 
 // LN / RANGED are compile-time switches: a kernel instance carries only the epilogue and

@@ -170,8 +170,8 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                     rope_cos->numel() >= rope_S * rope_D / 2 && rope_sin->numel() >= rope_S * rope_D / 2,
                 "RoPE epilogue: cos/sin fp32 [S][D/2]");
     TORCH_CHECK(rope_D % 4 == 0 && rope_cols % rope_D == 0 && rope_cols <= N && !swiglu && K % 64 == 0 &&
-                    !rows.has_value(),
-                "RoPE epilogue: D % 4 == 0, whole heads, LDS-DMA kernel, no SwiGLU / row range");
+                    !rows.has_value() && act == 0,
+                "RoPE epilogue: D % 4 == 0, whole heads, LDS-DMA kernel, no activation / SwiGLU / row range");
     g.rope = RopeArgs{rope_cos->data_ptr<float>(), rope_sin->data_ptr<float>(), (int)rope_S, (int)rope_D,
                       (int)rope_cols};
     if (config >= kRegStage) config = -1;

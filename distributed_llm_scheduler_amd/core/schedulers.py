@@ -199,7 +199,8 @@ class BaseScheduler:
         inst.node_ids = [n.id for n in node_list]
         inst.node_mem = [float(n.total_memory) for n in node_list]
         inst.node_speed = [float(n.compute_speed) for n in node_list]
-        inst.out_size = [float(getattr(self.tasks[t], "out_bytes", 0) or 0) / 1e9 for t in ids]
+        inst.out_size = [float(getattr(self.tasks[t], "xfer_bytes", getattr(self.tasks[t], "out_bytes", 0)) or 0) / 1e9
+                         for t in ids]
         self._configure_instance(inst)
         return inst, ids, pnames, node_list
 

@@ -58,11 +58,12 @@ class Task:
     node's cache after use)."""
 
     __slots__ = ("id", "memory_required", "compute_time", "dependencies", "params_needed",
-                 "completed", "assigned_node", "op", "out_bytes", "flops")
+                 "completed", "assigned_node", "op", "out_bytes", "flops", "edge_bytes")
 
     def __init__(self, task_id: str, memory_required: float, compute_time: float,
                  dependencies: Optional[List[str]] = None, params_needed: Optional[Set[str]] = None,
-                 op: Optional[OpSpec] = None, out_bytes: int = 0, flops: float = 0.0):
+                 op: Optional[OpSpec] = None, out_bytes: int = 0, flops: float = 0.0,
+                 edge_bytes: Optional[int] = None):
         self.id = task_id
         self.memory_required = memory_required
         self.compute_time = compute_time
@@ -73,6 +74,15 @@ class Task:
         self.op = op
         self.out_bytes = out_bytes
         self.flops = flops
+        # bytes one cross-GPU edge out of this task moves, when that is less than its whole
+        # output buffer (``out_bytes``, the activation arena size): an MoE expert returns only
+        # its routed rows, the routed hidden state ships each expert only its rows. Transfer
+        # costs (EFT) use it; None = out_bytes
+        self.edge_bytes = edge_bytes
+
+    @property
+    def xfer_bytes(self) -> int:
+        return self.out_bytes if self.edge_bytes is None else self.edge_bytes
 
     def __repr__(self) -> str:
         return (f"Task({self.id!r}, mem={self.memory_required:.3f}GB, t={self.compute_time:.3f}s, "
@@ -89,19 +99,21 @@ class Task:
         """Fresh, un-executed copy (the harness deep-copies before every run,
         ``/root/reference/simulation.py:308-317``)."""
         return Task(self.id, self.memory_required, self.compute_time, list(self.dependencies),
-                    set(self.params_needed), self.op, self.out_bytes, self.flops)
+                    set(self.params_needed), self.op, self.out_bytes, self.flops, self.edge_bytes)
 
     def to_dict(self) -> Dict[str, Any]:
         return {"id": self.id, "memory_required": self.memory_required, "compute_time": self.compute_time,
                 "dependencies": list(self.dependencies), "params_needed": sorted(self.params_needed),
                 "out_bytes": int(self.out_bytes), "flops": float(self.flops),
+                **({"edge_bytes": int(self.edge_bytes)} if self.edge_bytes is not None else {}),
                 "op": self.op.to_dict() if self.op is not None else None}
 
     @staticmethod
     def from_dict(d: Dict[str, Any]) -> "Task":
         op = OpSpec.from_dict(d["op"]) if d.get("op") else None
         return Task(d["id"], d["memory_required"], d["compute_time"], list(d.get("dependencies", [])),
-                    set(d.get("params_needed", [])), op, int(d.get("out_bytes", 0)), float(d.get("flops", 0.0)))
+                    set(d.get("params_needed", [])), op, int(d.get("out_bytes", 0)), float(d.get("flops", 0.0)),
+                    d.get("edge_bytes"))
 
 
 class Node:

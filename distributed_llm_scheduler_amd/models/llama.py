@@ -116,6 +116,14 @@ def build_llama_dag(cfg: "ModelConfig | str" = "llama3-8b", batch: int = 1, seq:
                            {"expert": e, "n_experts": E, "top_k": K, "ffn": F}, shape),
                     6.0 * rows * H * F, extra=M * K * (H + 3 * F) * dtype_bytes)
                 experts.append(f"layer_{i}_expert_{e}")
+            # a cross-GPU edge into or out of an expert moves only its routed rows (M*K/E
+            # expected): the executor ships each expert GPU exactly its experts' token rows and
+            # returns their compact outputs (program.py routed transfers)
+            rows_b = int(round(M * K / E)) * H * dtype_bytes
+            byid = {t.id: t for t in tasks[-(E + 2):]}
+            byid[tid(f"layer_{i}_ffn_norm")].edge_bytes = rows_b
+            for x in experts:
+                byid[tid(x)].edge_bytes = rows_b
             # combine = residual + gate-weighted gather of the experts' compact outputs; the
             # router edge carries the (tiny) logits so routing is known wherever this runs
             add(f"layer_{i}_output", 0.01, experts + [f"layer_{i}_router", f"layer_{i}_attn_residual"], [],

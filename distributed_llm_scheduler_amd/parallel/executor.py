@@ -49,12 +49,28 @@ class StepStats:
     sends: int = 0
     recvs: int = 0
     bytes_sent: int = 0
+    bytes_recv: int = 0
     param_fills: int = 0
     bytes_filled: int = 0
     peer_fills: int = 0   # parameter groups received from a peer's HBM over xGMI
     bytes_peer: int = 0
     timeline: List[Tuple[str, float, float]] = field(default_factory=list)  # (group, start_ms, end_ms)
     events: List[Tuple[str, str, float, float]] = field(default_factory=list)  # (name, category, start, end)
+
+
+class _Works:
+    """Several RCCL p2p works (the routed rows of one expert-parallel edge) waited as one; keeps
+    the sent / received views alive until then."""
+
+    def __init__(self, works, keep=()):
+        self.works = list(works)
+        self.keep = list(keep)
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+        self.keep = []
 
 
 def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.Tensor:
@@ -122,6 +138,14 @@ class DAGExecutor:
         self._params: Dict[str, Dict[str, torch.Tensor]] = {}  # pid -> {tensor name -> view}
         self._wflat: Dict[str, torch.Tensor] = {}               # tensor name -> resident view
         self._derived_cache: Dict[tuple, tuple] = {}             # (weight, ptr) -> (colsum, bias') for folded norms
+        # weights read by more than one task (GPT-2's tied wte: embedding gather + LM head) are
+        # never transformed in place: their folded form lives in a private buffer
+        self._side: Dict[str, torch.Tensor] = {}                 # weight -> private derived copy
+        self._w_users: Dict[str, int] = {}
+        for t in tasks:
+            if t.op is not None:
+                for v in set(x for x in t.op.weights.values() if isinstance(x, str)):
+                    self._w_users[v] = self._w_users.get(v, 0) + 1
         # GPU, host-image refills: a transformed weight's bytes are written back into a private
         # copy of its group's pinned image, so every later refill restores the TRANSFORMED
         # weight and its (colsum, bias') stay valid wherever the group lands (no re-derivation
@@ -141,6 +165,10 @@ class DAGExecutor:
         self._ext_stats: Dict[str, torch.Tensor] = {}   # the same buffers, by the tensor a norm reads
         self._stats_slab: Optional[torch.Tensor] = None
         self._moe_ptrs: Dict[tuple, torch.Tensor] = {}
+        # expert-parallel programs route eagerly (outside captured segments) while the expert
+        # kernels replay from a hipGraph: the routing then lives in fixed buffers per router
+        self._route_persist = any(i.route is not None for i in program.instrs)
+        self._route_bufs: Dict[str, tuple] = {}
         self._pending_sends: Dict[int, object] = {}  # send instruction index -> RCCL work
         self._param_recv: Dict[str, object] = {}     # group -> RCCL work of its peer fill
         self._started = False
@@ -221,8 +249,8 @@ class DAGExecutor:
         self._pn: Optional[Task] = None        # set by _issue_run for the run in flight
         self._pn_given: Optional[str] = None   # its consumer: the norm its producer wrote (if it did)
         self._pn_done: Optional[str] = None    # the norm the last producer actually wrote
-        if POST_NORM not in ("0", False) and self._copy_stream is None and not p.has_comm:
-            self._plan_post_norm()
+        if POST_NORM not in ("0", False) and self._copy_stream is None:
+            self._plan_post_norm()  # (pairs are adjacent runs: no p2p between producer and consumer)
 
     def _plan_post_norm(self) -> None:
         """Pair each norm that the next group would run as its own pass (its width is above
@@ -279,16 +307,17 @@ class DAGExecutor:
         program (only parameter loads between them), runs as ONE grouped launch pair (gate/up
         with SwiGLU, then down) instead of two GEMMs per expert: grid = experts x column
         tiles, so the layer's whole expert weight stream is one chip-wide launch. GPU only,
-        all experts of the layer here, and a program without evictions or p2p (parameters
-        never move, so the span's loads can be applied at the batch's first node)."""
+        all experts of the layer here, and a program without evictions or peer parameter
+        loads (parameters never move, so the span's loads can be applied at the batch's first
+        node); activation p2p elsewhere in the program does not matter."""
         self._moe_batch: Dict[int, Tuple[List[int], List[int]]] = {}
         self._moe_skip: set = set()
         self._moe_batched_ids: set = set()
         self._moe_bufs: Dict[int, tuple] = {}
         self._gate_route: Dict[str, Tuple[int, int]] = {}  # router task -> (E, top-k): GEMM + routing fused
         ins = self.prog.instrs
-        if not self.gpu or not MOE_BATCH or any(i.op in ("evict", "send", "recv") for i in ins):
-            return
+        if not self.gpu or not MOE_BATCH or any(i.op == "evict" or (i.op == "load" and i.peer >= 0) for i in ins):
+            return  # (p2p elsewhere in the program is fine: parameters never move)
 
         def expert_of(j):
             x = ins[j]
@@ -557,6 +586,7 @@ class DAGExecutor:
         for spec, _ in layout:  # these weights are original again: drop stale folded-norm state
             if spec.name not in self._derived_named:
                 self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
+                self._derived_cache.pop(("side", spec.name, views[spec.name].data_ptr()), None)
         img = self._img_override.get(pid)
         if img is None and self.gpu:
             img = self.store.group_image(pid)
@@ -644,6 +674,8 @@ class DAGExecutor:
         (``rope_perm = (n_q_heads, n_k_heads, head_dim)``). W is read by this fused group only,
         so overwriting it is safe."""
         W = self._w(w_name)
+        if self._w_users.get(w_name, 1) > 1 and (norm is not None or interleave or rope_perm is not None):
+            return self._prep_side(W, w_name, norm, b_name, interleave, rope_perm)
         named = self._derived_named.get(w_name)
         if named is not None:  # the arena holds the transformed weight (refilled from its image)
             return W, named[0], named[1]
@@ -675,6 +707,38 @@ class DAGExecutor:
             if wd is not W:
                 self._persist_transform(w_name, W, d)
         return W, d[0], d[1]
+
+    def _prep_side(self, W, w_name, norm, b_name, interleave, rope_perm):
+        """_prep for a weight other tasks also read: the transformed weight is written to a
+        private HBM buffer (derived again whenever the source group is re-filled)."""
+        key = ("side", w_name, W.data_ptr())
+        d = self._derived_cache.get(key)
+        if d is None:
+            bias = self._w(b_name) if b_name else None
+            cs = None
+            wd = W
+            if norm is not None:
+                nw = self._w(norm.op.weights["w"])
+                nb = self._w(norm.op.weights["b"]) if "b" in norm.op.weights else None
+                wd, cs, bd = ops.derive_norm_gemm(W, nw, nb, bias)
+                bias = bd if (bias is not None or nb is not None) else None
+            if interleave:
+                wd = ops.interleave_gate_up(wd)
+                cs = ops.interleave_gate_up(cs) if cs is not None else None
+                bias = ops.interleave_gate_up(bias) if bias is not None else None
+            if rope_perm is not None:
+                perm = ops.rope_pair_perm(*rope_perm, wd.shape[0]).to(wd.device)
+                wd = wd[perm].contiguous()
+                cs = cs[perm].contiguous() if cs is not None else None
+                bias = bias[perm].contiguous() if bias is not None else None
+            buf = self._side.get(w_name)
+            if buf is None or buf.shape != W.shape:
+                buf = torch.empty_like(W)
+                self._side[w_name] = buf
+            buf.copy_(wd)
+            d = (cs, bias, buf)
+            self._derived_cache[key] = d
+        return d[2], d[0], d[1]
 
     def _refills(self) -> bool:
         """Does this rank's program re-fill any parameter group after its first step (steady-state
@@ -719,7 +783,11 @@ class DAGExecutor:
         ``rope_perm``: RoPE in the epilogue over pair-interleaved q/k rows."""
         sw = act == "swiglu"
         ext = self._ext_stats.get(norm.op.inputs[0]) if norm is not None else None
-        if norm is not None and self.gpu and (ext is not None or x.shape[-1] <= FOLD_MAX_K):
+        shared = self._w_users.get(w_name, 1) > 1
+        if norm is not None and self.gpu and (ext is not None or x.shape[-1] <= FOLD_MAX_K) \
+                and not (shared and self._refills()):
+            # (a shared weight's folded copy is private: a step that re-fills its group would
+            # need the derivation inside the replayed step, so such programs run the norm)
             # folded norm: statistics handed over by x's producer (any K, split-K allowed), or
             # accumulated in this GEMM's main loop (K <= FOLD_MAX_K)
             W, cs, bd = self._prep(w_name, norm, b_name, interleave=sw, rope_perm=rope_perm)
@@ -765,8 +833,47 @@ class DAGExecutor:
             else:
                 idx, gate = ops.moe_router(logits, top_k)
                 r = (idx, gate) + tuple(ops.moe_align(idx, E))
+            if self._route_persist:
+                bufs = self._route_bufs.get(r_name)
+                if bufs is None or any(a.shape != b.shape for a, b in zip(bufs, r)):
+                    bufs = tuple(x.clone() for x in r)
+                    self._route_bufs[r_name] = bufs
+                else:
+                    for a, b in zip(bufs, r):
+                        a.copy_(b)
+                r = bufs
             self._moe_memo[key] = r
         return r
+
+    def _route_host(self, r_name: str, E: int, top_k: int) -> List[int]:
+        """Per-expert row offsets of router ``r_name``'s routing on the host (ONE device->host
+        sync per MoE layer and rank, at the first routed transfer that needs the counts)."""
+        key = ("host", r_name)
+        h = self._moe_memo.get(key)
+        if h is None:
+            h = [int(v) for v in self._moe_route(r_name, E, top_k)[4].tolist()]
+            self._moe_memo[key] = h
+        return h
+
+    def _routed_bufs(self, ins, recv: bool) -> List[torch.Tensor]:
+        """The views an expert-parallel edge moves (Instr.route): expert by expert, only the
+        routed rows — of the permuted hidden state (``rows``; on the receiver, straight into the
+        permuted-row buffer the local experts read) or of an expert's compact output (``out``)."""
+        kind, R, exps, E, K = ins.route
+        off = self._route_host(R, E, K)
+        if kind == "rows":
+            key = ("perm", ins.task, R)
+            if recv:
+                t = self.tasks[ins.task]
+                H = t.op.out_shape[-1]
+                M = math.prod(t.op.out_shape[:-1])
+                xp = self._scratch(f"moe_rows:{R}", (M * K, H))
+                self._moe_memo[key] = xp
+            else:
+                xp = self._moe_permuted(ins.task, R, E, K)
+            return [xp[off[e]:off[e + 1]] for e in exps if off[e + 1] > off[e]]
+        c = off[exps[0] + 1] - off[exps[0]]
+        return [self._flat(self._views[ins.task])[:c]] if c else []
 
     def _moe_permuted(self, h_name: str, r_name: str, E: int, top_k: int):
         key = ("perm", h_name, r_name)
@@ -774,6 +881,10 @@ class DAGExecutor:
         if xp is None:
             src = self._moe_route(r_name, E, top_k)[2]
             xp = ops.moe_permute(self._flat(self._x(h_name)), src)
+            if self._route_persist:  # a fixed buffer: captured expert kernels read it every step
+                buf = self._scratch(f"moe_perm:{h_name}", tuple(xp.shape))
+                buf.copy_(xp)
+                xp = buf
             self._moe_memo[key] = xp
         return xp
 
@@ -1016,17 +1127,31 @@ class DAGExecutor:
             elif ins.op == "recv":
                 self._wait_sends(ins)  # the recv buffer may still be read by a send to another peer
                 t0 = self._mark() if events is not None else None
-                recv_work[ins.task] = (dist.irecv(self._views[ins.task], src=ins.peer, group=pg), t0)
+                if ins.route is not None:  # expert-parallel edge: only the routed rows
+                    rw = recv_work.pop(ins.route[1], None)
+                    if rw is not None:  # the router's logits first: both ends route from them
+                        rw[0].wait()
+                    bufs = self._routed_bufs(ins, recv=True)
+                    recv_work[ins.task] = (_Works([dist.irecv(b, src=ins.peer, group=pg) for b in bufs], bufs), t0)
+                    stats.bytes_recv += sum(b.numel() * b.element_size() for b in bufs)
+                else:
+                    buf = self._views[ins.task]
+                    recv_work[ins.task] = (dist.irecv(buf, src=ins.peer, group=pg), t0)
+                    stats.bytes_recv += buf.numel() * buf.element_size()
                 stats.recvs += 1
             elif ins.op == "send":
-                buf = self._views[ins.task]
                 t0 = self._mark() if events is not None else None
-                w = dist.isend(buf, dst=ins.peer, group=pg)
+                if ins.route is not None:
+                    bufs = self._routed_bufs(ins, recv=False)
+                    w = _Works([dist.isend(b, dst=ins.peer, group=pg) for b in bufs], bufs)
+                else:
+                    bufs = [self._views[ins.task]]
+                    w = dist.isend(bufs[0], dst=ins.peer, group=pg)
                 self._pending_sends[i] = w
                 if events is not None:
                     events.append((f"{ins.task}->gpu{ins.peer}", "send", t0, self._mark()))
                 stats.sends += 1
-                stats.bytes_sent += buf.numel() * buf.element_size()
+                stats.bytes_sent += sum(b.numel() * b.element_size() for b in bufs)
             elif ins.op == "run":
                 self._pre_run(ins, recv_work, events)
                 self._issue_run(i, ins, stats, events)
@@ -1123,6 +1248,7 @@ class DAGExecutor:
         for spec, _ in layout:
             if spec.name not in self._derived_named:
                 self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
+                self._derived_cache.pop(("side", spec.name, views[spec.name].data_ptr()), None)
         self._param_recv[ins.param] = dist.irecv(self.param_slab[off:off + total], src=ins.peer, group=self.pg)
         self._valid.append((off, total, ins.param))
         stats.recvs += 1

@@ -249,7 +249,7 @@ def plan_stats(p: Plan) -> Dict:
         for d in tmap[tid].dependencies:
             if d in p.placement and p.placement[d] != r:
                 cross += 1
-                cross_bytes += tmap[d].out_bytes
+                cross_bytes += tmap[d].xfer_bytes
     return {
         "tasks_total": len(p.tasks),
         "tasks_completed": len(p.scheduler.completed_tasks),

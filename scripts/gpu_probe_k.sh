@@ -7,6 +7,6 @@ export DLS_SKIP_BUILD=1
 for c in 34 10 ${EXTRA_CFGS}; do
   bn=256; [ $c = 10 ] && bn=128
   for K in 64 128 256 768 1536 3072; do
-    timeout -k 10 60 python3 benchmarks/probe_gemm_round.py --cfg $c --bn $bn --K $K --reps 20 --hot 2>&1 | grep cfg | sed "s/^/K=$K /" || exit 3
+    timeout -k 10 60 python3 benchmarks/probe_gemm_round.py --cfg $c --bn $bn --K $K --reps 20 ${MODE} 2>&1 | grep cfg | sed "s/^/K=$K /" || exit 3
   done
 done
