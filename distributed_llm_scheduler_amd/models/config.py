@@ -69,6 +69,10 @@ PRESETS: Dict[str, ModelConfig] = {
     "mini-mixtral": ModelConfig("mini-mixtral", "mixtral", 2, 256, 4, 1024, n_positions=256, ffn_dim=256,
                                 n_kv_head=2, n_experts=4, top_k=2, tie_embeddings=False),
 }
+# one full-width layer of the big models (every kernel shape of the real model, S = 512):
+# GPU numerics tests against the fp32 reference
+PRESETS["llama3-8b-1l"] = PRESETS["llama3-8b"].with_(name="llama3-8b-1l", n_layer=1)
+PRESETS["mixtral-8x7b-1l"] = PRESETS["mixtral-8x7b"].with_(name="mixtral-8x7b-1l", n_layer=1)
 PRESETS["gpt2-small"] = PRESETS["gpt2"].with_(name="gpt2-small")
 PRESETS["llama-3-8b"] = PRESETS["llama3-8b"]
 PRESETS["mixtral"] = PRESETS["mixtral-8x7b"]

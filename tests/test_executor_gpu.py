@@ -21,13 +21,14 @@ def _check(p, ex, store, tol, rid=""):
         assert err < tol * scale, (err, scale)
         return
     # MoE: a token whose k-th/(k+1)-th router logits (nearly) tie can pick another expert
-    # under bf16 logits; that changes its row (and, through attention, later rows a
-    # little). Every other row must match; near-tie rows must stay a small minority.
+    # under bf16 logits (bf16 keeps 8 significant bits: a gap below 0.02 at logit magnitudes
+    # of a few units is within its rounding). ONLY such rows may differ; every other row must
+    # match the reference, and near-tie rows must stay a small minority.
     row_err = (out - ref).abs().amax(-1)
     risky = torch.stack([m.abs() < 0.02 for m in margins]).any(0)
     bad = row_err > tol * scale
     assert bad.float().mean().item() < 0.1, (int(bad.sum()), int(risky.sum()), row_err.max().item(), scale)
-    assert not (bad & ~risky).any() or bad.float().mean().item() < 0.05, (int((bad & ~risky).sum()), int(bad.sum()))
+    assert not (bad & ~risky).any(), (int((bad & ~risky).sum()), int(bad.sum()), row_err[~risky].max().item(), scale)
 
 
 @pytest.mark.parametrize("model,tp", [("mini-gpt2", 1), ("mini-llama", 1), ("mini-mixtral", 1),
@@ -42,6 +43,24 @@ def test_dag_on_gpu_matches_reference(model, tp, graph):
     if graph:
         assert ex.capture()
         ex.step()
+    torch.cuda.synchronize()
+    _check(p, ex, store, 0.03)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("model", ["llama3-8b-1l", "mixtral-8x7b-1l"])
+def test_full_width_layer_matches_reference(model):
+    """One FULL-WIDTH layer of Llama-3-8B (H 4096, GQA 32/8 x 128, SwiGLU F 14336, vocab 128256)
+    and of Mixtral-8x7B (8 experts, top-2) at S = 512 — the exact shapes the split-K post-norm,
+    SwiGLU-epilogue, grouped-expert and LM-head paths are tuned for — run through the DAG
+    executor (hipGraph) and compared with the fp32 reference forward."""
+    p = runtime.plan(model, world=1, seq=512, batch=1)
+    assert p.completed == p.total
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=True)
+    ex.step()
+    assert ex.capture()
+    ex.step()
     torch.cuda.synchronize()
     _check(p, ex, store, 0.03)
 
