@@ -21,11 +21,13 @@ def _check(p, ex, store, tol, rid=""):
         assert err < tol * scale, (err, scale)
         return
     # MoE: a token whose k-th/(k+1)-th router logits (nearly) tie can pick another expert
-    # under bf16 logits (bf16 keeps 8 significant bits: a gap below 0.02 at logit magnitudes
-    # of a few units is within its rounding). ONLY such rows may differ; every other row must
+    # under bf16: the router reads the bf16-rounded normed hidden state (8 significant bits)
+    # and its logits are rounded to bf16 — at H = 4096 and logits of a few units that is an
+    # error of a few 1e-2 (measured flips on the full-width Mixtral layer at gaps of 0.017 and
+    # 0.024, benchmarks/debug_mixtral_rows.py). ONLY such rows may differ; every other row must
     # match the reference, and near-tie rows must stay a small minority.
     row_err = (out - ref).abs().amax(-1)
-    risky = torch.stack([m.abs() < 0.02 for m in margins]).any(0)
+    risky = torch.stack([m.abs() < 0.05 for m in margins]).any(0)
     bad = row_err > tol * scale
     assert bad.float().mean().item() < 0.1, (int(bad.sum()), int(risky.sum()), row_err.max().item(), scale)
     assert not (bad & ~risky).any(), (int((bad & ~risky).sum()), int(bad.sum()), row_err[~risky].max().item(), scale)
