@@ -1,0 +1,220 @@
+// Native step runner: the per-rank issue loop of a steady-state step in C++.
+//
+// The Python executor (parallel/executor.py) decides WHAT a step does — which kernel-group
+// segments (captured hipGraphs) run, which parameter groups are re-filled and on which stream,
+// where the copy stream and the compute stream wait for each other, which RCCL p2p sends and
+// receives are posted and where each is waited for. A steady-state step does exactly the same
+// thing every time, so the executor records that action sequence once (``StepRunner.add_*``
+// while it runs one step eagerly) and every later step replays it here with one Python call:
+// no interpreter work per instruction (SURVEY §2.3 "C++ runtime", replacing the reference's
+// assign = execute loop, /root/reference/schedulers.py:78-104).
+//
+// Actions: launch a hipGraphExec; pull a pinned host image into HBM with the host-pull kernel;
+// hipMemcpyAsync; hipMemsetAsync; record / wait a runner-owned hipEvent on the compute or the
+// copy stream; post a p2p send / recv through the c10d ProcessGroup of the Python world (RCCL
+// on ROCm, gloo on the CPU test backend — the same ops ``dist.isend`` / ``dist.irecv`` call);
+// wait a posted p2p op (stream-side for RCCL). Every op still outstanding at the end of the
+// step is waited for, as the Python step does.
+#include <torch/extension.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/utils/pybind.h>
+#include <c10/hip/HIPStream.h>
+
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace {
+
+enum Kind : int { GRAPH = 0, PULL, MEMCPY, MEMSET, EV_RECORD, EV_WAIT, SEND, RECV, WORK_WAIT, PYCALL };
+
+struct Action {
+  Kind kind;
+  int stream = 0;  // 0 compute (torch's current stream at run()), 1 the copy stream
+  uint64_t exec = 0;
+  void* dst = nullptr;
+  const void* src = nullptr;
+  size_t bytes = 0;
+  int blocks = 0;
+  int value = 0;
+  int index = 0;  // event index / work index / peer rank
+  at::Tensor tensor;
+  py::object fn;
+};
+
+class StepRunner {
+ public:
+  StepRunner() = default;
+  ~StepRunner() {
+    for (auto e : events_)
+      if (e) (void)hipEventDestroy(e);
+  }
+
+  void set_process_group(py::object pg) {
+    pg_ = pg.is_none() ? c10::intrusive_ptr<c10d::ProcessGroup>() : pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
+  }
+  void set_copy_stream(uint64_t s) { copy_ = reinterpret_cast<hipStream_t>(s); }
+
+  void add_graph(uint64_t exec) {
+    TORCH_CHECK(exec != 0, "null hipGraphExec");
+    any_device_ = true;
+    Action a{GRAPH};
+    a.exec = exec;
+    acts_.push_back(a);
+  }
+  void add_pull(const at::Tensor& dst, const at::Tensor& src, int64_t bytes, int64_t blocks, int64_t stream) {
+    TORCH_CHECK(dst.is_cuda() && src.is_pinned(), "pull: device destination, pinned host source");
+    TORCH_CHECK(dst.nbytes() >= (size_t)bytes && src.nbytes() >= (size_t)bytes && bytes % 16 == 0,
+                "pull: byte count exceeds a buffer or is not a multiple of 16");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0,
+                "pull: 16-byte alignment");
+    void* dev_src = nullptr;
+    TORCH_CHECK(hipHostGetDevicePointer(&dev_src, src.data_ptr(), 0) == hipSuccess && dev_src != nullptr,
+                "pull: pinned host image is not mapped into the GPU address space");
+    any_device_ = true;
+    Action a{PULL, (int)stream};
+    a.dst = dst.data_ptr();
+    a.src = dev_src;
+    a.bytes = bytes;
+    a.blocks = (int)blocks;
+    a.tensor = src;  // keep the host image alive
+    acts_.push_back(a);
+  }
+  void add_memcpy(const at::Tensor& dst, const at::Tensor& src, int64_t bytes, int64_t stream) {
+    TORCH_CHECK(dst.nbytes() >= (size_t)bytes && src.nbytes() >= (size_t)bytes, "memcpy: byte count exceeds a buffer");
+    any_device_ = true;
+    Action a{MEMCPY, (int)stream};
+    a.dst = dst.data_ptr();
+    a.src = src.data_ptr();
+    a.bytes = bytes;
+    a.tensor = src;
+    acts_.push_back(a);
+  }
+  void add_memset(const at::Tensor& dst, int64_t value, int64_t stream) {
+    any_device_ = true;
+    Action a{MEMSET, (int)stream};
+    a.dst = dst.data_ptr();
+    a.bytes = dst.nbytes();
+    a.value = (int)value;
+    acts_.push_back(a);
+  }
+  // runner-owned events, addressed by index (created on first use)
+  void add_event_record(int64_t ev, int64_t stream) { acts_.push_back(event_action(EV_RECORD, ev, stream)); }
+  void add_event_wait(int64_t ev, int64_t stream) { acts_.push_back(event_action(EV_WAIT, ev, stream)); }
+  // p2p ops get work indices in the order they are added
+  int64_t add_send(const at::Tensor& t, int64_t peer) { return add_p2p(SEND, t, peer); }
+  int64_t add_recv(const at::Tensor& t, int64_t peer) { return add_p2p(RECV, t, peer); }
+  void add_work_wait(int64_t w) {
+    TORCH_CHECK(w >= 0 && w < n_works_, "unknown p2p work ", w);
+    Action a{WORK_WAIT};
+    a.index = (int)w;
+    acts_.push_back(a);
+  }
+  // CPU backend only: a kernel group has no hipGraph there, the runner calls back
+  void add_pycall(py::object fn) {
+    Action a{PYCALL};
+    a.fn = fn;
+    acts_.push_back(a);
+  }
+
+  int64_t size() const { return (int64_t)acts_.size(); }
+
+  void run() {
+    const bool gpu = any_device_;
+    hipStream_t cs = gpu ? c10::hip::getCurrentHIPStream().stream() : nullptr;
+    std::vector<c10::intrusive_ptr<c10d::Work>> works(n_works_);
+    for (auto& a : acts_) {
+      hipStream_t s = a.stream == 1 && copy_ ? copy_ : cs;
+      switch (a.kind) {
+        case GRAPH:
+          C10_HIP_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(a.exec), cs));
+          break;
+        case PULL:
+          launch_host_pull(a.src, a.dst, (int64_t)a.bytes, a.blocks, s);
+          break;
+        case MEMCPY:
+          C10_HIP_CHECK(hipMemcpyAsync(a.dst, a.src, a.bytes, hipMemcpyDefault, s));
+          break;
+        case MEMSET:
+          C10_HIP_CHECK(hipMemsetAsync(a.dst, a.value, a.bytes, s));
+          break;
+        case EV_RECORD:
+          C10_HIP_CHECK(hipEventRecord(event(a.index), s));
+          break;
+        case EV_WAIT:
+          C10_HIP_CHECK(hipStreamWaitEvent(s, event(a.index), 0));
+          break;
+        case SEND:
+        case RECV: {
+          TORCH_CHECK(pg_, "p2p action without a process group");
+          std::vector<at::Tensor> ts{a.tensor};
+          works[a.value] = a.kind == SEND ? pg_->send(ts, a.index, 0) : pg_->recv(ts, a.index, 0);
+          break;
+        }
+        case WORK_WAIT:
+          if (works[a.index]) {
+            works[a.index]->wait();  // RCCL: the current stream waits; gloo: blocks
+            works[a.index].reset();
+          }
+          break;
+        case PYCALL: {
+          py::gil_scoped_acquire g;
+          a.fn();
+          break;
+        }
+      }
+    }
+    for (auto& w : works)  // the step's p2p ops are complete when it returns (as in Python)
+      if (w) w->wait();
+  }
+
+ private:
+  Action event_action(Kind k, int64_t ev, int64_t stream) {
+    TORCH_CHECK(ev >= 0 && ev < 4096, "event index");
+    if ((size_t)ev >= events_.size()) events_.resize(ev + 1, nullptr);
+    if (!events_[ev]) C10_HIP_CHECK(hipEventCreateWithFlags(&events_[ev], hipEventDisableTiming));
+    any_device_ = true;
+    Action a{k, (int)stream};
+    a.index = (int)ev;
+    return a;
+  }
+  hipEvent_t event(int i) { return events_[i]; }
+  int64_t add_p2p(Kind k, const at::Tensor& t, int64_t peer) {
+    Action a{k};
+    a.tensor = t;
+    a.index = (int)peer;
+    a.value = n_works_;
+    if (t.is_cuda()) any_device_ = true;
+    acts_.push_back(a);
+    return n_works_++;
+  }
+
+  std::vector<Action> acts_;
+  std::vector<hipEvent_t> events_;
+  hipStream_t copy_ = nullptr;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  int n_works_ = 0;
+  bool any_device_ = false;
+};
+
+}  // namespace
+
+void register_runner(py::module& m) {
+  py::class_<StepRunner>(m, "StepRunner")
+      .def(py::init<>())
+      .def("set_process_group", &StepRunner::set_process_group)
+      .def("set_copy_stream", &StepRunner::set_copy_stream)
+      .def("add_graph", &StepRunner::add_graph)
+      .def("add_pull", &StepRunner::add_pull)
+      .def("add_memcpy", &StepRunner::add_memcpy)
+      .def("add_memset", &StepRunner::add_memset)
+      .def("add_event_record", &StepRunner::add_event_record)
+      .def("add_event_wait", &StepRunner::add_event_wait)
+      .def("add_send", &StepRunner::add_send)
+      .def("add_recv", &StepRunner::add_recv)
+      .def("add_work_wait", &StepRunner::add_work_wait)
+      .def("add_pycall", &StepRunner::add_pycall)
+      .def("size", &StepRunner::size)
+      .def("run", &StepRunner::run, py::call_guard<py::gil_scoped_release>());
+}

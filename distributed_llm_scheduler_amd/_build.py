@@ -148,18 +148,19 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     """Compile every csrc/kernels/*.hip for gfx950 and link the torch op library."""
     kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
-    binding = os.path.join(CSRC, "kernels", "ops_binding.cpp")
-    if not force and not _stale(OPS_SO, kern + hdrs + [binding]):
+    # host C++ against torch: the op bindings and the native step runner (runner.cpp)
+    hosts = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.cpp")))
+    if not force and not _stale(OPS_SO, kern + hdrs + hosts):
         return OPS_SO
     with _BuildLock("ops"):
-        if not force and not _stale(OPS_SO, kern + hdrs + [binding]):
+        if not force and not _stale(OPS_SO, kern + hdrs + hosts):
             return OPS_SO  # another process built it while we waited
-        return _build_ops(kern, hdrs, binding, force, verbose, jobs)
+        return _build_ops(kern, hdrs, hosts, force, verbose, jobs)
 
 
-def _build_ops(kern, hdrs, binding, force, verbose, jobs) -> str:
+def _build_ops(kern, hdrs, hosts, force, verbose, jobs) -> str:
     os.makedirs(BUILD_DIR, exist_ok=True)
-    d0 = _digest(kern + hdrs + [binding])
+    d0 = _digest(kern + hdrs + hosts)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     inc, defs, libs = _torch_flags()
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
@@ -180,17 +181,20 @@ def _build_ops(kern, hdrs, binding, force, verbose, jobs) -> str:
             _record(obj, [src] + hdrs, d)
         return obj
 
+    def compile_host(src):
+        obj = os.path.join(BUILD_DIR, os.path.splitext(os.path.basename(src))[0] + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            d = _digest([src] + hdrs)
+            _run([hipcc, "-O2", "-std=c++17", "-fPIC", *inc, *defs, f"-I{os.path.join(CSRC, 'kernels')}",
+                  f"-I{ROCM}/include", "-x", "c++", "-c", src, "-o", obj], verbose)
+            _record(obj, [src] + hdrs, d)
+        return obj
+
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(compile_kernel, kern))
-    bobj = os.path.join(BUILD_DIR, "ops_binding.o")
-    if force or _stale(bobj, [binding] + hdrs):
-        db = _digest([binding] + hdrs)
-        _run([hipcc, "-O2", "-std=c++17", "-fPIC", *inc, *defs, f"-I{os.path.join(CSRC, 'kernels')}", f"-I{ROCM}/include",
-              "-x", "c++", "-c", binding, "-o", bobj], verbose)
-        _record(bobj, [binding] + hdrs, db)
-    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, bobj, *libs, "-o", OPS_SO + ".tmp"], verbose)
+        objs = list(ex.map(compile_kernel, kern)) + list(ex.map(compile_host, hosts))
+    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, *libs, "-o", OPS_SO + ".tmp"], verbose)
     os.replace(OPS_SO + ".tmp", OPS_SO)
-    _record(OPS_SO, kern + hdrs + [binding], d0)
+    _record(OPS_SO, kern + hdrs + hosts, d0)
     return OPS_SO
 
 

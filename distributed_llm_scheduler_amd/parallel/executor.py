@@ -73,6 +73,54 @@ class _Works:
         self.keep = []
 
 
+class _REvent:
+    """An event of the native step runner (index into its own hipEvents), used in place of a
+    torch Event while a step is recorded."""
+    __slots__ = ("idx",)
+
+    def __init__(self, idx: int):
+        self.idx = idx
+
+
+class _RWork:
+    """A p2p op of the native step runner: ``wait()`` records the wait."""
+    __slots__ = ("runner", "idx")
+
+    def __init__(self, runner, idx: int):
+        self.runner, self.idx = runner, idx
+
+    def wait(self):
+        self.runner.add_work_wait(self.idx)
+
+
+class _Recorder:
+    """Records one steady-state step's device actions into a native ``StepRunner`` (csrc/kernels/
+    runner.cpp) instead of executing them (a dry run of the Python issue loop)."""
+
+    def __init__(self, runner):
+        self.r = runner
+        self.n_events = 0
+        self.carry: Dict[int, int] = {}  # load index -> event index of its cross-step fill
+
+    def event(self, carry_load: Optional[int] = None) -> _REvent:
+        if carry_load is not None:
+            if carry_load not in self.carry:
+                self.carry[carry_load] = self.n_events
+                self.n_events += 1
+            return _REvent(self.carry[carry_load])
+        self.n_events += 1
+        return _REvent(self.n_events - 1)
+
+
+RUNNER = os.environ.get("DLS_RUNNER", "1") != "0"  # native step runner for segment-replayed programs
+# CPU backend (tests): the runner replays the recorded step with kernel groups as Python
+# callbacks and p2p through the gloo ProcessGroup — the same action list as on the GPU
+RUNNER_CPU = os.environ.get("DLS_RUNNER_CPU", "0") == "1"
+# CPU backend (tests): the runner replays the recorded step with kernel groups as Python
+# callbacks and p2p through the gloo ProcessGroup — the same action list as on the GPU
+RUNNER_CPU = os.environ.get("DLS_RUNNER_CPU", "0") == "1"
+
+
 def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.Tensor:
     """Deterministic synthetic token ids for external input ``name`` — identical on every
     rank and in tests, whichever rank happens to own the consuming task."""
@@ -237,6 +285,10 @@ class DAGExecutor:
         self._capture_plan: Optional[Dict[int, int]] = None  # set while capture_segments runs
         self._seg_pool = None
         self._cap_stream = None  # side stream segment captures run on (_capture_segment)
+        self._rec: Optional[_Recorder] = None   # set while a step is recorded for the runner
+        self._runner = None                     # native StepRunner replaying the recorded step
+        self._runner_stats: Optional[StepStats] = None
+        self._stream_kind = 0                   # 0 compute / 1 copy stream (recording of fills)
         self._carry_at: Dict[int, List[int]] = {}  # instr -> next step's loads issued after it
         self._carry: Dict[int, object] = {}  # next step's loads already issued -> their events
         self._copy_stream = None
@@ -575,6 +627,36 @@ class DAGExecutor:
         r = self._region.get(pid)
         return r is not None and (r[0], r[1], pid) in self._valid
 
+    # --- device actions: executed, or recorded for the native step runner (self._rec) ---
+    def _new_event(self, timing: bool = False, carry_load: Optional[int] = None):
+        if self._rec is not None:
+            return self._rec.event(carry_load)
+        return torch.cuda.Event(enable_timing=timing)
+
+    def _record(self, ev, stream=None) -> None:
+        if self._rec is not None:
+            self._rec.r.add_event_record(ev.idx, 1 if stream is not None and stream is self._copy_stream else 0)
+        elif stream is not None:
+            ev.record(stream)
+        else:
+            ev.record()
+
+    def _stream_wait(self, stream, ev) -> None:
+        if self._rec is not None:
+            self._rec.r.add_event_wait(ev.idx, 1 if stream is self._copy_stream else 0)
+        else:
+            stream.wait_event(ev)
+
+    def _isend(self, buf, peer):
+        if self._rec is not None:
+            return _RWork(self._rec.r, self._rec.r.add_send(buf, peer))
+        return dist.isend(buf, dst=peer, group=self.pg)
+
+    def _irecv(self, buf, peer):
+        if self._rec is not None:
+            return _RWork(self._rec.r, self._rec.r.add_recv(buf, peer))
+        return dist.irecv(buf, src=peer, group=self.pg)
+
     def _fill(self, off, total, layout, views, pid, stats: StepStats, dma: bool = False) -> bool:
         """Copy the group into its arena region unless the region already holds it. ``dma``:
         through the copy engines even when refills are pulled by a kernel (a copy overlapping
@@ -590,11 +672,29 @@ class DAGExecutor:
         img = self._img_override.get(pid)
         if img is None and self.gpu:
             img = self.store.group_image(pid)
+        rec = self._rec
         if img is not None and self.gpu and REFILL == "pull" and not dma and img.is_pinned():
-            ops.ext().host_pull(self.param_slab[off:off + total], img, REFILL_BLOCKS)
+            if rec is not None:
+                rec.r.add_pull(self.param_slab[off:off + total], img, total, REFILL_BLOCKS, self._stream_kind)
+            else:
+                ops.ext().host_pull(self.param_slab[off:off + total], img, REFILL_BLOCKS)
         elif img is not None:  # one DMA of the whole group image
-            self.param_slab[off:off + total].copy_(img, non_blocking=True)
+            if rec is not None and not self.gpu:  # CPU runner: a callback copy
+                dst = self.param_slab[off:off + total]
+                rec.r.add_pycall(lambda: dst.copy_(img))
+            elif rec is not None:
+                rec.r.add_memcpy(self.param_slab[off:off + total], img, total, self._stream_kind)
+            else:
+                self.param_slab[off:off + total].copy_(img, non_blocking=True)
         else:
+            if rec is not None and not self.gpu:  # CPU runner: a callback fill
+                rec.r.add_pycall(lambda: [self.store.fill(sp.name, views[sp.name]) for sp, _ in layout])
+                self._valid.append((off, total, pid))
+                stats.param_fills += 1
+                stats.bytes_filled += total
+                return True
+            if rec is not None:
+                raise RuntimeError("step runner: a parameter refill without a host image cannot be recorded")
             for spec, _ in layout:
                 self.store.fill(spec.name, views[spec.name])
         self._valid.append((off, total, pid))
@@ -602,20 +702,26 @@ class DAGExecutor:
         stats.bytes_filled += total
         return True
 
-    def _prefetch(self, i: int, after, stats: StepStats, pending: Dict[int, object], events) -> None:
-        """Issue load i's copy on the copy stream behind the compute-stream event ``after``."""
+    def _prefetch(self, i: int, after, stats: StepStats, pending: Dict[int, object], events,
+                  carry: bool = False) -> None:
+        """Issue load i's copy on the copy stream behind the compute-stream event ``after``
+        (``carry``: for the next step's start, issued under this step's tail)."""
         pid = self.prog.instrs[i].param
         off, total, layout, views = self._group_views(i, pid)
         if (off, total, pid) in self._valid:
             pending[i] = None
             return
         cs = self._copy_stream
-        cs.wait_event(after)
+        self._stream_wait(cs, after)
         with torch.cuda.stream(cs):
             t0 = self._mark() if events is not None else None
-            self._fill(off, total, layout, views, pid, stats, dma=True)
-            done = torch.cuda.Event(enable_timing=events is not None)
-            done.record(cs)
+            self._stream_kind = 1
+            try:
+                self._fill(off, total, layout, views, pid, stats, dma=True)
+            finally:
+                self._stream_kind = 0
+            done = self._new_event(events is not None, carry_load=i if carry else None)
+            self._record(done, cs)
         if events is not None:
             events.append((pid, "load", t0, done))
         pending[i] = done
@@ -624,7 +730,7 @@ class DAGExecutor:
         """The compute stream waits for ``pid``'s copy-stream fill (issued ahead by _prefetch)."""
         done = self._await.pop(pid, None)
         if done is not None:
-            torch.cuda.current_stream(self.device).wait_event(done)
+            self._stream_wait(torch.cuda.current_stream(self.device), done)
 
     def _load(self, instr_index: int, pid: str, stats: StepStats) -> None:
         off, total, layout, views = self._group_views(instr_index, pid)
@@ -1058,8 +1164,9 @@ class DAGExecutor:
         pg = self.pg
         tr = self.trace
         self._pending_sends = {}
-        self._moe_memo = {}
-        self._pn_done = None
+        self._reset_step_state()
+        if self._rec is not None and not self.gpu:  # replayed steps reset it too
+            self._rec.r.add_pycall(self._reset_step_state)
         if self.prog.start_resident:  # warm-started program: its start groups are resident
             first = not self._started
             for pid, off in self.prog.start_resident.items():
@@ -1069,16 +1176,21 @@ class DAGExecutor:
                 self._map(pid, o, total, views)
         self._started = True
         if self._stats_slab is not None and not self._zero_in_embedding:
-            self._stats_slab.zero_()
+            if self._rec is not None:
+                self._rec.r.add_memset(self._stats_slab, 0, 0)
+            else:
+                self._stats_slab.zero_()
 
         recv_work: Dict[str, Tuple[object, object]] = {}
         hoist = self._hoist if self._copy_stream is not None else None
         pending: Dict[int, object] = {}
         if hoist:
             pending, self._carry = self._carry, {}  # issued by the previous step's tail
+            if self._rec is not None:  # those fills: the runner's cross-step events
+                pending = {k: (None if v is None else self._rec.event(carry_load=k)) for k, v in pending.items()}
         if hoist and -1 in hoist and any(k not in pending for k in hoist[-1]):
-            ev0 = torch.cuda.Event()
-            ev0.record()
+            ev0 = self._new_event()
+            self._record(ev0)
             for k in hoist[-1]:
                 if k not in pending:
                     self._prefetch(k, ev0, stats, pending, events)
@@ -1094,7 +1206,10 @@ class DAGExecutor:
                 for k in range(i, seg_end):  # everything the segment's runs wait for, before it
                     self._pre_run(self.prog.instrs[k], recv_work, events)
                 if i in segs:
-                    segs[i][1].replay()
+                    if self._rec is not None:
+                        self._rec.r.add_graph(segs[i][1].raw_cuda_graph_exec())
+                    else:
+                        segs[i][1].replay()
                 else:  # capture_segments: record this segment's kernels
                     self._segments[i] = (seg_end, self._capture_segment(i, seg_end, stats))
                 stats.kernels += seg_end - i
@@ -1128,6 +1243,8 @@ class DAGExecutor:
                 self._wait_sends(ins)  # the recv buffer may still be read by a send to another peer
                 t0 = self._mark() if events is not None else None
                 if ins.route is not None:  # expert-parallel edge: only the routed rows
+                    if self._rec is not None:
+                        raise RuntimeError("step runner: routed transfers need the routing on the host")
                     rw = recv_work.pop(ins.route[1], None)
                     if rw is not None:  # the router's logits first: both ends route from them
                         rw[0].wait()
@@ -1136,7 +1253,7 @@ class DAGExecutor:
                     stats.bytes_recv += sum(b.numel() * b.element_size() for b in bufs)
                 else:
                     buf = self._views[ins.task]
-                    recv_work[ins.task] = (dist.irecv(buf, src=ins.peer, group=pg), t0)
+                    recv_work[ins.task] = (self._irecv(buf, ins.peer), t0)
                     stats.bytes_recv += buf.numel() * buf.element_size()
                 stats.recvs += 1
             elif ins.op == "send":
@@ -1146,7 +1263,7 @@ class DAGExecutor:
                     w = _Works([dist.isend(b, dst=ins.peer, group=pg) for b in bufs], bufs)
                 else:
                     bufs = [self._views[ins.task]]
-                    w = dist.isend(bufs[0], dst=ins.peer, group=pg)
+                    w = self._isend(bufs[0], ins.peer)
                 self._pending_sends[i] = w
                 if events is not None:
                     events.append((f"{ins.task}->gpu{ins.peer}", "send", t0, self._mark()))
@@ -1154,23 +1271,28 @@ class DAGExecutor:
                 stats.bytes_sent += sum(b.numel() * b.element_size() for b in bufs)
             elif ins.op == "run":
                 self._pre_run(ins, recv_work, events)
-                self._issue_run(i, ins, stats, events)
+                if self._rec is not None:  # CPU runner: the group runs as a callback, with the
+                    # parameter mapping of this point of the step (a GPU segment has its pointers baked in)
+                    snap = (dict(self._params), dict(self._wflat), dict(self._region), list(self._valid))
+                    self._rec.r.add_pycall(lambda _i=i, _ins=ins, _s=snap: self._run_snapshot(_i, _ins, _s))
+                else:
+                    self._issue_run(i, ins, stats, events)
                 stats.kernels += 1
             if hoist and i in self._carry_at:  # the next step's first refills, under this tail
-                evc = torch.cuda.Event()
-                evc.record()
+                evc = self._new_event()
+                self._record(evc)
                 for k in self._carry_at[i]:
-                    self._prefetch(k, evc, stats, self._carry, events)
+                    self._prefetch(k, evc, stats, self._carry, events, carry=True)
             if hoist and i in hoist:  # loads whose region is free from here on
-                ev = torch.cuda.Event()
-                ev.record()
+                ev = self._new_event()
+                self._record(ev)
                 for k in hoist[i]:
                     self._prefetch(k, ev, stats, pending, events)
             if tr:
                 Roctx.pop()
         for done in pending.values():  # (none in a well-formed program: each load is reached)
             if done is not None:
-                torch.cuda.current_stream(self.device).wait_event(done)
+                self._stream_wait(torch.cuda.current_stream(self.device), done)
         for pid in list(self._await):
             self._await_fill(pid)
         for w, _ in recv_work.values():
@@ -1182,6 +1304,15 @@ class DAGExecutor:
             w.wait()
         self._param_recv = {}
         self._steps_done += 1
+
+    def _run_snapshot(self, i, ins, snap) -> None:
+        self._params, self._wflat, self._region, self._valid = (dict(snap[0]), dict(snap[1]), dict(snap[2]),
+                                                                list(snap[3]))
+        self._issue_run(i, ins, StepStats(), None)
+
+    def _reset_step_state(self) -> None:
+        self._moe_memo = {}
+        self._pn_done = None
 
     def _pre_run(self, ins, recv_work, events) -> None:
         """What a run must wait for: copy-stream fills and peer receives of its parameter
@@ -1235,7 +1366,7 @@ class DAGExecutor:
             pw.wait()  # this rank received the group itself: forward it once it arrived
         total = group_layout(self.store.groups[ins.param])[0]
         buf = self.param_slab[ins.param_off:ins.param_off + total]
-        self._pending_sends[i] = dist.isend(buf, dst=ins.peer, group=self.pg)
+        self._pending_sends[i] = self._isend(buf, ins.peer)
         stats.sends += 1
         stats.bytes_sent += total
 
@@ -1249,7 +1380,7 @@ class DAGExecutor:
             if spec.name not in self._derived_named:
                 self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
                 self._derived_cache.pop(("side", spec.name, views[spec.name].data_ptr()), None)
-        self._param_recv[ins.param] = dist.irecv(self.param_slab[off:off + total], src=ins.peer, group=self.pg)
+        self._param_recv[ins.param] = self._irecv(self.param_slab[off:off + total], ins.peer)
         self._valid.append((off, total, ins.param))
         stats.recvs += 1
         stats.peer_fills += 1
@@ -1269,7 +1400,19 @@ class DAGExecutor:
         ``stats.timeline`` (kernel groups) and ``stats.events`` (kernels, parameter fills,
         p2p sends/recvs), in ms from the step start."""
         stats = StepStats()
-        if self._graph is not None and not profile:
+        if self._runner is not None and profile:
+            self._leave_runner()
+        if self._runner is not None:
+            if self.trace:
+                Roctx.push(f"runner_step:rank{self.prog.rank}")
+            self._runner.run()
+            if self.trace:
+                Roctx.pop()
+            stats = StepStats(**{k: getattr(self._runner_stats, k) for k in ("kernels", "sends", "recvs",
+                                                                              "bytes_sent", "bytes_recv",
+                                                                              "param_fills", "bytes_filled",
+                                                                              "peer_fills", "bytes_peer")})
+        elif self._graph is not None and not profile:
             if self.trace:
                 Roctx.push(f"graph_step:rank{self.prog.rank}")
             self._graph.replay()
@@ -1408,6 +1551,57 @@ class DAGExecutor:
         cur.wait_stream(cs)
         return g
 
+    def _runner_ok(self) -> bool:
+        """Can this rank's steady-state step be recorded for the native runner? Every run is in
+        a captured segment, no transfer needs the routing on the host (expert-parallel routed
+        rows), and every steady-state refill copies a host image."""
+        if not RUNNER or self.trace or self.debug:
+            return False
+        if not ((self.gpu and self._segments) or (not self.gpu and RUNNER_CPU)):
+            return False
+        if any(i.route is not None for i in self.prog.instrs):
+            return False
+        if self._refills() and self.gpu:
+            for i in self.prog.instrs:
+                if i.op == "load" and i.peer < 0 and self._img_override.get(i.param) is None:
+                    img = self.store.group_image(i.param)
+                    if img is None or not img.is_pinned():
+                        return False
+        return True
+
+    def build_runner(self) -> bool:
+        """Record one steady-state step (a dry run of the issue loop: every device action goes
+        to a native StepRunner instead of the device), then execute it; later steps are one
+        ``StepRunner.run()`` each (csrc/kernels/runner.cpp). Host bookkeeping is cyclic in the
+        steady state, so the recorded step is every step."""
+        if not self._runner_ok():
+            return False
+        if self.gpu:
+            torch.cuda.synchronize(self.device)  # the previous steps' cross-step fills are complete
+        r = ops.ext().StepRunner()
+        if self._copy_stream is not None:
+            r.set_copy_stream(self._copy_stream.cuda_stream)
+        if self.pg is not None:
+            r.set_process_group(self.pg)
+        self._rec = _Recorder(r)
+        stats = StepStats()
+        try:
+            self._step_body(stats)
+        finally:
+            self._rec = None
+        r.run()  # ... the recorded step, executed
+        self._runner, self._runner_stats = r, stats
+        return True
+
+    def _leave_runner(self) -> None:
+        """Back to the Python issue loop (a profiled step): the runner's cross-step fills become
+        plain completed work."""
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+        self._runner = None
+        self._carry = {}
+        self._await = {}
+
     def capture_segments(self) -> bool:
         """Piecewise capture for programs that must stay eager around RCCL p2p or copy-stream
         refills: one hipGraph per kernel-group segment (_plan_segments), sharing one memory
@@ -1423,6 +1617,8 @@ class DAGExecutor:
         self._step_body(StepStats())  # segments captured in order as the step reaches them
         self._capture_plan = None
         torch.cuda.synchronize(self.device)
+        if self._segments:
+            self.build_runner()
         return bool(self._segments)
 
     def refine_tuning(self, top: int = 3, reps: int = 20, min_gain: float = 0.01, force: bool = False,

@@ -499,3 +499,54 @@ def test_expert_parallel_routed_rows(world):
         assert r["bytes_sent"] == exp["send"] and r["bytes_recv"] == exp["recv"], (r["rank"], r["bytes_sent"], exp)
     full = sum(len([x for x in r["routes"] if x[0] == "send"]) for r in res) * M * H * 2
     assert sum(r["bytes_sent"] for r in res) < full  # less than whole buffers per edge
+
+
+def _runner_worker(rank, world, port, q, model, kw):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from distributed_llm_scheduler_amd.parallel import executor as exm
+        exm.RUNNER_CPU = True
+        p = runtime.plan(model, world=world, seq=16, batch=1, **kw)
+        store = runtime.make_store(p)
+        ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
+        for _ in range(2):
+            py = ex.step()  # the Python issue loop (steady state from the second step)
+        assert ex.build_runner()
+        for _ in range(3):
+            st = ex.step()  # native StepRunner replays
+        res = {"rank": rank, "actions": ex._runner.size(), "errs": [],
+               "same": (st.sends, st.recvs, st.bytes_sent) == (py.sends, py.recvs, py.bytes_sent)}
+        for rid in [f"r{k}/" for k in range(kw.get("replicas", 1))] if kw.get("replicas", 1) > 1 else [""]:
+            if p.placement.get(f"{rid}output_projection") == rank:
+                res["errs"].append(_ref_check(p, ex, store, rid))
+        ex.step(profile=True)  # back to the Python loop after the runner
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("model,kw", [("tiny-llama", dict(replicas=2, placement="pipeline")),
+                                      ("tiny-gpt2", dict(tp=2, placement="tensor")),
+                                      ("tiny-gpt2", dict(replicas=2, cap_gb=0.00012, cost_model="bytes"))])
+def test_native_step_runner_replays_multi_rank_steps(model, kw):
+    """The native StepRunner (csrc/kernels/runner.cpp) records one steady-state step of a
+    multi-rank program — p2p sends / receives through the c10d ProcessGroup, their waits, and
+    (on CPU) the kernel groups as callbacks — and replays it: same transfers, outputs still equal
+    to the fp32 reference (pipeline, tensor-parallel and capped replicas with peer parameter
+    fills), and the Python loop can resume after it."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_runner_worker, args=(r, world, port, q, model, kw)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert all(r["same"] and r["actions"] > 0 for r in res)
+    errs = [e for r in res for e in r["errs"]]
+    assert errs and all(err < 0.03 * scale for err, scale in errs), errs
