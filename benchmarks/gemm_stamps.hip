@@ -1,5 +1,5 @@
 // In-kernel phase timing of one LDS-DMA GEMM config (diagnostic executable): compiles
-// csrc/kernels/gemm_glds.hip into this translation unit with DLS_STAMP recording
+// csrc/kernels/gemm_glds_impl.h (configs 34, 24, 27, 17) into this translation unit with DLS_STAMP recording
 // s_memrealtime (100 MHz) per workgroup at: tile start, after the main loop, after the output
 // image is in LDS, after the store pass.
 //
@@ -18,7 +18,21 @@ __device__ unsigned long long g_stamps[4096 * 4];
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                          \
     g_stamps[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime();                   \
   }
-#include "../csrc/kernels/gemm_glds.hip"
+#include "../csrc/kernels/gemm_glds_impl.h"
+DLS_GLDS_DEFINE(34)
+DLS_GLDS_DEFINE(24)
+DLS_GLDS_DEFINE(27)
+DLS_GLDS_DEFINE(17)
+// splitk = 1 only: the split-K reduce launcher of the library is stubbed out below
+static bool launch_gemm_glds_local(const GemmArgs& a, int cfg, int splitk) {
+  switch (cfg) {
+    case 24: return glds_launch_cfg24(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
+    case 27: return glds_launch_cfg27(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
+    case 17: return glds_launch_cfg17(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
+    default: return glds_launch_cfg34(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
+  }
+}
+bool glds_reduce(const GemmArgs&, int, float*, hipStream_t, const float*, int, float, const int*, const Epi&) { return false; }
 
 int main(int argc, char** argv) {
   const int cfg = argc > 1 ? atoi(argv[1]) : 34;
@@ -38,10 +52,10 @@ int main(int argc, char** argv) {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipMemset(C, 0, (size_t)M * N * 2);
-  for (int i = 0; i < 5; ++i) launch_gemm_glds(g, cfg, 1, nullptr, 0, nullptr, 0, 1e-5f, nullptr);
+  for (int i = 0; i < 5; ++i) launch_gemm_glds_local(g, cfg, 1);
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), std::vector<unsigned long long>(4096 * 4, 0).data(), 4096 * 4 * 8);
   hipEventRecord(e0);
-  launch_gemm_glds(g, cfg, 1, nullptr, 0, nullptr, 0, 1e-5f, nullptr);
+  launch_gemm_glds_local(g, cfg, 1);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;

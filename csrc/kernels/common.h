@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels.h"
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -89,5 +91,24 @@ __device__ __forceinline__ float apply_act(float v, int act) {
     case ACT_SILU: return silu(v);
     case ACT_RELU: return fmaxf(v, 0.f);
     default: return v;
+  }
+}
+
+// rotate the adjacent column pairs (c, c+1) of v[0..n) that start at output column col
+// (even) of row `row` — see RopeArgs
+template <int NV>
+__device__ __forceinline__ void rope_pairs(float* v, int row, int col, const RopeArgs& rp) {
+  if (col >= rp.cols) return;
+  const int half = rp.D >> 1;
+  const int pos = row % rp.S;
+  const int j0 = (col % rp.D) >> 1;
+  const float* cp = rp.cos + (size_t)pos * half + j0;
+  const float* sp = rp.sin + (size_t)pos * half + j0;
+#pragma unroll
+  for (int p = 0; p < NV / 2; ++p) {
+    const float c = cp[p], sn = sp[p];
+    const float x0 = v[2 * p], x1 = v[2 * p + 1];
+    v[2 * p] = x0 * c - x1 * sn;
+    v[2 * p + 1] = x1 * c + x0 * sn;
   }
 }

@@ -1,917 +1,12 @@
-// Multistage bf16 GEMM with LDS-DMA staging (global_load_lds_dwordx4), optional split-K.
-//
-//   C = act(alpha * A @ W^T + bias) + R      A [M][K], W [N][K] (K contiguous), K % 64 == 0
-//
-// Why this structure (cdna_hip_programming.md §5 "Pipelining across barriers", T1, T2):
-//  * GPT-2 / Llama serving GEMMs have M = 512 rows: a grid barely covers the 256 CUs, so
-//    each CU runs ~1 block and a K-loop that keeps ONE tile in flight is latency-bound —
-//    especially when the weights stream cold from HBM (measured 1.6-2x slower inside the
-//    DAG than in a hot-cache loop). Here STAGES-1 K-tiles are in flight per block.
-//  * LDS-DMA needs no staging VGPRs and no ds_write pass; the image is lane-linear (1 KiB
-//    per wave instruction = 8 rows x 128 B), so the XOR swizzle (chunk ^ (row & 7)) is
-//    applied to the per-lane SOURCE address and again on the ds_read (rule 21).
-//  * ONE raw s_barrier per K-tile: wait(tile kt) -> barrier -> issue(tile kt+STAGES-1 into
-//    the buffer everyone finished reading before this barrier) -> MFMAs on tile kt. The
-//    wait is a counted vmcnt (never 0 in steady state); __syncthreads() is avoided because
-//    its fence drains every outstanding DMA.
-//  * Split-K (host-chosen) multiplies the block count for skinny N; partial fp32 tiles go
-//    to a workspace slab and a vectorised reduce kernel applies the fused epilogue.
-//  * XCD-aware tile order (T1): the blocks of one weight panel share an XCD's L2.
+// Multistage bf16 GEMM with LDS-DMA staging — host dispatch and the split-K reduce kernels.
+// The device code and the per-config launcher live in gemm_glds_impl.h; every tile config is
+// instantiated in one of the gemm_glds_cfg*.hip translation units (compiled in parallel).
 #include <cstdlib>
-#include <type_traits>
 #include "common.h"
 #include "kernels.h"
-
-// In-kernel phase stamps for diagnostic builds (benchmarks/gemm_stamps.hip defines it before
-// including this file); empty in the library.
-#ifndef DLS_STAMP
-#define DLS_STAMP(k)
-#endif
+#include "gemm_glds_cfgs.h"
 
 namespace {
-
-__device__ __forceinline__ int kslice_count(int K, int kslice) { return K / kslice; }
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// wait until at most `ahead` tiles (PW DMA instructions each) are still in flight; the
-// immediate must be a compile-time constant, so unroll over the possible values
-template <int PW, int A>
-__device__ __forceinline__ void wait_tiles(int ahead) {
-  if constexpr (A == 0) {
-    wait_vm<0>();
-  } else {
-    if (ahead >= A) wait_vm<PW * A>();
-    else wait_tiles<PW, A - 1>(ahead);
-  }
-}
-__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
-// BXS = extra weight (B) stages: 0 -> A and W tiles share STAGES buffers and travel
-// together; 1 -> A keeps STAGES buffers (it is L2-resident: short latency) while the COLD
-// weight stream gets STAGES + 1, i.e. one more tile of HBM latency covered inside the same
-// 160 KiB of LDS (e.g. 256x256: 2 x 32 KiB A + 3 x 32 KiB W).
-// rotate the adjacent column pairs (c, c+1) of v[0..n) that start at output column col
-// (even) of row `row` — see RopeArgs
-template <int NV>
-__device__ __forceinline__ void rope_pairs(float* v, int row, int col, const RopeArgs& rp) {
-  if (col >= rp.cols) return;
-  const int half = rp.D >> 1;
-  const int pos = row % rp.S;
-  const int j0 = (col % rp.D) >> 1;
-  const float* cp = rp.cos + (size_t)pos * half + j0;
-  const float* sp = rp.sin + (size_t)pos * half + j0;
-#pragma unroll
-  for (int p = 0; p < NV / 2; ++p) {
-    const float c = cp[p], sn = sp[p];
-    const float x0 = v[2 * p], x1 = v[2 * p + 1];
-    v[2 * p] = x0 * c - x1 * sn;
-    v[2 * p + 1] = x1 * c + x0 * sn;
-  }
-}
-
-// KG_ = K groups: KG wave groups of WM x WN waves share each output tile; a stage holds KG
-// consecutive 64-deep K-tiles and group g multiplies tile g of every stage (intra-block
-// split-K: KG x the waves — and DMA issuers — per CU on a skinny grid, no reduce kernel; the
-// groups' accumulators are summed through LDS before the epilogue).
-// RING_ = 1: the 256x256 half-tile ring main loop (mainloop_ring) instead of whole-K-tile stages
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0, int KG_ = 1, int RING_ = 0>
-struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_, BXS = BXS_;
-  static constexpr int KG = KG_, RING = RING_;
-  static constexpr int BK = 64, CH = 8;
-  static constexpr int NW = WM * WN, T = 64 * NW * KG;
-  static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  static constexpr int ROWS = BM + BN, INSTR = ROWS / 8, PW = INSTR / NW;
-  static constexpr int SUB = ROWS * CH;     // one 64-deep K-tile image (bf16x8 units)
-  static constexpr int STAGE = SUB * KG;    // bf16x8 units
-  // split staging (BXS > 0): separate A / W rings
-  static constexpr int SA = STAGES, SB = STAGES + BXS;
-  static constexpr int PWA = BM / 8 / NW, PWB = BN / 8 / NW;
-  static constexpr int A_STAGE = BM * CH, B_STAGE = BN * CH;
-  static constexpr int LDS_UNITS = BXS ? SA * A_STAGE + SB * B_STAGE : STAGES * STAGE;
-  static_assert(INSTR % NW == 0, "stage rows must split evenly over waves");
-  static_assert(!BXS || ((BM / 8) % NW == 0 && (BN / 8) % NW == 0), "split rings: rows must split over waves");
-  static_assert(FM >= 1 && FN >= 1, "wave tile too small");
-  static_assert(PW * (STAGES - 2) <= 63, "vmcnt range");
-  static_assert(STAGES >= 2 && STAGES <= 8, "stages");
-  static_assert(LDS_UNITS * 16 <= 163840, "LDS budget");
-  static_assert(KG == 1 || (BXS == 0 && PRIO == 0), "K groups use the joint ring");
-  static_assert(KG == 1 || NW * 64 * FM * FN * 16 <= LDS_UNITS * 16, "K-group reduction must fit the LDS");
-  static_assert(!RING || (BM == 256 && BN == 256 && WM == 2 && WN == 4 && STAGES == 2 && KG == 1 && BXS == 0),
-                "the ring main loop is written for 256x256 tiles, 8 waves as 2 x 4, 8 x 16 KiB slots");
-};
-
-// split rings: wait until at most a*PWA + b*PWB DMA instructions are outstanding, with
-// a in [0, AMAX] and b in {a, a + 1} (see the issue order in glds_tile)
-template <int PWA, int PWB, int A>
-__device__ __forceinline__ void wait_ab(int a, int b) {
-  if constexpr (A == 0) {
-    if (b >= 1) wait_vm<PWB>();
-    else wait_vm<0>();
-  } else {
-    if (a >= A) {
-      if (b > A) wait_vm<A * PWA + (A + 1) * PWB>();
-      else wait_vm<A * PWA + A * PWB>();
-    } else {
-      wait_ab<PWA, PWB, A - 1>(a, b);
-    }
-  }
-}
-
-// MFMAs of one staged K-tile: A rows at sA[row * CH], W rows at sB[row * CH] (both XOR
-// swizzled by row & 7, see the DMA source addresses).
-// SKIP: only the wave's first fmv row fragments hold real rows (grouped experts: an expert's
-// routed rows end inside the tile) — the others are neither read nor multiplied
-template <class C, bool SKIP = false>
-__device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int lane, int wm, int wn, bool ln_acc,
-                                         f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM], float (&st_q)[C::FM],
-                                         int fmv = C::FM) {
-  // All fragments of the K-tile (both 32-deep halves) are requested before the first MFMA:
-  // the second half's ds_reads then complete under the first half's MFMAs instead of
-  // behind an lgkmcnt(0) (the compiler counts lgkmcnt per consumer).
-  bf16x8 af[2][C::FM], bw[2][C::FN];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-      const int row = wn * C::WTN + j * 16 + (lane & 15);
-      bw[kk][j] = sB[row * C::CH + (chunk ^ (row & 7))];
-    }
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      if (SKIP && i >= fmv) break;
-      const int row = wm * C::WTM + i * 16 + (lane & 15);
-      af[kk][i] = sA[row * C::CH + (chunk ^ (row & 7))];
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);  // keep every ds_read ahead of the MFMAs (counted lgkmcnt waits)
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    if (ln_acc) {
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = bf2f(af[kk][i][e]);
-          st_s[i] += x;
-          st_q[i] += x * x;
-        }
-    }
-    // swapped operands: acc = (W A^T) tile, i.e. C^T — lane holds 4 consecutive output
-    // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
-    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      if (SKIP && i >= fmv) break;
-#pragma unroll
-      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[kk][j], af[kk][i], acc[i][j]);
-    }
-    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
-  }
-}
-
-// Joint rings (BXS == 0): A and W rows of a K-tile share one stage and one DMA batch.
-// GATHER: A row r is row arows[r] of A (MoE token gather) — a compile-time switch: a runtime
-// null check in every launch's prologue cost the GPT-2 GEMMs ~5 %.
-template <class C, bool GATHER = false>
-__device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restrict__ A, int lda,
-                                               const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
-                                               int kbeg, int nk, int lane, int wave, int kgrp, int wm, int wn,
-                                               bool ln_acc, f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
-                                               float (&st_q)[C::FM], const int* __restrict__ arows) {
-  // `wave` is the wave's index in the whole block (all K groups issue DMA); instruction
-  // gi = wave*PW + j loads 8 rows of K-tile gi / INSTR of the stage
-  const bf16* src[C::PW];
-  int dst[C::PW];
-#pragma unroll
-  for (int j = 0; j < C::PW; ++j) {
-    const int gi = wave * C::PW + j;
-    const int sub = gi / C::INSTR, r8 = gi % C::INSTR;
-    const int row = 8 * r8 + (lane >> 3);
-    const int gch = (lane & 7) ^ (row & 7);
-    const int kofs = kbeg + sub * C::BK + gch * 8;
-    if (row < C::BM) {
-      int gm = min(m0 + row, M - 1);
-      if constexpr (GATHER) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
-      src[j] = A + (size_t)gm * lda + kofs;
-    } else {
-      const int gn = min(n0 + row - C::BM, N - 1);
-      src[j] = W + (size_t)gn * ldw + kofs;
-    }
-    dst[j] = sub * C::SUB + r8 * 64;
-  }
-  auto issue = [&](int kt) {
-    bf16x8* stage = smem + (kt % C::STAGES) * C::STAGE;
-#pragma unroll
-    for (int j = 0; j < C::PW; ++j) {
-      __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * (C::BK * C::KG)),
-                                       (__attribute__((address_space(3))) void*)(stage + dst[j]), 16, 0, 0);
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < C::STAGES - 1; ++s)
-    if (s < nk) issue(s);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(C::STAGES - 2, nk - 1 - kt);  // tiles issued after kt, still allowed in flight
-    wait_tiles<C::PW, C::STAGES - 2>(ahead);
-    raw_barrier();
-    if (kt + C::STAGES - 1 < nk) issue(kt + C::STAGES - 1);
-    const bf16x8* st = smem + (kt % C::STAGES) * C::STAGE + kgrp * C::SUB;
-    mma_tile<C>(st, st + C::BM * C::CH, lane, wm, wn, ln_acc, acc, st_s, st_q);
-  }
-}
-
-// Half-tile ring (256 x 256 tiles, 8 waves as 2 (M) x 4 (N), wave tile 128 x 64).
-//
-// Why: with whole 64-KiB K-tiles double-buffered (C8) the next tile is issued in one burst
-// and waited for with vmcnt(0) one K-tile later; on the GPT-2 LM head every K-tile then
-// stalls on the DMA (one 256-tile round of 256x256x768 tiles: 49 us = 2.1 TFLOP/s per CU,
-// benchmarks/bench_lmhead.py). Here a K-tile is four 16-KiB HALF-tiles (A rows 0-127,
-// A rows 128-255, W rows 0-127, W rows 128-255) in 8 slots (two K-tiles), and the wave's
-// 128 x 64 output is computed as four quadrants (64 x 32, 16 MFMAs each) in the order
-//   q0 (A top, W left)  q1 (A top, W right)  q2 (A bottom, W right)  q3 (A bottom, W left)
-// so a K-tile's W halves are last read in q1 and its A halves in q2: K-tile t+2's W halves
-// are issued into them at q2 of K-tile t and its A halves at q3 — four to six quadrant
-// phases before they are read, with two to three K-tiles' worth of DMA in flight at all
-// times instead of one burst per K-tile.
-// Synchronisation (cdna_hip_programming.md §5, "Read a staged buffer one phase AFTER the
-// wait that retires it"; RAW / WAR):
-//  * q0 of K-tile t: every wave waits (counted vmcnt: only K-tile t+1's 8 DMA instructions
-//    may still be outstanding) and then joins the barrier -> t's slots are complete for all;
-//  * q2 / q3: a barrier before the DMA issue — every wave has finished (lgkmcnt-waited,
-//    consumed by its MFMAs) the reads of the slots being re-filled (W after q1, A after q2).
-// Each wave's fragment reads of a quadrant are all issued before its 16 MFMAs.
-template <class C>
-__device__ __forceinline__ void mainloop_ring(bf16x8* smem, const bf16* __restrict__ A, int lda,
-                                              const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
-                                              int kbeg, int nk, int lane, int wave, int wm, int wn,
-                                              f32x4 (&acc)[C::FM][C::FN]) {
-  constexpr int SLOT = 128 * 8;  // bf16x8 units per 16-KiB half-tile slot (128 rows x 128 B)
-  // this thread's two DMA pieces of every half-tile: rows 8 * (2 * wave + j) + lane / 8
-  const bf16* srcA[2][2];
-  const bf16* srcB[2][2];
-  int dst[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int r = 8 * (2 * wave + j) + (lane >> 3);
-    const int gch = (lane & 7) ^ (r & 7);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      srcA[h][j] = A + (size_t)min(m0 + h * 128 + r, M - 1) * lda + kbeg + gch * 8;
-      srcB[h][j] = W + (size_t)min(n0 + h * 128 + r, N - 1) * ldw + kbeg + gch * 8;
-    }
-    dst[j] = (2 * wave + j) * 64;
-  }
-  // slot of half-tile kind hk (0 A0, 1 A1, 2 W0, 3 W1) of K-tile t
-  auto slot = [&](int t, int hk) { return smem + ((t & 1) * 4 + hk) * SLOT; };
-  auto issue = [&](int t, int hk) {
-    const bf16* const* src = hk < 2 ? srcA[hk] : srcB[hk - 2];
-    bf16x8* st = slot(t, hk);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + dst[j]), 16, 0, 0);
-  };
-  // prologue: K-tiles 0 and 1 (W halves first: issue order inside a K-tile does not matter
-  // for the counted waits, which retire whole K-tiles)
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-    if (t < nk) {
-      issue(t, 2);
-      issue(t, 3);
-      issue(t, 0);
-      issue(t, 1);
-    }
-  const int ah = wm;            // the wave's A half (rows 128 * wm ..)
-  const int bh = 2 + (wn >> 1);  // its W half
-  const int brow0 = (wn & 1) * 64;
-  bf16x8 af[2][4], bl[2][2], br[2][2];
-  for (int t = 0; t < nk; ++t) {
-    // ---- q0: K-tile t complete; A top + W left
-    if (t + 1 < nk) wait_vm<8>();
-    else wait_vm<0>();
-    raw_barrier();
-    const bf16x8* sa = slot(t, ah);
-    const bf16x8* sb = slot(t, bh);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = i * 16 + (lane & 15);
-        af[kk][i] = sa[row * C::CH + (chunk ^ (row & 7))];
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = brow0 + j * 16 + (lane & 15);
-        bl[kk][j] = sb[row * C::CH + (chunk ^ (row & 7))];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16x16x32(bl[kk][j], af[kk][i], acc[i][j]);
-    // ---- q1: A top + W right
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = brow0 + 32 + j * 16 + (lane & 15);
-        br[kk][j] = sb[row * C::CH + (chunk ^ (row & 7))];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][2 + j] = mfma16x16x32(br[kk][j], af[kk][i], acc[i][2 + j]);
-    // ---- q2: every wave is past its q1 reads -> K-tile t+2's W halves go into t's W slots
-    raw_barrier();
-    if (t + 2 < nk) {
-      issue(t + 2, 2);
-      issue(t + 2, 3);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = 64 + i * 16 + (lane & 15);
-        af[kk][i] = sa[row * C::CH + (chunk ^ (row & 7))];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[4 + i][2 + j] = mfma16x16x32(br[kk][j], af[kk][i], acc[4 + i][2 + j]);
-    // ---- q3: every wave is past its q2 reads -> K-tile t+2's A halves; A bottom + W left
-    // (both already in registers)
-    raw_barrier();
-    if (t + 2 < nk) {
-      issue(t + 2, 0);
-      issue(t + 2, 1);
-    }
-    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[4 + i][j] = mfma16x16x32(bl[kk][j], af[kk][i], acc[4 + i][j]);
-    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
-  }
-}
-
-constexpr int kPolStream = 2;  // gfx950 CPol NT (streaming) bit of the DMA's aux operand
-
-// Split rings (BXS > 0): issue order B0 [A0 B1] [A1 B2] ... — iteration t issues
-// A(t + SA - 1) then B(t + SB - 1). Waiting for A(t) then leaves a = min(SA-2, nk-1-t)
-// later A tiles and b = min(a + 1, nk-1-t) later W tiles in flight (B(t) precedes A(t)).
-template <class C, int WPOL = 0, bool SKIP = false, bool GATHER = false>
-__device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restrict__ A, int lda,
-                                               const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
-                                               int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
-                                               f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
-                                               float (&st_q)[C::FM], int fmv, const int* __restrict__ arows) {
-  static_assert(C::SB == C::SA + 1, "split rings: W ring is one deeper than A");
-  const bf16* srcA[C::PWA];
-  const bf16* srcB[C::PWB];
-#pragma unroll
-  for (int j = 0; j < C::PWA; ++j) {
-    const int row = 8 * (wave * C::PWA + j) + (lane >> 3);
-    int gm = min(m0 + row, M - 1);
-    if constexpr (GATHER) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
-    srcA[j] = A + (size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8;
-  }
-#pragma unroll
-  for (int j = 0; j < C::PWB; ++j) {
-    const int row = 8 * (wave * C::PWB + j) + (lane >> 3);
-    const int gn = min(n0 + row, N - 1);
-    srcB[j] = W + (size_t)gn * ldw + kbeg + ((lane & 7) ^ (row & 7)) * 8;
-  }
-  bf16x8* ringA = smem;
-  bf16x8* ringB = smem + C::SA * C::A_STAGE;
-  auto issueA = [&](int kt) {
-    bf16x8* st = ringA + (kt % C::SA) * C::A_STAGE;
-#pragma unroll
-    for (int j = 0; j < C::PWA; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + (wave * C::PWA + j) * 64), 16,
-                                       0, 0);
-  };
-  auto issueB = [&](int kt) {
-    bf16x8* st = ringB + (kt % C::SB) * C::B_STAGE;
-#pragma unroll
-    for (int j = 0; j < C::PWB; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + (wave * C::PWB + j) * 64), 16,
-                                       0, WPOL);
-  };
-  constexpr int DA = C::SA - 1;
-  issueB(0);
-#pragma unroll
-  for (int s = 0; s < DA; ++s) {
-    if (s < nk) issueA(s);
-    if (s + 1 < nk) issueB(s + 1);
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const int a = min(DA - 1, nk - 1 - kt);
-    const int b = min(a + 1, nk - 1 - kt);
-    wait_ab<C::PWA, C::PWB, DA - 1>(a, b);
-    raw_barrier();
-    if (kt + DA < nk) issueA(kt + DA);
-    if (kt + DA + 1 < nk) issueB(kt + DA + 1);
-    mma_tile<C, SKIP>(ringA + (kt % C::SA) * C::A_STAGE, ringB + (kt % C::SB) * C::B_STAGE, lane, wm, wn, ln_acc,
-                      acc, st_s, st_q, fmv);
-  }
-}
-
-// One output tile (tm, tn) over K-slice ks. Everything from here to the end of the epilogue
-// is per tile; the kernel below maps blocks to tiles (or loops over a device-side row range).
-// LN: row statistics of a folded norm accumulated in the main loop (else, with ln_mode set,
-// they come from ep.ext_stats).
-// WPOL: cache policy of the split rings' weight DMA (0 default, kPolStream = nt for weights
-// read exactly once per step, e.g. MoE experts far larger than the MALL)
-template <class C, int LN, int WPOL = 0, bool SKIP = false, bool GATHER = false>
-__device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
-                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
-                                          const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
-                                          float* __restrict__ part, int M, int Mmax, int N, int K, int act,
-                                          float alpha, int ks, int kslice, int tm, int tn,
-                                          const float* __restrict__ ln_colsum, int ln_mode, float ln_eps,
-                                          const Epi& ep, const int* __restrict__ arows = nullptr) {
-  const RopeArgs& rope = ep.rope;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kgrp = wave / C::NW, wq = wave % C::NW;  // K group, wave within the group
-  const int wm = wq / C::WN, wn = wq % C::WN;
-  const int m0 = tm * C::BM, n0 = tn * C::BN;
-  if (m0 >= M) return;  // whole block idle (uniform: before any barrier)
-  DLS_STAMP(0)
-  const int kbeg = ks * kslice;
-  const int nk = kslice / (C::BK * C::KG);
-
-  f32x4 acc[C::FM][C::FN];
-#pragma unroll
-  for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // fused LayerNorm/RMSNorm prologue: row statistics of A accumulated from the A fragments
-  // that stream through LDS anyway (waves with wn == 0; full K per block, splitk == 1)
-  const bool ln_acc = LN && ln_mode != 0 && wn == 0;
-  float st_s[C::FM], st_q[C::FM];
-#pragma unroll
-  for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
-  if constexpr (C::RING && !SKIP && !GATHER)  // (grouped expert launches keep the joint ring)
-    mainloop_ring<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, acc);
-  else if constexpr (C::BXS > 0)
-    mainloop_split<C, WPOL, SKIP, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
-                                  st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), arows);
-  else
-    mainloop_joint<C, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
-                      st_q, arows);
-  DLS_STAMP(1)
-  if constexpr (C::KG > 1) {
-    // sum the K groups' accumulators into group 0 (lane-contiguous 16-B records)
-    __syncthreads();
-    f32x4* red = reinterpret_cast<f32x4*>(smem);
-    for (int g2 = 1; g2 < C::KG; ++g2) {
-      if (kgrp == g2) {
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-          for (int j = 0; j < C::FN; ++j) red[((i * C::FN + j) * C::NW + wq) * 64 + lane] = acc[i][j];
-      }
-      __syncthreads();
-      if (kgrp == 0) {
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-          for (int j = 0; j < C::FN; ++j) acc[i][j] += red[((i * C::FN + j) * C::NW + wq) * 64 + lane];
-      }
-      __syncthreads();
-    }
-  }
-
-  const int g4 = (lane >> 4) * 4, r16 = lane & 15;
-  if (part != nullptr && ep.tile_sem != nullptr) {
-    // In-launch split-K combine (cdna_hip_programming.md §projection GEMM item 2, sc1 form):
-    // every K slice stores its fp32 tile WRITE-THROUGH (sc1) into its slab, drains, and one
-    // lane draws a ticket from the tile's agent-scope counter; the slice that draws
-    // splitk-1 reads the other slabs with sc1 loads (no L1 copy can be stale), adds them to
-    // its registers and runs the ordinary epilogue. No separate reduce kernel, no spinning.
-    const size_t slab = (size_t)Mmax * N;
-    const int tiles_m = (M + C::BM - 1) / C::BM;
-    int* sem = ep.tile_sem + tm + tn * tiles_m;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(part, 0, (int)(slab * kslice_count(K, kslice) * 4), 0x00020000);
-    if (kgrp == 0) {
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int row = m0 + wm * C::WTM + i * 16 + r16;
-        if (row >= M) continue;
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) {
-          const int col = n0 + wn * C::WTN + j * 16 + g4;
-          if (col >= N) continue;  // N % 8 == 0 on split-K launches: a fragment is in or out whole
-          const f32x4 v = acc[i][j];
-          u32x4 u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-          __builtin_amdgcn_raw_buffer_store_b128(u, rsrc, (int)(((size_t)ks * slab + (size_t)row * N + col) * 4), 0,
-                                                 16);
-        }
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);  // the block's one LDS array (staging is free now)
-    if (threadIdx.x == 0) {
-      const int old = __hip_atomic_fetch_add(sem, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == kslice_count(K, kslice) - 1;
-      if (last) __hip_atomic_store(sem, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-      flag[0] = last;
-    }
-    __syncthreads();
-    const bool last = flag[0] != 0;
-    if (!last) return;  // block-uniform
-    if (kgrp == 0) {
-      const int nsl = kslice_count(K, kslice);
-      for (int s2 = 0; s2 < nsl; ++s2) {
-        if (s2 == ks) continue;
-#pragma unroll
-        for (int i = 0; i < C::FM; ++i) {
-          const int row = min(m0 + wm * C::WTM + i * 16 + r16, M - 1);
-#pragma unroll
-          for (int j = 0; j < C::FN; ++j) {
-            const int col = min(n0 + wn * C::WTN + j * 16 + g4, N - 4);
-            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(
-                rsrc, (int)(((size_t)s2 * slab + (size_t)row * N + col) * 4), 0, 16);
-            acc[i][j] += f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]),
-                               __uint_as_float(u[3])};
-          }
-        }
-      }
-    }
-    part = nullptr;  // the tile now holds the full sum: ordinary epilogue below
-  }
-  // epilogue: lane (g = lane>>4, r = lane&15) of fragment (i, j) holds C[row][col..col+3]
-  // with row = m0 + wm*WTM + 16i + r, col = n0 + wn*WTN + 16j + 4g
-  float ln_rs[C::FM], ln_mu[C::FM];
-  if (ln_mode != 0) {
-    if constexpr (LN) {
-    // reduce the 4 lane groups (k-chunks) -> full-row sums, publish per row via LDS
-    float* stats = reinterpret_cast<float*>(smem);
-    raw_barrier();  // every wave is past its last LDS read of the staging buffers
-    if (ln_acc) {
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        float a = st_s[i], q = st_q[i];
-        a += __shfl_xor(a, 16, 64);
-        a += __shfl_xor(a, 32, 64);
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        if (lane < 16) {
-          const int lr = wm * C::WTM + i * 16 + lane;
-          stats[2 * lr] = a;
-          stats[2 * lr + 1] = q;
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      const int lr = wm * C::WTM + i * 16 + r16;
-      const float a = stats[2 * lr], q = stats[2 * lr + 1];
-      const float inv_k = 1.0f / (float)K;
-      if (ln_mode == 1) {
-        const float mu = a * inv_k;
-        const float var = fmaxf(q * inv_k - mu * mu, 0.f);
-        ln_mu[i] = mu;
-        ln_rs[i] = rsqrtf(var + ln_eps);
-      } else {
-        ln_mu[i] = 0.f;
-        ln_rs[i] = rsqrtf(q * inv_k + ln_eps);
-      }
-    }
-      } else {
-      // statistics handed over by the producer of A (fp32 [M][2] = sum, sum of squares)
-      const float inv_k = 1.0f / (float)K;
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int row = min(m0 + wm * C::WTM + i * 16 + r16, M - 1);
-        const float a = ep.ext_stats[2 * row], q = ep.ext_stats[2 * row + 1];
-        const float mu = ln_mode == 1 ? a * inv_k : 0.f;
-        ln_mu[i] = mu;
-        ln_rs[i] = rsqrtf(fmaxf(q * inv_k - mu * mu, 0.f) + ln_eps);
-      }
-    }
-  }
-  // 8-byte vector stores need 8-B aligned rows (ldc % 4 == 0) — N itself may be ragged
-  // (the LM head writes 50257 columns into rows padded to 50304); a fragment whose 4
-  // columns straddle N falls back to scalars.
-  const bool vec_ok = (ldc % 4 == 0) && (!R || ldr % 4 == 0);
-  if (part != nullptr) {  // split-K: fp32 partial slab, reduced by splitk_reduce_kernel
-    if (kgrp != 0) return;
-    float* P = part + (size_t)ks * Mmax * N;
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      const int row = m0 + wm * C::WTM + i * 16 + r16;
-      if (row >= M) continue;
-#pragma unroll
-      for (int j = 0; j < C::FN; ++j) {
-        const int col = n0 + wn * C::WTN + j * 16 + g4;
-        if (N % 4 == 0 && col + 3 < N) {
-          *reinterpret_cast<f32x4*>(P + (size_t)row * N + col) = acc[i][j];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (col + e < N) P[(size_t)row * N + col + e] = acc[i][j][e];
-        }
-      }
-    }
-    return;
-  }
-  if (act == ACT_SWIGLU) {
-    if (kgrp != 0) return;
-    // fragment pairs (2jj, 2jj+1) hold gate and up for the same 16 output columns
-    const int NO = N / 2;
-#pragma unroll
-    for (int jj = 0; jj < C::FN / 2; ++jj) {
-      const int gcol = n0 + wn * C::WTN + jj * 32 + g4;  // gate column in W' space
-      const int ocol = (n0 + wn * C::WTN) / 2 + jj * 16 + g4;
-      if (ocol >= NO) continue;
-      float bg[4] = {0.f, 0.f, 0.f, 0.f}, bu[4] = {0.f, 0.f, 0.f, 0.f};
-      float cg[4] = {0.f, 0.f, 0.f, 0.f}, cu[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (bias) {
-          bg[e] = bf2f(bias[gcol + e]);
-          bu[e] = bf2f(bias[gcol + 16 + e]);
-        }
-        if (ln_mode != 0) {
-          cg[e] = ln_colsum[gcol + e];
-          cu[e] = ln_colsum[gcol + 16 + e];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int row = m0 + wm * C::WTM + i * 16 + r16;
-        if (row >= M) continue;
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float g = acc[i][2 * jj][e], u = acc[i][2 * jj + 1][e];
-          if (ln_mode != 0) {
-            g = ln_rs[i] * (g - ln_mu[i] * cg[e]);
-            u = ln_rs[i] * (u - ln_mu[i] * cu[e]);
-          } else {
-            g *= alpha;
-            u *= alpha;
-          }
-          o[e] = f2bf(silu(g + bg[e]) * (u + bu[e]));
-        }
-        if (vec_ok && ocol + 3 < NO) {
-          *reinterpret_cast<bf16x4*>(Cp + (size_t)row * ldc + ocol) = o;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (ocol + e < NO) Cp[(size_t)row * ldc + ocol + e] = o[e];
-        }
-      }
-    }
-    return;
-  }
-  // Staged epilogue: each wave writes its finished fragments (bias, activation, folded norm,
-  // RoPE applied; bf16) into a tile image in LDS, then the block stores the tile as whole
-  // 16-B-per-lane row segments (residual add and row statistics on the way out). A lane's
-  // fragment holds only 4 columns (8 B) of 16 different rows, so storing fragments directly
-  // scatters 32-B pieces over 16 rows per instruction — partial lines that measured
-  // ~1.2 TB/s on the 51 MB LM-head output; full rows run at the HBM write rate.
-  // BNC 16-B chunks per tile row, stored in rows of BNP (power of two >= 8) chunks: image chunk
-  // c of row r sits at c ^ (r & 7), and BNP consecutive lanes own one row in the store pass
-  constexpr int BNC = C::BN / 8;
-  constexpr int BNP = BNC <= 8 ? 8 : BNC <= 16 ? 16 : BNC <= 32 ? 32 : 64;
-  static_assert(C::BN % 8 == 0 && BNC <= 64, "staged epilogue: BN % 8 == 0, BN <= 512");
-  static_assert(C::BM * BNP * 16 <= C::LDS_UNITS * 16, "output tile image must fit the staging LDS");
-  static_assert((C::BM * BNP) % 64 == 0 && ((C::BM * BNP) % C::T == 0 || C::BM * BNP < C::T),
-                "store pass: every wave makes the same number of passes (shuffles stay wave-uniform)");
-  bf16* img = reinterpret_cast<bf16*>(smem);
-  __syncthreads();  // every wave is done with the staging buffers (and the norm statistics)
-  // The activation / folded-norm / RoPE choice is made ONCE per tile and the fragment pass is
-  // instantiated per combination: a runtime switch per output value (apply_act) unrolled over
-  // the 128 values per lane of a 256 x 256 tile compiled to ~25k instructions of branches
-  // around inlined GeLU / SiLU bodies, and the instruction fetches of jumping through them made
-  // this pass take 19.5 us per tile on MI355X (benchmarks/gemm_stamps.hip) — 3x the main loop
-  // of the GPT-2 LM head.
-  auto image_pass = [&](auto act_tag, auto ln_tag, auto rope_tag) {
-    constexpr int ACT = decltype(act_tag)::value;
-    constexpr bool LNM = decltype(ln_tag)::value, ROPE = decltype(rope_tag)::value;
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-      if (kgrp != 0) break;  // K group 0 holds the summed tile
-      const int cl = wn * C::WTN + j * 16 + g4;  // local column of this lane's 4 values
-      const int col = n0 + cl;
-      const bool full = col + 3 < N;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      float csv[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(W') of the 4 columns (folded norm)
-      if (bias) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
-      }
-      if constexpr (LNM) {
-        if (full && (N % 4 == 0)) {
-          const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_colsum + col);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) csv[e] = c4[e];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) csv[e] = col + e < N ? ln_colsum[col + e] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int rl = wm * C::WTM + i * 16 + r16;
-        float v[4];
-        if constexpr (LNM) {
-          // W.LN(x) = rstd * (W' x - mu * colsum(W')) + (bias + W b), W' = W * ln_w (host-derived)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = act_c<ACT>(ln_rs[i] * (acc[i][j][e] - ln_mu[i] * csv[e]) + bv[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = act_c<ACT>(alpha * acc[i][j][e] + bv[e]);
-        }
-        if constexpr (ROPE) rope_pairs<4>(v, m0 + rl, col, rope);
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
-        *reinterpret_cast<bf16x4*>(img + rl * BNP * 8 + (((cl >> 3) ^ (rl & 7)) << 3) + (cl & 7)) = o;
-      }
-    }
-  };
-  using B0 = std::integral_constant<bool, false>;
-  using B1 = std::integral_constant<bool, true>;
-  auto by_ln = [&](auto act_tag, auto rope_tag) {
-    if (ln_mode != 0) image_pass(act_tag, B1{}, rope_tag);
-    else image_pass(act_tag, B0{}, rope_tag);
-  };
-  if (rope.cols) {
-    by_ln(std::integral_constant<int, ACT_NONE>{}, B1{});  // RoPE epilogues carry no activation
-  } else {
-    switch (act) {
-      case ACT_GELU_TANH: by_ln(std::integral_constant<int, ACT_GELU_TANH>{}, B0{}); break;
-      case ACT_SILU: by_ln(std::integral_constant<int, ACT_SILU>{}, B0{}); break;
-      case ACT_RELU: by_ln(std::integral_constant<int, ACT_RELU>{}, B0{}); break;
-      default: by_ln(std::integral_constant<int, ACT_NONE>{}, B0{}); break;
-    }
-  }
-  __syncthreads();
-  DLS_STAMP(2)
-  const bool v16 = ((reinterpret_cast<uintptr_t>(Cp) | ((uintptr_t)ldc * 2)) & 15) == 0 &&
-                   (!R || ((reinterpret_cast<uintptr_t>(R) | ((uintptr_t)ldr * 2)) & 15) == 0);
-  const bf16x8* img8 = reinterpret_cast<const bf16x8*>(img);
-  const int tid_ = threadIdx.x;
-  // consecutive groups of BNP threads own one tile row per pass (lanes past BNC idle)
-#pragma unroll 2
-  for (int q = tid_; q < C::BM * BNP; q += C::T) {
-    const int rl = q / BNP, cc = q % BNP;
-    const int row = m0 + rl, col = n0 + cc * 8;
-    bf16x8 o = img8[rl * BNP + (cc ^ (rl & 7))];
-    float s1 = 0.f, s2 = 0.f;
-    if (cc < BNC && row < M && col < N) {
-      if (v16 && col + 8 <= N) {
-        if (R) {
-          const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(R + (size_t)row * ldr + col);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(o[e]) + bf2f(r8[e]));
-        }
-        *reinterpret_cast<bf16x8*>(Cp + (size_t)row * ldc + col) = o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float y = bf2f(o[e]);
-          s1 += y;
-          s2 += y * y;
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (col + e >= N) continue;
-          float x = bf2f(o[e]);
-          if (R) x += bf2f(R[(size_t)row * ldr + col + e]);
-          const bf16 ob = f2bf(x);
-          Cp[(size_t)row * ldc + col + e] = ob;
-          const float y = bf2f(ob);
-          s1 += y;
-          s2 += y * y;
-        }
-      }
-    }
-    if (ep.stats_out) {
-#pragma unroll
-      for (int o_ = 1; o_ < BNP; o_ <<= 1) {
-        s1 += __shfl_xor(s1, o_, 64);
-        s2 += __shfl_xor(s2, o_, 64);
-      }
-      if (cc == 0 && row < M) {
-        atomicAdd(ep.stats_out + 2 * row, s1);
-        atomicAdd(ep.stats_out + 2 * row + 1, s2);
-      }
-    }
-  }
-  DLS_STAMP(3)
-}
-
-// LN / RANGED are compile-time switches: a kernel instance carries only the epilogue and
-// tile walk it needs (the folded-norm statistics and the row-range loop cost registers).
-template <class C, int LN, int RANGED>
-__global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
-                                                         const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
-                                                         int ldc, const bf16* __restrict__ bias,
-                                                         const bf16* __restrict__ R, int ldr,
-                                                         float* __restrict__ part, int M, int N, int K, int act,
-                                                         float alpha, int tiles_m, int tiles_n, int splitk,
-                                                         int kslice, const float* __restrict__ ln_colsum,
-                                                         int ln_mode, float ln_eps, const int* __restrict__ rows,
-                                                         int compact_rows, Epi ep) {
-  __shared__ bf16x8 smem[C::LDS_UNITS];
-  const int ntile = tiles_m * tiles_n;
-  if constexpr (RANGED == 2) {
-    // persistent: a resident grid walks the tiles; tile t+1's first K-tiles are issued right
-    // behind tile t's epilogue stores, so the store drain overlaps the next load latency
-    // instead of holding the CU (one block per CU cannot overlap them across blocks)
-    const int total = ntile * splitk;
-    for (int L = blockIdx.x, it = 0; L < total; L += gridDim.x, ++it) {
-      if (it) raw_barrier();  // every wave is done reading the previous tile's output image
-      const int ks = L / ntile, tile = L % ntile;
-      glds_tile<C, LN>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice,
-                       tile % tiles_m, tile / tiles_m, ln_colsum, (LN || ep.ext_stats) ? ln_mode : 0, ln_eps, ep);
-    }
-    return;
-  }
-  if constexpr (RANGED == 3) {
-    // grouped MoE experts: block (g, tn) walks expert g's row range [rows[g], rows[g+1]) of
-    // its column panel with expert g's weight; consecutive blocks share an expert (its rows
-    // stay L2-resident while its weight panels stream)
-    const int g = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
-    const int r0 = rows[g], cnt = rows[g + 1] - r0;
-    const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
-    const bf16* Wg = reinterpret_cast<const bf16*>(ep.grp_w[g]);
-    bf16* Cg = ep.grp_c ? reinterpret_cast<bf16*>(ep.grp_c[g]) : Cp + (size_t)r0 * ldc;
-    // gathered A: the group's rows are tokens a_rows[r0 ..]; else rows r0.. of the sorted A.
-    // The gather map travels in the `part` argument, unused by grouped launches (no split-K):
-    // a new Epi field would change every GEMM launch's argument layout
-    const int* a_rows = reinterpret_cast<const int*>(part);
-    const int* ag = a_rows ? a_rows + r0 : nullptr;
-    const bf16* Ag = a_rows ? A : A + (size_t)r0 * lda;
-#define DLS_GROUPED_WALK(GA)                                                                                      \
-  for (int t = 0; t * C::BM < Mr; ++t) {                                                                           \
-    if (t) raw_barrier(); /* every wave is done reading the staging buffers of the previous tile */                \
-    if (C::BXS > 0 && ep.w_stream)                                                                                 \
-      glds_tile<C, 0, kPolStream, true, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, \
-                                            act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep, ag);                \
-    else                                                                                                           \
-      glds_tile<C, 0, 0, false, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, act,   \
-                                    alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep, ag);                             \
-  }
-    if (a_rows) {
-      DLS_GROUPED_WALK(true)
-    } else {
-      DLS_GROUPED_WALK(false)
-    }
-#undef DLS_GROUPED_WALK
-    return;
-  }
-  const int bid = xcd_remap(blockIdx.x, ntile * splitk);
-  const int ks = bid / ntile, tile = bid % ntile;
-  const int tm = tile % tiles_m, tn = tile / tiles_m;
-  if constexpr (!RANGED) {
-    glds_tile<C, LN>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn,
-                     ln_colsum, (LN || ep.ext_stats) ? ln_mode : 0, ln_eps, ep);
-    return;
-  }
-  // device-side row range (MoE expert): the host launched ONE tile row (tiles_m == 1) — no
-  // idle blocks holding CUs — and each block walks the range's M tiles of its column panel
-  const int r0 = rows[0], Mr = compact_rows ? min(rows[1] - r0, compact_rows) : rows[1] - r0;
-  A += (size_t)r0 * lda;
-  if (!compact_rows) Cp += (size_t)r0 * ldc;
-  if (R) R += (size_t)r0 * ldr;
-  if (part) part += (size_t)r0 * N;
-  for (int t = 0; t * C::BM < Mr; ++t) {
-    if (t) raw_barrier();  // every wave is done reading the staging buffers of the previous tile
-    glds_tile<C, 0>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, Mr, M, N, K, act, alpha, ks, kslice, t, tn,
-                    ln_colsum, 0, ln_eps, ep);
-  }
-}
-
 // Epilogue of a split-K GEMM for 8 consecutive columns c..c+7 of row m (non-SwiGLU):
 // norm fold with handed-over row statistics, bias, activation, RoPE, residual.
 struct ReduceNorm {
@@ -1181,54 +276,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_norm_kernel(const float* __
   }
 }
 
-// resident blocks of a persistent launch: CUs x blocks per CU (occupancy query, cached)
-template <class C, int LN>
-int persistent_grid() {
-  static int g = 0;
-  if (!g) {
-    int dev = 0, cus = 256, per = 1;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, gemm_glds_kernel<C, LN, 2>, C::T, 0);
-    g = cus * (per > 0 ? per : 1);
-  }
-  return g;
-}
+}  // namespace
 
-template <class C>
-bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
-            float ln_eps, const int* rows, bool persist) {
-  // in-launch combine only while the last arriver's serial read of the other slices stays small
-  // (cdna_hip_programming.md: ~1 us per 16 KB; Llama-3-8B's 256x128 split-4 tiles would read
-  // 384 KB in one block, far slower than the reduce kernel)
-  const bool fixup = splitk > 1 && !rows && (splitk - 1) * C::BM * C::BN * 4 <= 64 * 1024;
-  const Epi ep{a.rope, a.stats_out, a.ext_stats, fixup ? a.tile_sem : nullptr};
-  static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
-  const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
-  const int kslice = a.K / splitk;
-  const int total = tiles_m * tiles_n * splitk;
-  dim3 grid(total), block(C::T);
-#define DLS_K(LN_, RG_)                                                                                           \
-  hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
-                     a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
-                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows, ep)
-  const bool ln_in = ln_mode != 0 && !a.ext_stats;
-  if (rows) DLS_K(0, 1);
-  else if (persist) {
-    if (ln_in) {
-      if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) {
-        grid = dim3(std::min(total, persistent_grid<C, 1>()));
-        DLS_K(1, 2);
-      }
-    } else {
-      grid = dim3(std::min(total, persistent_grid<C, 0>()));
-      DLS_K(0, 2);
-    }
-  } else if (ln_in) {
-    if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) DLS_K(1, 0);  // 256x256: no registers left for it
-  } else DLS_K(0, 0);
-#undef DLS_K
-  if (splitk > 1 && !ep.tile_sem) {
+bool glds_reduce(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float* ln_colsum, int ln_mode,
+                 float ln_eps, const int* rows, const Epi& ep) {
+  {
     const ReduceNorm nm{ln_colsum, a.ext_stats ? ln_mode : 0, ln_eps, a.K};
     if (a.norm_out && !rows && a.act != kActSwiglu && a.N % 8 == 0 && a.N <= 256 * 8 * RN_MAXV) {
 #define DLS_RN(VPT, SK)                                                                                          \
@@ -1258,63 +310,10 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     }
   }
   return false;
+  return false;
 }
 
-using C0 = Cfg<256, 128, 4, 2, 3>;  // 8 waves, 64x64 per wave: large GEMMs
-using C1 = Cfg<128, 128, 2, 2, 3>;  // 4 waves, 64x64 per wave
-using C2 = Cfg<128, 64, 2, 2, 4>;   // 4 waves, 64x32 per wave
-using C3 = Cfg<64, 64, 2, 2, 4>;    // 4 waves, 32x32 per wave
-using C4 = Cfg<64, 128, 2, 2, 4>;
-using C5 = Cfg<64, 64, 2, 2, 8>;    // deep pipeline: 7 K-tiles in flight (cold-weight latency)
-using C6 = Cfg<128, 64, 2, 2, 6>;   // 5 in flight, 2x rows per block
-using C7 = Cfg<128, 128, 2, 2, 4>;
-using C8 = Cfg<256, 256, 2, 4, 2>;     // 8 waves, 128x64 per wave, 2 x 64 KiB stages: big square-ish GEMMs
-using C9 = Cfg<256, 256, 2, 4, 2, 1>;  // same with s_setprio(1) around the MFMA cluster (T5)
-using C10 = Cfg<256, 128, 4, 2, 3, 1>; // C0 with s_setprio
-using C11 = Cfg<128, 128, 2, 2, 4, 1>; // C7 with s_setprio
-// split rings: the cold weight stream one tile deeper than the L2-resident activations
-using C12 = Cfg<256, 256, 2, 4, 2, 0, 1>;  // 2 x 32 KiB A + 3 x 32 KiB W = 160 KiB
-using C13 = Cfg<256, 256, 2, 4, 2, 1, 1>;
-using C14 = Cfg<256, 128, 4, 2, 3, 0, 1>;  // 3 x 32 KiB A + 4 x 16 KiB W = 160 KiB
-using C15 = Cfg<128, 128, 2, 2, 3, 0, 1>;  // 3 x 16 KiB A + 4 x 16 KiB W
-// two K groups (8 waves, intra-block split-K) for the skinny M = 512 GEMMs
-using C16 = Cfg<64, 64, 2, 2, 3, 0, 0, 2>;   // 3 x 32 KiB stages
-using C17 = Cfg<64, 64, 2, 2, 2, 0, 0, 2>;   // 2 x 32 KiB: two blocks per CU
-using C18 = Cfg<128, 64, 2, 2, 2, 0, 0, 2>;  // 2 x 48 KiB
-using C19 = Cfg<64, 128, 2, 2, 2, 0, 0, 2>;
-using C20 = Cfg<64, 64, 2, 2, 2, 0, 0, 4>;   // four K groups: 16 waves, 2 x 64 KiB stages
-using C21 = Cfg<64, 64, 1, 2, 2, 0, 0, 4>;   // four K groups of 2 waves (64x32 each)
-// tiles sized so a 512-row GEMM covers the 256 CUs exactly once (per-CU L2->LDS bytes, not
-// MFMA rate, bound these: 512x3072 -> 8x32 tiles of 64x96, 512x2304 -> 16x16 of 32x144,
-// 512x768 -> 16x16 of 32x48)
-using C22 = Cfg<64, 96, 2, 2, 4>;
-using C23 = Cfg<32, 144, 2, 1, 4>;
-using C24 = Cfg<32, 48, 2, 1, 4>;
-using C25 = Cfg<64, 96, 2, 2, 3, 0, 0, 2>;
-using C26 = Cfg<32, 144, 2, 1, 3, 0, 0, 2>;
-using C27 = Cfg<32, 48, 2, 1, 4, 0, 0, 2>;
-// 128x128 with two K groups: each stage's DMA covers 256 contiguous bytes of every weight row
-// (two K-tiles back to back) — the HBM-streaming MoE expert GEMMs (128 routed rows, cold weights)
-using C28 = Cfg<128, 128, 2, 2, 2, 0, 0, 2>;
-// 192-row tiles: a top-2 expert of a 512-token batch gets ~128 +- 11 routed rows, so 128-row
-// tiles need a second pass over the WHOLE weight panel for most experts; 192 rows take any
-// such expert in one pass (its weights stream from HBM exactly once)
-using C29 = Cfg<192, 128, 2, 2, 3>;
-using C30 = Cfg<192, 128, 2, 2, 2, 0, 0, 2>;
-using C31 = Cfg<192, 128, 2, 2, 2, 0, 1>;  // split rings: 2 x 24 KiB A + 3 x 16 KiB W
-// deeper split rings for the HBM-streaming expert GEMMs: 3 x 24 KiB A + 4 x 16 KiB W = 136 KiB
-// keeps 2 A and 3 W tiles in flight (C31: 1 and 2); C33 issues them from 8 waves (48 x 64 wave
-// tiles). Measured (Mixtral-8x7B grouped launches): C33 441 / 206 us for gate-up / down vs C31
-// 465 / 215; C32 (same rings, 4 waves) no faster than C31 — the wave count, not the ring
-// depth, moved it. A 192 x 256 tile (half the routed-row bytes per weight byte) ran > 550 us.
-// Role-split rings (half the waves DMA only W, 5-6 tiles deep; the other half only A, 2 deep;
-// 8 or 16 waves) were slower still: 537-545 / 254-268 us — not bytes in flight but the number of
-// DMA-issuing waves per stream bounds these launches.
-using C32 = Cfg<192, 128, 2, 2, 3, 0, 1>;
-using C33 = Cfg<192, 128, 4, 2, 3, 0, 1>;
-// 256 x 256 with the half-tile ring main loop (mainloop_ring): LM heads and the large GEMMs
-using C34 = Cfg<256, 256, 2, 4, 2, 0, 0, 1, 1>;
-using C35 = Cfg<256, 256, 2, 4, 2, 1, 0, 1, 1>;
+namespace {
 
 struct Shape {
   int bm, bn;
@@ -1331,48 +330,16 @@ constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64
 constexpr int kNumCfg = 36;
 static_assert(kNumCfg <= kGemmPersist, "config ids must stay below the persistent-launch flag");
 
-// call f(Cfg{}) for config id cfg (unknown ids: C3)
-template <class F>
-void with_cfg(int cfg, F&& f) {
-  switch (cfg) {
-    case 0: f(C0{}); break;
-    case 1: f(C1{}); break;
-    case 2: f(C2{}); break;
-    case 4: f(C4{}); break;
-    case 5: f(C5{}); break;
-    case 6: f(C6{}); break;
-    case 7: f(C7{}); break;
-    case 8: f(C8{}); break;
-    case 9: f(C9{}); break;
-    case 10: f(C10{}); break;
-    case 11: f(C11{}); break;
-    case 12: f(C12{}); break;
-    case 13: f(C13{}); break;
-    case 14: f(C14{}); break;
-    case 15: f(C15{}); break;
-    case 16: f(C16{}); break;
-    case 17: f(C17{}); break;
-    case 18: f(C18{}); break;
-    case 19: f(C19{}); break;
-    case 20: f(C20{}); break;
-    case 21: f(C21{}); break;
-    case 22: f(C22{}); break;
-    case 23: f(C23{}); break;
-    case 24: f(C24{}); break;
-    case 25: f(C25{}); break;
-    case 26: f(C26{}); break;
-    case 27: f(C27{}); break;
-    case 28: f(C28{}); break;
-    case 29: f(C29{}); break;
-    case 30: f(C30{}); break;
-    case 31: f(C31{}); break;
-    case 32: f(C32{}); break;
-    case 33: f(C33{}); break;
-    case 34: f(C34{}); break;
-    case 35: f(C35{}); break;
-    default: f(C3{}); break;
-  }
-}
+using LaunchFn = bool (*)(const GemmArgs&, int, float*, hipStream_t, const float*, int, float, const int*, bool);
+using GroupedFn = void (*)(const GemmArgs&, int, const int*, const unsigned long long*, const unsigned long long*,
+                           hipStream_t, const int*);
+#define DLS_GLDS_L(ID) glds_launch_cfg##ID,
+#define DLS_GLDS_G(ID) glds_grouped_cfg##ID,
+constexpr LaunchFn kLaunch[] = {DLS_GLDS_ALL(DLS_GLDS_L)};
+constexpr GroupedFn kGrouped[] = {DLS_GLDS_ALL(DLS_GLDS_G)};
+#undef DLS_GLDS_L
+#undef DLS_GLDS_G
+static_assert(sizeof(kLaunch) / sizeof(kLaunch[0]) == kNumCfg, "one launcher per config");
 
 }  // namespace
 
@@ -1419,11 +386,7 @@ bool launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
   // the SwiGLU epilogue pairs 16-column gate/up fragments: wave tiles must be multiples of 32
   // columns (configs 22-27 have 48- / 144-column wave tiles)
   if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
-  bool normed = false;
-  with_cfg(cfg, [&](auto c) {
-    normed = launch<decltype(c)>(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist);
-  });
-  return normed;
+  return kLaunch[cfg < kNumCfg ? cfg : 3](a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist);
 }
 
 void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const int* offsets,
@@ -1431,19 +394,5 @@ void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const in
                               const int* a_rows) {
   cfg &= kGemmPersist - 1;
   if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
-  with_cfg(cfg, [&](auto c) {
-    using C = decltype(c);
-    // expert weights (read once per step, far larger than the MALL) are DMA'd with the nt
-    // policy: Mixtral-8x7B 27.05 vs 27.89 ms per step (DLS_EXPERT_NT=0 restores the default)
-    static const int w_stream = [] {
-      const char* e = std::getenv("DLS_EXPERT_NT");
-      return e && e[0] == '0' ? 0 : 1;
-    }();
-    const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs, w_stream};
-    const int tiles_n = (a.N + C::BN - 1) / C::BN;
-    hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(n_groups * tiles_n), dim3(C::T), 0, s, (const bf16*)a.A,
-                       a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0,
-                       const_cast<float*>(reinterpret_cast<const float*>(a_rows)), a.M, a.N, a.K, a.act,
-                       a.alpha, 1, tiles_n, 1, a.K, nullptr, 0, 1e-5f, offsets, a.compact_rows, ep);
-  });
+  kGrouped[cfg < kNumCfg ? cfg : 3](a, n_groups, offsets, w_ptrs, c_ptrs, s, a_rows);
 }
