@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_llm_scheduler_amd import ops  # noqa: E402
 from distributed_llm_scheduler_amd.ops.tuning import PERSIST, _graph_time  # noqa: E402
 
-SHAPES = {0: (256, 128), 1: (128, 128), 8: (256, 256), 9: (256, 256), 12: (256, 256), 13: (256, 256),
+SHAPES = {36: (256, 224), 0: (256, 128), 1: (128, 128), 8: (256, 256), 9: (256, 256), 12: (256, 256), 13: (256, 256),
           14: (256, 128), 7: (128, 128), 15: (128, 128), 10: (256, 128), 34: (256, 256), 35: (256, 256)}
 
 
@@ -51,7 +51,7 @@ def main():
     rec("torch", _graph_time(lambda i: torch.matmul(x, ws[i % 4].t(), out=o), reps=8))
     ref = (x.float() @ ws[0].float().t())
     for c in [int(v) for v in a.cfgs.split(",")]:
-        for persist in ((0,) if c in (34, 35) else (0, PERSIST)):
+        for persist in ((0,) if c >= 34 else (0, PERSIST)):
             cfg = c + persist
             try:
                 ext.gemm(x, ws[0], None, None, 0, 1.0, o, cfg, 1)

@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=1, help="coordinate-descent passes over the shapes")
+    ap.add_argument("--cfgs", default=None, help="only candidates with these config ids (comma list)")
+    ap.add_argument("--keys", default=None, help="only these shape keys, e.g. 512x50257x768 (comma list)")
+    ap.add_argument("--min-gain", type=float, default=0.002)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -41,7 +44,9 @@ def main():
     out = {}
     for r in range(args.rounds):
         out[f"round{r}"] = {k: [list(v[0]), list(v[1]), v[2]] for k, v in
-                            ex.refine_tuning(reps=args.reps, min_gain=0.002, force=True, exhaustive=True, log=log).items()}
+                            ex.refine_tuning(reps=args.reps, min_gain=args.min_gain, force=True, exhaustive=True, log=log,
+                                             cfgs={int(c) for c in args.cfgs.split(",")} if args.cfgs else None,
+                                             keys=set(args.keys.split(",")) if args.keys else None).items()}
     print(json.dumps({"changes": out, "timings": timings}), flush=True)
 
 

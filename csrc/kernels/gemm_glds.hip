@@ -323,11 +323,13 @@ constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64
                              {256, 256}, {256, 256}, {256, 128}, {128, 128}, {64, 64},   {64, 64},
                              {128, 64},  {64, 128},  {64, 64},   {64, 64},   {64, 96},   {32, 144},
                              {32, 48},   {64, 96},   {32, 144},  {32, 48},   {128, 128}, {192, 128},
-                             {192, 128}, {192, 128}, {192, 128}, {192, 128}, {256, 256}, {256, 256}};
+                             {192, 128}, {192, 128}, {192, 128}, {192, 128}, {256, 256}, {256, 256},
+                             {256, 224}, {256, 224}, {128, 96},  {128, 96},  {128, 64}};
 constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
                           64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128, 128,
-                          64, 128, 64, 64, 64, 64, 64};
-constexpr int kNumCfg = 36;
+                          64, 128, 64, 64, 64, 64, 64, 64, 64, 64, 128, 128};
+constexpr int kNumCfg = 41;
+constexpr bool swiglu_bad(int c) { return (c >= 22 && c <= 27) || c == 36 || c == 38 || c == 39; }
 static_assert(kNumCfg <= kGemmPersist, "config ids must stay below the persistent-launch flag");
 
 using LaunchFn = bool (*)(const GemmArgs&, int, float*, hipStream_t, const float*, int, float, const int*, bool);
@@ -384,8 +386,8 @@ bool launch_gemm_glds(const GemmArgs& a, int cfg, int splitk, void* workspace, h
     if (cfg < kNumCfg && kKStep[cfg] != 64) cfg = 3;  // K groups: no in-kernel row statistics
   }
   // the SwiGLU epilogue pairs 16-column gate/up fragments: wave tiles must be multiples of 32
-  // columns (configs 22-27 have 48- / 144-column wave tiles)
-  if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
+  // columns (configs 22-27, 38, 39: 48- / 144-column wave tiles; 36: 112)
+  if (a.act == kActSwiglu && swiglu_bad(cfg)) cfg = kKStep[cfg] == 64 ? 3 : 17;
   return kLaunch[cfg < kNumCfg ? cfg : 3](a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, persist);
 }
 
@@ -393,6 +395,6 @@ void launch_gemm_glds_grouped(const GemmArgs& a, int cfg, int n_groups, const in
                               const unsigned long long* w_ptrs, const unsigned long long* c_ptrs, hipStream_t s,
                               const int* a_rows) {
   cfg &= kGemmPersist - 1;
-  if (a.act == kActSwiglu && cfg >= 22 && cfg <= 27) cfg = kKStep[cfg] == 64 ? 3 : 17;
+  if (a.act == kActSwiglu && swiglu_bad(cfg)) cfg = kKStep[cfg] == 64 ? 3 : 17;
   kGrouped[cfg < kNumCfg ? cfg : 3](a, n_groups, offsets, w_ptrs, c_ptrs, s, a_rows);
 }

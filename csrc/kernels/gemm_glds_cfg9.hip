@@ -1,0 +1,5 @@
+// Tile configs 36, 37 of the LDS-DMA GEMM (gemm_glds_impl.h).
+#include "gemm_glds_impl.h"
+
+DLS_GLDS_DEFINE(36)
+DLS_GLDS_DEFINE(37)

@@ -69,16 +69,18 @@ struct Cfg {
   static constexpr int BK = 64, CH = 8;
   static constexpr int NW = WM * WN, T = 64 * NW * KG;
   static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  static constexpr int ROWS = BM + BN, INSTR = ROWS / 8, PW = INSTR / NW;
+  // DMA instructions (8 rows x 128 B each) per wave: when the rows do not split evenly over
+  // the waves, the last waves repeat the stage's last instruction (same bytes to the same LDS
+  // slot), so every wave issues the same count and the counted vmcnt waits stay uniform
+  static constexpr int ROWS = BM + BN, INSTR = ROWS / 8, PW = (INSTR + NW - 1) / NW;
   static constexpr int SUB = ROWS * CH;     // one 64-deep K-tile image (bf16x8 units)
   static constexpr int STAGE = SUB * KG;    // bf16x8 units
   // split staging (BXS > 0): separate A / W rings
   static constexpr int SA = STAGES, SB = STAGES + BXS;
-  static constexpr int PWA = BM / 8 / NW, PWB = BN / 8 / NW;
+  static constexpr int PWA = (BM / 8 + NW - 1) / NW, PWB = (BN / 8 + NW - 1) / NW;
   static constexpr int A_STAGE = BM * CH, B_STAGE = BN * CH;
   static constexpr int LDS_UNITS = BXS ? SA * A_STAGE + SB * B_STAGE : STAGES * STAGE;
-  static_assert(INSTR % NW == 0, "stage rows must split evenly over waves");
-  static_assert(!BXS || ((BM / 8) % NW == 0 && (BN / 8) % NW == 0), "split rings: rows must split over waves");
+  static_assert(BM % 8 == 0 && BN % 8 == 0, "DMA pieces are 8 rows");
   static_assert(FM >= 1 && FN >= 1, "wave tile too small");
   static_assert(PW * (STAGES - 2) <= 63, "vmcnt range");
   static_assert(STAGES >= 2 && STAGES <= 8, "stages");
@@ -116,32 +118,33 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
                                          int fmv = C::FM) {
   // All fragments of the K-tile (both 32-deep halves) are requested before the first MFMA:
   // the second half's ds_reads then complete under the first half's MFMAs instead of
-  // behind an lgkmcnt(0) (the compiler counts lgkmcnt per consumer).
-  bf16x8 af[2][C::FM], bw[2][C::FN];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
+  // behind an lgkmcnt(0) (the compiler counts lgkmcnt per consumer). Wave tiles with more
+  // than 12 fragments per half (32 x 224: 2 + 14) load one half at a time — both halves'
+  // fragments next to 28 accumulators would not fit the 256 registers of two waves per SIMD.
+  constexpr bool HALVES = C::FM + C::FN > 12;
+  constexpr int NH = HALVES ? 1 : 2;
+  bf16x8 af[NH][C::FM], bw[NH][C::FN];
+  auto load = [&](int kk, int h) {
     const int chunk = kk * 4 + (lane >> 4);
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
       const int row = wn * C::WTN + j * 16 + (lane & 15);
-      bw[kk][j] = sB[row * C::CH + (chunk ^ (row & 7))];
+      bw[h][j] = sB[row * C::CH + (chunk ^ (row & 7))];
     }
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
       if (SKIP && i >= fmv) break;
       const int row = wm * C::WTM + i * 16 + (lane & 15);
-      af[kk][i] = sA[row * C::CH + (chunk ^ (row & 7))];
+      af[h][i] = sA[row * C::CH + (chunk ^ (row & 7))];
     }
-  }
-  __builtin_amdgcn_sched_barrier(0);  // keep every ds_read ahead of the MFMAs (counted lgkmcnt waits)
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
+  };
+  auto compute = [&](int h) {
     if (ln_acc) {
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float x = bf2f(af[kk][i][e]);
+          const float x = bf2f(af[h][i][e]);
           st_s[i] += x;
           st_q[i] += x * x;
         }
@@ -153,9 +156,24 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
     for (int i = 0; i < C::FM; ++i) {
       if (SKIP && i >= fmv) break;
 #pragma unroll
-      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[kk][j], af[kk][i], acc[i][j]);
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[h][j], af[h][i], acc[i][j]);
     }
     if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  if constexpr (HALVES) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      load(kk, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    load(0, 0);
+    load(1, NH - 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep every ds_read ahead of the MFMAs (counted lgkmcnt waits)
+    compute(0);
+    compute(NH - 1);
   }
 }
 
@@ -174,7 +192,7 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
   int dst[C::PW];
 #pragma unroll
   for (int j = 0; j < C::PW; ++j) {
-    const int gi = wave * C::PW + j;
+    const int gi = min(wave * C::PW + j, C::INSTR * C::KG - 1);  // (repeats: see Cfg::PW)
     const int sub = gi / C::INSTR, r8 = gi % C::INSTR;
     const int row = 8 * r8 + (lane >> 3);
     const int gch = (lane & 7) ^ (row & 7);
@@ -376,14 +394,14 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
   const bf16* srcB[C::PWB];
 #pragma unroll
   for (int j = 0; j < C::PWA; ++j) {
-    const int row = 8 * (wave * C::PWA + j) + (lane >> 3);
+    const int row = 8 * min(wave * C::PWA + j, C::BM / 8 - 1) + (lane >> 3);
     int gm = min(m0 + row, M - 1);
     if constexpr (GATHER) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
     srcA[j] = A + (size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8;
   }
 #pragma unroll
   for (int j = 0; j < C::PWB; ++j) {
-    const int row = 8 * (wave * C::PWB + j) + (lane >> 3);
+    const int row = 8 * min(wave * C::PWB + j, C::BN / 8 - 1) + (lane >> 3);
     const int gn = min(n0 + row, N - 1);
     srcB[j] = W + (size_t)gn * ldw + kbeg + ((lane & 7) ^ (row & 7)) * 8;
   }
@@ -394,7 +412,7 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 #pragma unroll
     for (int j = 0; j < C::PWA; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + (wave * C::PWA + j) * 64), 16,
+                                       (__attribute__((address_space(3))) void*)(st + min(wave * C::PWA + j, C::BM / 8 - 1) * 64), 16,
                                        0, 0);
   };
   auto issueB = [&](int kt) {
@@ -402,7 +420,7 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 #pragma unroll
     for (int j = 0; j < C::PWB; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + (wave * C::PWB + j) * 64), 16,
+                                       (__attribute__((address_space(3))) void*)(st + min(wave * C::PWB + j, C::BN / 8 - 1) * 64), 16,
                                        0, WPOL);
   };
   constexpr int DA = C::SA - 1;
@@ -1003,6 +1021,17 @@ using C33 = Cfg<192, 128, 4, 2, 3, 0, 1>;
 // 256 x 256 with the half-tile ring main loop (mainloop_ring): LM heads and the large GEMMs
 using C34 = Cfg<256, 256, 2, 4, 2, 0, 0, 1, 1>;
 using C35 = Cfg<256, 256, 2, 4, 2, 1, 0, 1, 1>;
+// 224-column tiles: a 512-row GEMM whose N is a multiple of 7 x 32 fills the 256 CUs in whole
+// rounds (Llama-3-8B gate/up N = 28672 -> 2 x 128 = 256 tiles of 256 x 224; 256 x 256 leaves 32
+// CUs idle), and the GPT-2 LM head (N = 50304) takes 450 tiles = 1.76 rounds instead of 394
+// tiles of 256 x 256 whose second round is half empty. Split rings: 2 x 32 KiB A + 3 x 28 KiB W.
+using C36 = Cfg<256, 224, 4, 2, 2, 0, 1>;  // wave 64 x 112 (plain epilogues)
+using C37 = Cfg<256, 224, 8, 1, 2, 0, 1>;  // wave 32 x 224: SwiGLU gate/up pairs (multiples of 32)
+// 128 x 96 / 128 x 64 tiles of 8 waves for the long-K projections (K = 4096: 512 x 6144 ->
+// 4 x 64 = 256 tiles, 512 x 4096 -> 4 x 64 = 256 tiles of 128 x 64) without split-K partials
+using C38 = Cfg<128, 96, 4, 2, 4>;             // wave 32 x 48, 4 x 28 KiB stages
+using C39 = Cfg<128, 96, 2, 2, 2, 0, 0, 2>;    // two K groups of wave 64 x 48, 2 x 56 KiB stages
+using C40 = Cfg<128, 64, 2, 2, 3, 0, 0, 2>;    // two K groups of wave 64 x 32, 3 x 48 KiB stages
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,

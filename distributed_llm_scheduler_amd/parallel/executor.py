@@ -1622,13 +1622,15 @@ class DAGExecutor:
         return bool(self._segments)
 
     def refine_tuning(self, top: int = 3, reps: int = 20, min_gain: float = 0.01, force: bool = False,
-                      exhaustive: bool = False, log=None) -> Dict:
+                      exhaustive: bool = False, log=None, cfgs=None, keys=None) -> Dict:
         """GEMM config choice by WHOLE-STEP time: for every GEMM shape this rank runs (costliest
         first), try the microbenchmark's runner-up configs inside the captured hipGraph of the
         real step and keep one only if the step gets faster by > ``min_gain``. The cold-weight
         microbenchmark misses the DAG's cache state and neighbour kernels; this does not.
         ``exhaustive``: every valid (config, split-K <= 4) of the shape instead of the runner-ups
-        (``log(key, cand, ms)`` sees each timing). Persists the choices (ops/gemm_tuning.json).
+        (``log(key, cand, ms)`` sees each timing); ``cfgs``: only candidates with these config ids
+        (e.g. newly added tile configs against the current choice); ``keys``: only these shape
+        keys ("MxNxK[tag]"). Persists the choices (ops/gemm_tuning.json).
         Returns {key: (old, new, step_ms)}."""
         from ..ops import tuning
 
@@ -1653,7 +1655,11 @@ class DAGExecutor:
             return sorted(ts)[1]
 
         shapes = sorted(self.gemm_shapes(), key=lambda s: -(s[0] * s[1] * s[2]))
+        if keys:
+            shapes = [s for s in shapes if f"{s[0]}x{s[1]}x{s[2]}{s[3]}" in keys]
         base = step_ms()
+        if log is not None:
+            log("baseline", (), base)
         changes = {}
         for sh in shapes:
             M, N, K, tg = sh
@@ -1671,6 +1677,9 @@ class DAGExecutor:
                          if c[1] <= 4 and (c[0] < tuning.REGSTAGE or c[0] == tuning.LIB)]
             else:
                 cands = tuning.runner_ups(M, N, K, tg, top + 1)
+            if cfgs:
+                cands = [c for c in tuning.candidates(M, N, K, ops.ext().gemm_glds_num_configs(), tg)
+                         if c[0] in cfgs and c[1] <= 4]
             for cand in cands:
                 if tuple(cand) == tuple(cur):
                     continue

@@ -50,7 +50,8 @@ def test_gemm_identity_asymmetric():
                                            (20, 1), (21, 1), (21, 3), (22, 1), (23, 1), (24, 1),
                                            (25, 1), (26, 1), (27, 1), (22, 4), (24, 2), (27, 3), (28, 1), (28, 2),
                                            (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2),
-                                           (34, 1), (35, 1), (34, 2), (34, 3), (98, 1)])
+                                           (34, 1), (35, 1), (34, 2), (34, 3), (98, 1),
+                                           (36, 1), (37, 1), (36, 2), (38, 1), (38, 2), (39, 1), (40, 1), (40, 3)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
@@ -226,7 +227,8 @@ def _ref_swiglu(x, w13, bias=None):
 
 
 @pytest.mark.parametrize("config,splitk", [(-1, 0), (0, 1), (3, 1), (3, 4), (8, 1), (7, 2), (2, 1), (12, 1),
-                                           (14, 2), (15, 1), (17, 1), (16, 2), (21, 1), (22, 1), (25, 2)])
+                                           (14, 2), (15, 1), (17, 1), (16, 2), (21, 1), (22, 1), (25, 2),
+                                           (37, 1), (37, 2), (40, 1), (36, 1)])
 @pytest.mark.parametrize("M,F,K", [(512, 1024, 768), (200, 512, 1024), (64, 96, 128)])
 def test_gemm_swiglu_epilogue(M, F, K, config, splitk):
     if config >= 16 and K % (ops.ext().gemm_glds_kstep(config) * splitk):
@@ -513,7 +515,8 @@ def test_gemm_emits_row_stats(config, splitk, N):
 
 @pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
 @pytest.mark.parametrize("config,splitk,act", [(3, 1, 0), (3, 4, 1), (0, 2, 0), (8, 1, 0), (12, 2, 0), (3, 1, 4),
-                                               (34, 1, 0), (34, 2, 1), (35, 1, 0)])
+                                               (34, 1, 0), (34, 2, 1), (35, 1, 0),
+                                               (36, 1, 0), (37, 1, 4), (38, 1, 0), (39, 2, 0), (40, 1, 1)])
 def test_gemm_folded_norm_external_stats(mode, config, splitk, act):
     M, N, K = 256, 1024, 2048
     x = _rand(M, K, scale=2.0, seed=110) + 0.3
