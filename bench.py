@@ -30,6 +30,7 @@ import gc
 import json
 import os
 import sys
+import threading
 import time
 
 import torch
@@ -189,6 +190,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="headline only (no capped / strong sub-results)")
     ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of each capped / strong sub-run")
     ap.add_argument("--strong-mb", type=int, default=8, help="micro-batches of the strong-scaling pipeline run")
+    ap.add_argument("--extras-timeout", type=float, default=300.0,
+                    help="seconds the capped / strong sub-results may take before the headline is printed without them")
     ap.add_argument("--profile", action="store_true", help="also print a measured per-kernel timeline")
     ap.add_argument("--trace-out", default=None, help="write a measured Chrome trace (all ranks) to this path")
     ap.add_argument("--roctx", action="store_true", help="roctx range per DAG instruction (rocprofv3 --marker-trace)")
@@ -222,30 +225,11 @@ def main():
                cost_model=args.cost_model, placement=args.placement, tp=args.tp, sp=args.sp, init=args.init,
                refine=args.refine_tuning, roctx=args.roctx, profile=args.profile, trace_out=args.trace_out, **common)
 
-    extras = {}
-    if not args.no_extras:
-        ew = min(args.warmup, 2)
-        # the reference's 80 % memory regime, executed (one request per GPU, each GPU capped at
-        # 80 % of one request DAG's need under the reference's cost model)
-        cap80 = regime_cap_gb(args.model, 0.8, args.batch, args.seq, "reference")
-        capped = {"memory_regime": 0.8, "cost_model": "reference", "mem_cap_gb_per_gpu": cap80}
-        for sched in ("MRU_spec", "EFT", "DFS"):
-            r = run(ctx, args.extra_steps, ew, scheduler=sched, cap_gb=cap80, replicas=world,
-                    cost_model="reference", placement="scheduler", tag=f":capped-{sched}", **common)
-            capped[sched] = {k: r[k] for k in ("tasks_completed", "tasks_total", "ms_per_step", "refill_gb_per_step",
-                                               "param_loads_per_step", "param_evictions_per_step", "cross_gpu_edges")}
-        extras["capped"] = capped
-        # strong scaling with real cross-GPU edges: a fixed batch of micro-batches, pipeline
-        # placement over the N GPUs (at N = 1: the same batch on one GPU)
-        r = run(ctx, args.extra_steps, ew, scheduler="EFT", cap_gb=288.0, replicas=args.strong_mb,
-                cost_model="bytes", placement="pipeline", tag=":strong", **common)
-        extras["strong"] = {"micro_batches": args.strong_mb, "placement": f"pipeline over {world} GPU(s)",
-                            "scaling": "strong",
-                            "tokens_per_step": args.strong_mb * args.batch * args.seq,
-                            **{k: r[k] for k in ("ms_per_step", "per_rank_ms", "tasks_completed", "tasks_total",
-                                                 "cross_gpu_edges", "cross_gpu_bytes", "hip_graph")}}
+    def emit(extras):
+        if rank == 0:
+            print(json.dumps(result(head, extras)), flush=True)
 
-    if rank == 0:
+    def result(head, extras):
         ms = head["ms_per_step"]
         tokens = replicas * args.batch * args.seq
         pname = head["scheduler"] if args.placement == "scheduler" else args.placement
@@ -295,7 +279,60 @@ def main():
         }
         if "timeline_ms" in head:
             out["timeline_ms"] = head["timeline_ms"]
-        print(json.dumps(out), flush=True)
+        return out
+
+    extras = {}
+    # The sub-results must never cost the headline: if they have not finished within
+    # --extras-timeout seconds (a multi-GPU sub-run stuck in a collective, say), every rank's
+    # watchdog fires — rank 0 prints the headline line with the extras marked unfinished and
+    # each rank exits (os._exit: no collective teardown that could block on a stuck peer).
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(args.extras_timeout):
+            log(f"[bench] rank {rank}: sub-results unfinished after {args.extras_timeout} s; exiting")
+            emit({**extras, "extras_error": f"sub-results unfinished after {args.extras_timeout} s"})
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+
+    if not args.no_extras:
+        threading.Thread(target=watchdog, daemon=True).start()
+    if not args.no_extras:
+        ew = min(args.warmup, 2)
+        # the reference's 80 % memory regime, executed (one request per GPU, each GPU capped at
+        # 80 % of one request DAG's need under the reference's cost model)
+        cap80 = regime_cap_gb(args.model, 0.8, args.batch, args.seq, "reference")
+        capped = {"memory_regime": 0.8, "cost_model": "reference", "mem_cap_gb_per_gpu": cap80}
+        extras["capped"] = capped
+        for sched in ("MRU_spec", "EFT", "DFS"):
+            try:
+                r = run(ctx, args.extra_steps, ew, scheduler=sched, cap_gb=cap80, replicas=world,
+                        cost_model="reference", placement="scheduler", tag=f":capped-{sched}", **common)
+            except Exception as e:  # noqa: BLE001 — recorded in the JSON line, the headline stands
+                log(f"[bench] capped {sched} failed: {e!r}")
+                capped[sched] = {"error": repr(e)[:300]}
+                continue
+            capped[sched] = {k: r[k] for k in ("tasks_completed", "tasks_total", "ms_per_step", "refill_gb_per_step",
+                                               "param_loads_per_step", "param_evictions_per_step", "cross_gpu_edges")}
+        # strong scaling with real cross-GPU edges: a fixed batch of micro-batches, pipeline
+        # placement over the N GPUs (at N = 1: the same batch on one GPU)
+        strong = {"micro_batches": args.strong_mb, "placement": f"pipeline over {world} GPU(s)", "scaling": "strong",
+                  "tokens_per_step": args.strong_mb * args.batch * args.seq}
+        extras["strong"] = strong
+        try:
+            r = run(ctx, args.extra_steps, ew, scheduler="EFT", cap_gb=288.0, replicas=args.strong_mb,
+                    cost_model="bytes", placement="pipeline", tag=":strong", **common)
+            strong.update({k: r[k] for k in ("ms_per_step", "per_rank_ms", "tasks_completed", "tasks_total",
+                                             "cross_gpu_edges", "cross_gpu_bytes", "hip_graph")})
+        except Exception as e:  # noqa: BLE001
+            log(f"[bench] strong sub-run failed: {e!r}")
+            strong["error"] = repr(e)[:300]
+
+    if world > 1:
+        dist.barrier()
+    done.set()
+    emit(extras)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

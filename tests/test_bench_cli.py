@@ -102,3 +102,16 @@ def test_bench_extras_two_ranks():
         assert cap[s]["ms_per_step"] > 0 and cap[s]["tasks_total"] > 0
     assert cap["MRU_spec"]["tasks_completed"] == cap["MRU_spec"]["tasks_total"]
     assert ln["strong"]["cross_gpu_edges"] > 0 and ln["strong"]["micro_batches"] == 4
+
+
+@pytest.mark.timeout(300)
+def test_bench_extras_watchdog_keeps_headline():
+    """Sub-results that do not finish in --extras-timeout never cost the headline: every rank's
+    watchdog fires, rank 0 prints ONE line with the headline and the extras marked unfinished,
+    and the job exits 0 (2 gloo ranks)."""
+    lines = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                  "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *ARGS,
+                  "--extras-timeout", "0.01"])
+    assert len(lines) == 1
+    _check(lines[0], 2)
+    assert "unfinished" in lines[0]["extras_error"]
