@@ -54,8 +54,8 @@ __device__ __forceinline__ void wait_tiles(int ahead) {
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
 // BXS = extra weight (B) stages: 0 -> A and W tiles share STAGES buffers and travel
-// together; 1 -> A keeps STAGES buffers (it is L2-resident: short latency) while the COLD
-// weight stream gets STAGES + 1, i.e. one more tile of HBM latency covered inside the same
+// together; >= 1 -> A keeps STAGES buffers (it is L2-resident: short latency) while the COLD
+// weight stream gets STAGES + BXS, i.e. BXS more tiles of HBM latency covered inside the same
 // 160 KiB of LDS (e.g. 256x256: 2 x 32 KiB A + 3 x 32 KiB W).
 // KG_ = K groups: KG wave groups of WM x WN waves share each output tile; a stage holds KG
 // consecutive 64-deep K-tiles and group g multiplies tile g of every stage (intra-block
@@ -83,6 +83,7 @@ struct Cfg {
   static_assert(BM % 8 == 0 && BN % 8 == 0, "DMA pieces are 8 rows");
   static_assert(FM >= 1 && FN >= 1, "wave tile too small");
   static_assert(PW * (STAGES - 2) <= 63, "vmcnt range");
+  static_assert(!BXS || (SA - 2) * PWA + (SA - 1) * PWB <= 63, "vmcnt range (split rings)");
   static_assert(STAGES >= 2 && STAGES <= 8, "stages");
   static_assert(LDS_UNITS * 16 <= 163840, "LDS budget");
   static_assert(KG == 1 || (BXS == 0 && PRIO == 0), "K groups use the joint ring");
@@ -91,6 +92,24 @@ struct Cfg {
                 "the ring main loop is written for 256x256 tiles, 8 waves as 2 x 4, 8 x 16 KiB slots");
 };
 
+// split rings with a W ring D = BXS tiles deeper than the A ring: wait until at most
+// a*PWA + b*PWB DMA instructions are outstanding, a in [0, AM], b in [0, BM] (any pair)
+template <int PWA, int PWB, int AM, int BM>
+__device__ __forceinline__ void wait_ab_any(int a, int b) {
+  if constexpr (AM > 0) {
+    if (a < AM) {
+      wait_ab_any<PWA, PWB, AM - 1, BM>(a, b);
+      return;
+    }
+  }
+  if constexpr (BM > 0) {
+    if (b < BM) {
+      wait_ab_any<PWA, PWB, AM, BM - 1>(a, b);
+      return;
+    }
+  }
+  wait_vm<AM * PWA + BM * PWB>();
+}
 // split rings: wait until at most a*PWA + b*PWB DMA instructions are outstanding, with
 // a in [0, AMAX] and b in {a, a + 1} (see the issue order in glds_tile)
 template <int PWA, int PWB, int A>
@@ -389,7 +408,8 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
                                                int kbeg, int nk, int lane, int wave, int wm, int wn, bool ln_acc,
                                                f32x4 (&acc)[C::FM][C::FN], float (&st_s)[C::FM],
                                                float (&st_q)[C::FM], int fmv, const int* __restrict__ arows) {
-  static_assert(C::SB == C::SA + 1, "split rings: W ring is one deeper than A");
+  constexpr int D = C::SB - C::SA;  // W tiles issued ahead of the A tile of the same K step
+  static_assert(D >= 1, "split rings: the W ring is deeper than the A ring");
   const bf16* srcA[C::PWA];
   const bf16* srcB[C::PWB];
 #pragma unroll
@@ -424,19 +444,23 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
                                        0, WPOL);
   };
   constexpr int DA = C::SA - 1;
-  issueB(0);
+#pragma unroll
+  for (int q = 0; q < D; ++q)
+    if (q < nk) issueB(q);
 #pragma unroll
   for (int s = 0; s < DA; ++s) {
     if (s < nk) issueA(s);
-    if (s + 1 < nk) issueB(s + 1);
+    if (s + D < nk) issueB(s + D);
   }
   for (int kt = 0; kt < nk; ++kt) {
     const int a = min(DA - 1, nk - 1 - kt);
-    const int b = min(a + 1, nk - 1 - kt);
-    wait_ab<C::PWA, C::PWB, DA - 1>(a, b);
+    // W tiles issued after A(kt): B(kt + D) .. B(min(kt + DA - 1 + D, nk - 1))
+    const int b = max(0, min(DA, nk - kt - D));
+    if constexpr (D == 1) wait_ab<C::PWA, C::PWB, DA - 1>(a, b);
+    else wait_ab_any<C::PWA, C::PWB, DA - 1, DA>(a, b);
     raw_barrier();
     if (kt + DA < nk) issueA(kt + DA);
-    if (kt + DA + 1 < nk) issueB(kt + DA + 1);
+    if (kt + DA + D < nk) issueB(kt + DA + D);
     mma_tile<C, SKIP>(ringA + (kt % C::SA) * C::A_STAGE, ringB + (kt % C::SB) * C::B_STAGE, lane, wm, wn, ln_acc,
                       acc, st_s, st_q, fmv);
   }
@@ -1032,6 +1056,9 @@ using C37 = Cfg<256, 224, 8, 1, 2, 0, 1>;  // wave 32 x 224: SwiGLU gate/up pair
 using C38 = Cfg<128, 96, 4, 2, 4>;             // wave 32 x 48, 4 x 28 KiB stages
 using C39 = Cfg<128, 96, 2, 2, 2, 0, 0, 2>;    // two K groups of wave 64 x 48, 2 x 56 KiB stages
 using C40 = Cfg<128, 64, 2, 2, 3, 0, 0, 2>;    // two K groups of wave 64 x 32, 3 x 48 KiB stages
+// MoE experts (192 routed rows, cold weights): the W ring TWO tiles deeper than the A ring —
+// 3 x 24 KiB A + 5 x 16 KiB W = 152 KiB, four weight tiles (64 KiB) in flight per CU (C33: 3)
+using C41 = Cfg<192, 128, 4, 2, 3, 0, 2>;
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,
