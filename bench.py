@@ -129,6 +129,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
         "cross_gpu_bytes": st["cross_gpu_bytes"],
         "kernels_per_rank": st["kernels_per_rank"],
         "refill_gb_per_step": round(sum(st["refill_gb_per_step_per_rank"]), 6),
+        "peer_fill_gb_per_step": round(sum(st.get("peer_fill_gb_per_step_per_rank", [0.0])), 6),
         "param_loads_per_step": sum(1 for i in plan.programs[ctx.rank].instrs if i.op == "load"),
         "param_evictions_per_step": sum(1 for i in plan.programs[ctx.rank].instrs if i.op == "evict"),
         "hip_graph": bool(captured),
@@ -314,7 +315,8 @@ def main():
                 capped[sched] = {"error": repr(e)[:300]}
                 continue
             capped[sched] = {k: r[k] for k in ("tasks_completed", "tasks_total", "ms_per_step", "refill_gb_per_step",
-                                               "param_loads_per_step", "param_evictions_per_step", "cross_gpu_edges")}
+                                               "peer_fill_gb_per_step", "param_loads_per_step",
+                                               "param_evictions_per_step", "cross_gpu_edges")}
         # strong scaling with real cross-GPU edges: a fixed batch of micro-batches, pipeline
         # placement over the N GPUs (at N = 1: the same batch on one GPU)
         strong = {"micro_batches": args.strong_mb, "placement": f"pipeline over {world} GPU(s)", "scaling": "strong",

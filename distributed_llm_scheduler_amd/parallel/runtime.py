@@ -262,6 +262,9 @@ def plan_stats(p: Plan) -> Dict:
         "act_arena_gb_per_rank": [pr.act_arena_bytes / 1e9 for pr in p.programs],
         # parameter bytes re-filled per steady-state step (evict/reload traffic of the plan)
         "refill_gb_per_step_per_rank": [steady_fill_bytes(pr, p.param_bytes) / 1e9 for pr in p.programs],
+        # of which received from a peer GPU's arena over xGMI (RCCL p2p) instead of the host
+        "peer_fill_gb_per_step_per_rank": [sum(int(p.param_bytes.get(i.param, 0)) for i in pr.instrs
+                                               if i.op == "load" and i.peer >= 0) / 1e9 for pr in p.programs],
         "tasks_per_rank": [sum(1 for r in p.placement.values() if r == k) for k in range(p.world)],
     }
 
