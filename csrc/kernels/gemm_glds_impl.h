@@ -78,6 +78,7 @@ struct Cfg {
   // split staging (BXS > 0): separate A / W rings
   static constexpr int SA = STAGES, SB = STAGES + BXS;
   static constexpr int PWA = (BM / 8 + NW - 1) / NW, PWB = (BN / 8 + NW - 1) / NW;
+  static constexpr bool EVEN = INSTR % NW == 0, EVEN_A = (BM / 8) % NW == 0, EVEN_B = (BN / 8) % NW == 0;
   static constexpr int A_STAGE = BM * CH, B_STAGE = BN * CH;
   static constexpr int LDS_UNITS = BXS ? SA * A_STAGE + SB * B_STAGE : STAGES * STAGE;
   static_assert(BM % 8 == 0 && BN % 8 == 0, "DMA pieces are 8 rows");
@@ -141,58 +142,84 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
   // than 12 fragments per half (32 x 224: 2 + 14) load one half at a time — both halves'
   // fragments next to 28 accumulators would not fit the 256 registers of two waves per SIMD.
   constexpr bool HALVES = C::FM + C::FN > 12;
-  constexpr int NH = HALVES ? 1 : 2;
-  bf16x8 af[NH][C::FM], bw[NH][C::FN];
-  auto load = [&](int kk, int h) {
-    const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-      const int row = wn * C::WTN + j * 16 + (lane & 15);
-      bw[h][j] = sB[row * C::CH + (chunk ^ (row & 7))];
-    }
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      if (SKIP && i >= fmv) break;
-      const int row = wm * C::WTM + i * 16 + (lane & 15);
-      af[h][i] = sA[row * C::CH + (chunk ^ (row & 7))];
-    }
-  };
-  auto compute = [&](int h) {
-    if (ln_acc) {
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = bf2f(af[h][i][e]);
-          st_s[i] += x;
-          st_q[i] += x * x;
-        }
-    }
-    // swapped operands: acc = (W A^T) tile, i.e. C^T — lane holds 4 consecutive output
-    // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
-    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      if (SKIP && i >= fmv) break;
-#pragma unroll
-      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[h][j], af[h][i], acc[i][j]);
-    }
-    if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
-  };
-  if constexpr (HALVES) {
+  if constexpr (!HALVES) {
+    bf16x8 af[2][C::FM], bw[2][C::FN];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      load(kk, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(0);
-      __builtin_amdgcn_sched_barrier(0);
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int row = wn * C::WTN + j * 16 + (lane & 15);
+        bw[kk][j] = sB[row * C::CH + (chunk ^ (row & 7))];
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        if (SKIP && i >= fmv) break;
+        const int row = wm * C::WTM + i * 16 + (lane & 15);
+        af[kk][i] = sA[row * C::CH + (chunk ^ (row & 7))];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep every ds_read ahead of the MFMAs (counted lgkmcnt waits)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (ln_acc) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = bf2f(af[kk][i][e]);
+            st_s[i] += x;
+            st_q[i] += x * x;
+          }
+      }
+      // swapped operands: acc = (W A^T) tile, i.e. C^T — lane holds 4 consecutive output
+      // COLUMNS of one row, so the epilogue moves 8-byte vectors instead of bf16 scalars
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        if (SKIP && i >= fmv) break;
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[kk][j], af[kk][i], acc[i][j]);
+      }
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
     }
   } else {
-    load(0, 0);
-    load(1, NH - 1);
-    __builtin_amdgcn_sched_barrier(0);  // keep every ds_read ahead of the MFMAs (counted lgkmcnt waits)
-    compute(0);
-    compute(NH - 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[C::FM], bw[C::FN];
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int row = wn * C::WTN + j * 16 + (lane & 15);
+        bw[j] = sB[row * C::CH + (chunk ^ (row & 7))];
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        if (SKIP && i >= fmv) break;
+        const int row = wm * C::WTM + i * 16 + (lane & 15);
+        af[i] = sA[row * C::CH + (chunk ^ (row & 7))];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (ln_acc) {
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = bf2f(af[i][e]);
+            st_s[i] += x;
+            st_q[i] += x * x;
+          }
+      }
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        if (SKIP && i >= fmv) break;
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32(bw[j], af[i], acc[i][j]);
+      }
+      if constexpr (C::PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 
@@ -211,7 +238,7 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
   int dst[C::PW];
 #pragma unroll
   for (int j = 0; j < C::PW; ++j) {
-    const int gi = min(wave * C::PW + j, C::INSTR * C::KG - 1);  // (repeats: see Cfg::PW)
+    const int gi = C::EVEN ? wave * C::PW + j : min(wave * C::PW + j, C::INSTR * C::KG - 1);  // (repeats: Cfg::PW)
     const int sub = gi / C::INSTR, r8 = gi % C::INSTR;
     const int row = 8 * r8 + (lane >> 3);
     const int gch = (lane & 7) ^ (row & 7);
@@ -414,14 +441,14 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
   const bf16* srcB[C::PWB];
 #pragma unroll
   for (int j = 0; j < C::PWA; ++j) {
-    const int row = 8 * min(wave * C::PWA + j, C::BM / 8 - 1) + (lane >> 3);
+    const int row = 8 * (C::EVEN_A ? wave * C::PWA + j : min(wave * C::PWA + j, C::BM / 8 - 1)) + (lane >> 3);
     int gm = min(m0 + row, M - 1);
     if constexpr (GATHER) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
     srcA[j] = A + (size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8;
   }
 #pragma unroll
   for (int j = 0; j < C::PWB; ++j) {
-    const int row = 8 * min(wave * C::PWB + j, C::BN / 8 - 1) + (lane >> 3);
+    const int row = 8 * (C::EVEN_B ? wave * C::PWB + j : min(wave * C::PWB + j, C::BN / 8 - 1)) + (lane >> 3);
     const int gn = min(n0 + row, N - 1);
     srcB[j] = W + (size_t)gn * ldw + kbeg + ((lane & 7) ^ (row & 7)) * 8;
   }
@@ -432,7 +459,7 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 #pragma unroll
     for (int j = 0; j < C::PWA; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + min(wave * C::PWA + j, C::BM / 8 - 1) * 64), 16,
+                                       (__attribute__((address_space(3))) void*)(st + (C::EVEN_A ? wave * C::PWA + j : min(wave * C::PWA + j, C::BM / 8 - 1)) * 64), 16,
                                        0, 0);
   };
   auto issueB = [&](int kt) {
@@ -440,7 +467,7 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 #pragma unroll
     for (int j = 0; j < C::PWB; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + min(wave * C::PWB + j, C::BN / 8 - 1) * 64), 16,
+                                       (__attribute__((address_space(3))) void*)(st + (C::EVEN_B ? wave * C::PWB + j : min(wave * C::PWB + j, C::BN / 8 - 1)) * 64), 16,
                                        0, WPOL);
   };
   constexpr int DA = C::SA - 1;
