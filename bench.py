@@ -191,7 +191,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="headline only (no capped / strong sub-results)")
     ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of each capped / strong sub-run")
     ap.add_argument("--strong-mb", type=int, default=8, help="micro-batches of the strong-scaling pipeline run")
-    ap.add_argument("--extras-timeout", type=float, default=300.0,
+    ap.add_argument("--extras-timeout", type=float, default=180.0,
                     help="seconds the capped / strong sub-results may take before the headline is printed without them")
     ap.add_argument("--profile", action="store_true", help="also print a measured per-kernel timeline")
     ap.add_argument("--trace-out", default=None, help="write a measured Chrome trace (all ranks) to this path")
