@@ -528,51 +528,6 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   float st_s[C::FM], st_q[C::FM];
 #pragma unroll
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
-  // Epilogue operands of SMALL tiles are requested before the K loop — the bias and folded-norm
-  // column sums of the lane's columns, the handed-over row statistics, the residual chunk each
-  // thread adds in the store pass — so their memory round trip hides under the loop instead of
-  // following it (benchmarks/gemm_stamps.hip: the epilogue was 0.9-1.2 us of a 4.8-7.3 us GPT-2
-  // GEMM). Large tiles keep their registers for the MFMA state.
-  constexpr int BNC = C::BN / 8;
-  constexpr int BNP = BNC <= 8 ? 8 : BNC <= 16 ? 16 : BNC <= 32 ? 32 : 64;
-  constexpr bool PF = C::BM * C::BN <= 64 * 128 && !SKIP && !GATHER;
-  constexpr int NQ = (C::BM * BNP + C::T - 1) / C::T;  // store-pass chunks per thread
-  const bool v16 = ((reinterpret_cast<uintptr_t>(Cp) | ((uintptr_t)ldc * 2)) & 15) == 0 &&
-                   (!R || ((reinterpret_cast<uintptr_t>(R) | ((uintptr_t)ldr * 2)) & 15) == 0);
-  float pf_b[PF ? C::FN : 1][4];
-  float pf_c[PF ? C::FN : 1][4];
-  float pf_s[PF ? C::FM : 1][2];
-  bf16x8 pf_r[PF ? NQ : 1];
-  if constexpr (PF) {
-    const int g4p = (lane >> 4) * 4;
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j) {
-      const int col = n0 + wn * C::WTN + j * 16 + g4p;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        pf_b[j][e] = bias && col + e < N ? bf2f(bias[col + e]) : 0.f;
-        pf_c[j][e] = ln_mode != 0 && col + e < N ? ln_colsum[col + e] : 0.f;
-      }
-    }
-    if (!LN && ln_mode != 0 && ep.ext_stats) {
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int row = min(m0 + wm * C::WTM + i * 16 + (lane & 15), M - 1);
-        pf_s[i][0] = ep.ext_stats[2 * row];
-        pf_s[i][1] = ep.ext_stats[2 * row + 1];
-      }
-    }
-    if (R && v16) {
-#pragma unroll
-      for (int it = 0; it < NQ; ++it) {
-        const int q = tid + it * C::T;
-        const int rl = q / BNP, cc = q % BNP;
-        const int row = m0 + rl, col = n0 + cc * 8;
-        if (q < C::BM * BNP && cc < BNC && row < M && col + 8 <= N)
-          pf_r[it] = *reinterpret_cast<const bf16x8*>(R + (size_t)row * ldr + col);
-      }
-    }
-  }
   if constexpr (C::RING && !SKIP && !GATHER)  // (grouped expert launches keep the joint ring)
     mainloop_ring<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, acc);
   else if constexpr (C::BXS > 0)
@@ -708,14 +663,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
       for (int i = 0; i < C::FM; ++i) {
         const int row = min(m0 + wm * C::WTM + i * 16 + r16, M - 1);
-        float a, q;
-        if constexpr (PF) {
-          a = pf_s[i][0];
-          q = pf_s[i][1];
-        } else {
-          a = ep.ext_stats[2 * row];
-          q = ep.ext_stats[2 * row + 1];
-        }
+        const float a = ep.ext_stats[2 * row], q = ep.ext_stats[2 * row + 1];
         const float mu = ln_mode == 1 ? a * inv_k : 0.f;
         ln_mu[i] = mu;
         ln_rs[i] = rsqrtf(fmaxf(q * inv_k - mu * mu, 0.f) + ln_eps);
@@ -805,6 +753,8 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   // ~1.2 TB/s on the 51 MB LM-head output; full rows run at the HBM write rate.
   // BNC 16-B chunks per tile row, stored in rows of BNP (power of two >= 8) chunks: image chunk
   // c of row r sits at c ^ (r & 7), and BNP consecutive lanes own one row in the store pass
+  constexpr int BNC = C::BN / 8;
+  constexpr int BNP = BNC <= 8 ? 8 : BNC <= 16 ? 16 : BNC <= 32 ? 32 : 64;
   static_assert(C::BN % 8 == 0 && BNC <= 64, "staged epilogue: BN % 8 == 0, BN <= 512");
   static_assert(C::BM * BNP * 16 <= C::LDS_UNITS * 16, "output tile image must fit the staging LDS");
   static_assert((C::BM * BNP) % 64 == 0 && ((C::BM * BNP) % C::T == 0 || C::BM * BNP < C::T),
@@ -828,17 +778,11 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
       const bool full = col + 3 < N;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       float csv[4] = {0.f, 0.f, 0.f, 0.f};  // colsum(W') of the 4 columns (folded norm)
-      if constexpr (PF) {  // requested before the K loop
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          bv[e] = pf_b[j][e];
-          csv[e] = pf_c[j][e];
-        }
-      } else if (bias) {
+      if (bias) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
       }
-      if constexpr (LNM && !PF) {
+      if constexpr (LNM) {
         if (full && (N % 4 == 0)) {
           const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_colsum + col);
 #pragma unroll
@@ -886,10 +830,13 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
   }
   __syncthreads();
   DLS_STAMP(2)
+  const bool v16 = ((reinterpret_cast<uintptr_t>(Cp) | ((uintptr_t)ldc * 2)) & 15) == 0 &&
+                   (!R || ((reinterpret_cast<uintptr_t>(R) | ((uintptr_t)ldr * 2)) & 15) == 0);
   const bf16x8* img8 = reinterpret_cast<const bf16x8*>(img);
   const int tid_ = threadIdx.x;
   // consecutive groups of BNP threads own one tile row per pass (lanes past BNC idle)
-  auto store_chunk = [&](int q, int it) {
+#pragma unroll 2
+  for (int q = tid_; q < C::BM * BNP; q += C::T) {
     const int rl = q / BNP, cc = q % BNP;
     const int row = m0 + rl, col = n0 + cc * 8;
     bf16x8 o = img8[rl * BNP + (cc ^ (rl & 7))];
@@ -897,9 +844,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     if (cc < BNC && row < M && col < N) {
       if (v16 && col + 8 <= N) {
         if (R) {
-          bf16x8 r8;
-          if constexpr (PF) r8 = pf_r[it];  // requested before the K loop
-          else r8 = *reinterpret_cast<const bf16x8*>(R + (size_t)row * ldr + col);
+          const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(R + (size_t)row * ldr + col);
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(o[e]) + bf2f(r8[e]));
         }
@@ -935,14 +880,6 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
         atomicAdd(ep.stats_out + 2 * row + 1, s2);
       }
     }
-  };
-  if constexpr (PF) {
-#pragma unroll
-    for (int it = 0; it < NQ; ++it)
-      if (tid_ + it * C::T < C::BM * BNP) store_chunk(tid_ + it * C::T, it);
-  } else {
-#pragma unroll 2
-    for (int q = tid_; q < C::BM * BNP; q += C::T) store_chunk(q, 0);
   }
   DLS_STAMP(3)
 }
