@@ -226,9 +226,18 @@ def main():
                cost_model=args.cost_model, placement=args.placement, tp=args.tp, sp=args.sp, init=args.init,
                refine=args.refine_tuning, roctx=args.roctx, profile=args.profile, trace_out=args.trace_out, **common)
 
+    emitted = threading.Lock()  # ONE line per job: whichever of the main thread / watchdog gets it
+
     def emit(extras):
+        if not emitted.acquire(blocking=False):
+            return False
         if rank == 0:
-            print(json.dumps(result(head, extras)), flush=True)
+            try:
+                line = json.dumps(result(head, extras))
+            except (RuntimeError, TypeError, ValueError):  # sub-results mutating under the watchdog
+                line = json.dumps(result(head, {"extras_error": extras.get("extras_error", "sub-results unreadable")}))
+            print(line, flush=True)
+        return True
 
     def result(head, extras):
         ms = head["ms_per_step"]
@@ -292,10 +301,10 @@ def main():
     def watchdog():
         if not done.wait(args.extras_timeout):
             log(f"[bench] rank {rank}: sub-results unfinished after {args.extras_timeout} s; exiting")
-            emit({**extras, "extras_error": f"sub-results unfinished after {args.extras_timeout} s"})
-            sys.stdout.flush()
-            sys.stderr.flush()
-            os._exit(0)
+            if emit({**extras, "extras_error": f"sub-results unfinished after {args.extras_timeout} s"}):
+                sys.stdout.flush()
+                sys.stderr.flush()
+                os._exit(0)
 
     if not args.no_extras:
         threading.Thread(target=watchdog, daemon=True).start()
