@@ -102,6 +102,10 @@ def test_bench_extras_two_ranks():
         assert cap[s]["ms_per_step"] > 0 and cap[s]["tasks_total"] > 0
     assert cap["MRU_spec"]["tasks_completed"] == cap["MRU_spec"]["tasks_total"]
     assert ln["strong"]["cross_gpu_edges"] > 0 and ln["strong"]["micro_batches"] == 4
+    # EFT keeps different equal groups resident on the two replicas: a group one rank streams is
+    # re-filled from the other rank's arena (RCCL p2p) rather than from the host
+    assert cap["EFT"]["peer_fill_gb_per_step"] > 0
+    assert cap["EFT"]["peer_fill_gb_per_step"] <= cap["EFT"]["refill_gb_per_step"]
 
 
 @pytest.mark.timeout(300)
