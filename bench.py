@@ -133,6 +133,8 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
         "param_loads_per_step": sum(1 for i in plan.programs[ctx.rank].instrs if i.op == "load"),
         "param_evictions_per_step": sum(1 for i in plan.programs[ctx.rank].instrs if i.op == "evict"),
         "hip_graph": bool(captured),
+        # segment-replayed programs (p2p or copy-stream refills): native runner or Python loop
+        "issue_mode": ex.issue_mode or ("graph" if captured else "python"),
     }
     if profile or trace_out:
         s = ex.step(profile=True)
@@ -277,6 +279,7 @@ def main():
             "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
             "per_rank_ms": head["per_rank_ms"],
             "hip_graph": head["hip_graph"],
+            "issue_mode": head["issue_mode"],
             "weights": "random-init",
             "baseline_note": "vs_baseline is null: the reference only simulates (abstract seconds from per-task "
                              "constants, dependency-free makespan; BASELINE.md), so it has no wall-clock number in "

@@ -54,6 +54,7 @@ def main():
            "instructions": len(p.programs[0].instrs), "prefetch": os.environ.get("DLS_PREFETCH", "auto")}
     for mode in ("eager", "segments", "runner"):
         exm.RUNNER = mode == "runner"
+        exm.RUNNER_MODE = "1" if mode == "runner" else "0"  # no measured fallback here
         ex = runtime.make_executor(p, 0, dev, store, use_graph=mode != "eager")
         for _ in range(3):
             ex.step()

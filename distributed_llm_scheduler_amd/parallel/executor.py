@@ -112,10 +112,12 @@ class _Recorder:
         return _REvent(self.n_events - 1)
 
 
-RUNNER = os.environ.get("DLS_RUNNER", "1") != "0"  # native step runner for segment-replayed programs
-# CPU backend (tests): the runner replays the recorded step with kernel groups as Python
-# callbacks and p2p through the gloo ProcessGroup — the same action list as on the GPU
-RUNNER_CPU = os.environ.get("DLS_RUNNER_CPU", "0") == "1"
+# native step runner for segment-replayed programs: "auto" (default) keeps it unless a
+# comm-free program's steps measure faster from the Python issue loop (Llama-3-8B at a 13.8 GB
+# cap: 55.3 vs 52.1 ms; at 15.5 GB the runner wins, 17.1 vs 18.0 — profiles/r3_final), "1"
+# always, "0" never
+RUNNER_MODE = os.environ.get("DLS_RUNNER", "auto")
+RUNNER = RUNNER_MODE != "0"
 # CPU backend (tests): the runner replays the recorded step with kernel groups as Python
 # callbacks and p2p through the gloo ProcessGroup — the same action list as on the GPU
 RUNNER_CPU = os.environ.get("DLS_RUNNER_CPU", "0") == "1"
@@ -287,6 +289,7 @@ class DAGExecutor:
         self._cap_stream = None  # side stream segment captures run on (_capture_segment)
         self._rec: Optional[_Recorder] = None   # set while a step is recorded for the runner
         self._runner = None                     # native StepRunner replaying the recorded step
+        self.issue_mode: Optional[str] = None  # "runner" / "python" for segment-replayed programs
         self._runner_stats: Optional[StepStats] = None
         self._stream_kind = 0                   # 0 compute / 1 copy stream (recording of fills)
         self._carry_at: Dict[int, List[int]] = {}  # instr -> next step's loads issued after it
@@ -1591,6 +1594,7 @@ class DAGExecutor:
             self._rec = None
         r.run()  # ... the recorded step, executed
         self._runner, self._runner_stats = r, stats
+        self.issue_mode = "runner"
         return True
 
     def _leave_runner(self) -> None:
@@ -1601,6 +1605,7 @@ class DAGExecutor:
         self._runner = None
         self._carry = {}
         self._await = {}
+        self.issue_mode = "python"
 
     def capture_segments(self) -> bool:
         """Piecewise capture for programs that must stay eager around RCCL p2p or copy-stream
@@ -1617,9 +1622,31 @@ class DAGExecutor:
         self._step_body(StepStats())  # segments captured in order as the step reaches them
         self._capture_plan = None
         torch.cuda.synchronize(self.device)
-        if self._segments:
-            self.build_runner()
+        if self._segments and self.build_runner() and RUNNER_MODE == "auto" and not self.prog.has_comm:
+            self._pick_issue_mode()
         return bool(self._segments)
+
+    def _pick_issue_mode(self, n: int = 3) -> None:
+        """Keep the native runner or the Python issue loop, whichever runs this rank's steps
+        faster (comm-free programs only: with p2p a rank's step time also depends on its peers).
+        The loop paces the issue of copy-stream fills at host speed, which on copy-bound steps
+        can beat issuing the whole step at once."""
+        def timed():
+            torch.cuda.synchronize(self.device)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                self.step()
+            torch.cuda.synchronize(self.device)
+            return (time.perf_counter() - t0) / n
+        t_runner = timed()
+        self._leave_runner()
+        self.step()  # the loop's first step re-issues the fills the runner carried across steps
+        t_loop = timed()
+        if t_loop < 0.98 * t_runner:
+            self.issue_mode = "python"
+            return
+        self.build_runner()
+        self.issue_mode = "runner"
 
     def refine_tuning(self, top: int = 3, reps: int = 20, min_gain: float = 0.01, force: bool = False,
                       exhaustive: bool = False, log=None, cfgs=None, keys=None) -> Dict:
