@@ -69,9 +69,9 @@ struct Cfg {
   static constexpr int BK = 64, CH = 8;
   static constexpr int NW = WM * WN, T = 64 * NW * KG;
   static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  // fragments of one 32-deep K half at a time (instead of both halves before the first MFMA):
-  // wave tiles with many fragments, or whose grouped-expert kernel would spill otherwise
-  static constexpr bool HALF_FRAGS = FM + FN > 12 || (BM == 192 && BN == 256);
+  // fragments of one 32-deep K half at a time (instead of both halves before the first MFMA)
+  // for wave tiles with many fragments (32 x 224)
+  static constexpr bool HALF_FRAGS = FM + FN > 12;
   // DMA instructions (8 rows x 128 B each) per wave: when the rows do not split evenly over
   // the waves, the last waves repeat the stage's last instruction (same bytes to the same LDS
   // slot), so every wave issues the same count and the counted vmcnt waits stay uniform
@@ -1089,9 +1089,6 @@ using C40 = Cfg<128, 64, 2, 2, 3, 0, 0, 2>;    // two K groups of wave 64 x 32, 
 // MoE experts (192 routed rows, cold weights): the W ring TWO tiles deeper than the A ring —
 // 3 x 24 KiB A + 5 x 16 KiB W = 152 KiB, four weight tiles (64 KiB) in flight per CU (C33: 3)
 using C41 = Cfg<192, 128, 4, 2, 3, 0, 2>;
-// MoE experts with half the gathered-row bytes per weight byte of C33 (192 x 256: A/W = 0.75
-// instead of 1.5): 8 waves of 96 x 64, split rings 2 x 24 KiB A + 3 x 32 KiB W = 144 KiB
-using C42 = Cfg<192, 256, 2, 4, 2, 0, 1>;
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,
