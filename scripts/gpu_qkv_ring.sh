@@ -10,3 +10,6 @@ cp distributed_llm_scheduler_amd/ops/gemm_tuning.json $O/tuning.json
 export DLS_GEMM_TUNING=$O/tuning.json
 timeout -k 10 600 python benchmarks/refine_dag.py --model llama3-8b --reps 5 --keys 512x6144x4096,512x4096x4096,512x4096x14336 --cfgs 42,43 > $O/refine.json 2> $O/refine.err || { tail -20 $O/refine.err; exit 5; }
 grep -v amdgpu $O/refine.err | tail -25
+unset DLS_GEMM_TUNING
+T0=distributed_llm_scheduler_amd/ops/gemm_tuning.json
+TAG=mixq TMO=400 STEPS=10 WARM=2 BENCH_ARGS="--model mixtral-8x7b" TABLES="$T0 benchmarks/tuning_ab/qkv_old.json" ROUNDS=2 bash scripts/gpu_ab_tables.sh || exit 6
