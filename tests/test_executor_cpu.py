@@ -550,3 +550,17 @@ def test_native_step_runner_replays_multi_rank_steps(model, kw):
     assert all(r["same"] and r["actions"] > 0 for r in res)
     errs = [e for r in res for e in r["errs"]]
     assert errs and all(err < 0.03 * scale for err, scale in errs), errs
+
+
+@pytest.mark.parametrize("model,kw", [("llama3-8b", dict(placement="pipeline")),
+                                      ("mixtral-8x7b", dict(placement="expert", replicas=1)),
+                                      ("gpt2", dict(placement="pipeline", replicas=8))])
+def test_multi_gpu_placements_keep_the_fused_groups(model, kw):
+    """Spreading a DAG over 2 / 8 GPUs (cross-GPU edges = RCCL p2p) keeps every fused kernel
+    group of the 1-GPU program: the groups of all ranks add up to the same count (planning only,
+    full-size models)."""
+    one = sum(runtime.plan(model, world=1, replicas=kw.get("replicas", 1)).stats["kernels_per_rank"])
+    for world in (2, 8):
+        p = runtime.plan(model, world=world, **kw)
+        assert p.stats["cross_gpu_edges"] > 0
+        assert sum(p.stats["kernels_per_rank"]) == one, (world, p.stats["kernels_per_rank"], one)
