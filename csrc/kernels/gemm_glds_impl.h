@@ -1089,11 +1089,6 @@ using C40 = Cfg<128, 64, 2, 2, 3, 0, 0, 2>;    // two K groups of wave 64 x 32, 
 // MoE experts (192 routed rows, cold weights): the W ring TWO tiles deeper than the A ring —
 // 3 x 24 KiB A + 5 x 16 KiB W = 152 KiB, four weight tiles (64 KiB) in flight per CU (C33: 3)
 using C41 = Cfg<192, 128, 4, 2, 3, 0, 2>;
-// 128 x 96 with more K-tiles in flight for cold-weight K = 4096 projections: joint ring of 5
-// stages (140 KiB, four in flight) / split rings with the W ring two tiles deeper (3 x 16 KiB A +
-// 5 x 12 KiB W = 108 KiB)
-using C42 = Cfg<128, 96, 4, 2, 5>;
-using C43 = Cfg<128, 96, 4, 2, 3, 0, 2>;
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,

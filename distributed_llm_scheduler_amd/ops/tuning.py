@@ -24,6 +24,10 @@ _lock = threading.Lock()
 _table: Optional[Dict[str, Tuple[int, int]]] = None
 _cands: Dict[str, list] = {}     # key -> runner-up (cfg, splitk) by microbenchmark time (for in-DAG refinement)
 _refined: Dict[str, bool] = {}   # key -> chosen by whole-step timing inside a DAG
+# model -> {key: choice}: a model whose step measured faster with another config for a shape it
+# shares with other models (Mixtral-8x7B's QKV GEMM after the MoE layer vs Llama-3-8B's)
+_overrides: Dict[str, Dict[str, Tuple[int, int]]] = {}
+_model: Optional[str] = None
 REGSTAGE = 100  # config ids >= 100 select the register-staged kernel (csrc ops_binding kRegStage)
 PERSIST = 64    # config | 64: the same LDS-DMA tile config as a persistent launch (kernels.h kGemmPersist)
 LIB = 200       # the vendor library (hipBLASLt through torch.mm): a candidate for PLAIN GEMMs only —
@@ -52,15 +56,27 @@ def table() -> Dict[str, Tuple[int, int]]:
                     _table = {k: tuple(v) for k, v in doc.get("gemm", {}).items()}
                     _cands.update({k: [tuple(c) for c in v] for k, v in doc.get("candidates", {}).items()})
                     _refined.update(doc.get("refined", {}))
+                    _overrides.update({m: {k: tuple(v) for k, v in t.items()}
+                                       for m, t in doc.get("model_overrides", {}).items()})
                 except (OSError, ValueError):
                     _table = {}
         return _table
 
 
+def set_model(name: Optional[str]) -> None:
+    """The model whose step the following GEMMs belong to (its ``model_overrides`` apply)."""
+    global _model
+    _model = name
+
+
 def lookup(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
-    """(config, splitk) for this shape/variant: tuned if known (a variant falls back to the
-    plain shape's LDS-DMA choice), else (-1, 0) = kernel heuristic."""
+    """(config, splitk) for this shape/variant: the current model's override if it has one,
+    else tuned if known (a variant falls back to the plain shape's LDS-DMA choice), else
+    (-1, 0) = kernel heuristic."""
     t = table()
+    v = _overrides.get(_model, {}).get(_key(M, N, K, tg))
+    if v is not None:
+        return v
     v = t.get(_key(M, N, K, tg))
     if v is None and tg:
         v = t.get(_key(M, N, K))
@@ -91,7 +107,9 @@ def _save() -> None:
         with open(tmp, "w") as f:
             json.dump({"device": "MI355X (gfx950)", "gemm": {k: list(v) for k, v in sorted(table().items())},
                        "candidates": {k: [list(c) for c in v] for k, v in sorted(_cands.items())},
-                       "refined": dict(sorted(_refined.items()))}, f, indent=1)
+                       "refined": dict(sorted(_refined.items())),
+                       "model_overrides": {m: {k: list(v) for k, v in sorted(t.items())}
+                                           for m, t in sorted(_overrides.items())}}, f, indent=1)
         os.replace(tmp, _PATH)
     except OSError:
         try:
@@ -127,9 +145,9 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
 
 
 # csrc gemm_glds kKStep: K granularity per LDS-DMA config id (64; 128 / 256 for two / four K groups)
-_KSTEP = [64] * 16 + [128] * 4 + [256] * 2 + [64] * 3 + [128] * 4 + [64, 128, 64, 64, 64] + [64, 64] + [64, 64, 64, 128, 128, 64, 64, 64]
+_KSTEP = [64] * 16 + [128] * 4 + [256] * 2 + [64] * 3 + [128] * 4 + [64, 128, 64, 64, 64] + [64, 64] + [64, 64, 64, 128, 128, 64]
 # configs whose 48- / 112- / 144-column wave tiles cannot pair SwiGLU gate/up fragments
-SWIGLU_BAD = frozenset(range(22, 28)) | {36, 38, 39, 42, 43}
+SWIGLU_BAD = frozenset(range(22, 28)) | {36, 38, 39}
 
 
 def kstep(cfg: int) -> int:
@@ -241,7 +259,11 @@ def _tune_grouped(e, M: int, N: int, K: int, dev, act: int, tg: str, save: bool)
 
 
 def set_choice(M: int, N: int, K: int, tg: str, choice: Tuple[int, int]) -> None:
-    table()[_key(M, N, K, tg)] = tuple(choice)
+    k = _key(M, N, K, tg)
+    if k in _overrides.get(_model, {}):  # the current model's own choice for a shared shape
+        _overrides[_model][k] = tuple(choice)
+    else:
+        table()[k] = tuple(choice)
 
 
 def runner_ups(M: int, N: int, K: int, tg: str = "", n: int = 3) -> list:

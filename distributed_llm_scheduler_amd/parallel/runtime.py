@@ -284,8 +284,10 @@ def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None
                   trace: bool = False, debug: bool = False):
     """``debug=True``: validate every rank's program first (parallel/validate.py) and run the
     executor with arena canaries and output finiteness checks."""
+    from ..ops import tuning
     from .executor import DAGExecutor
 
+    tuning.set_model(p.model)  # per-model GEMM choices (tuning.lookup) for this executor's steps
     if debug:
         from .validate import check_plan
 
