@@ -1,0 +1,5 @@
+// Tile configs 42, 43 of the LDS-DMA GEMM (gemm_glds_impl.h).
+#include "gemm_glds_impl.h"
+
+DLS_GLDS_DEFINE(42)
+DLS_GLDS_DEFINE(43)
