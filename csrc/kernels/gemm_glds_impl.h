@@ -1089,11 +1089,6 @@ using C40 = Cfg<128, 64, 2, 2, 3, 0, 0, 2>;    // two K groups of wave 64 x 32, 
 // MoE experts (192 routed rows, cold weights): the W ring TWO tiles deeper than the A ring —
 // 3 x 24 KiB A + 5 x 16 KiB W = 152 KiB, four weight tiles (64 KiB) in flight per CU (C33: 3)
 using C41 = Cfg<192, 128, 4, 2, 3, 0, 2>;
-// 64 x 48 tiles for the skinny N = 768 GEMMs of GPT-2 with split-K: 8 x 16 tiles x 2 K slices =
-// 256 blocks whose fp32 partials (12 KiB per slice) the in-launch combine sums (fc2, K = 3072:
-// 344 KB per CU instead of the 491 KB of one 32 x 48 tile over the whole K)
-using C42 = Cfg<64, 48, 2, 1, 4, 0, 0, 2>;  // two K groups of 2 waves (wave 32 x 48), 4 x 28 KiB stages
-using C43 = Cfg<64, 48, 2, 1, 4>;           // 2 waves, 4 x 14 KiB stages (several blocks per CU)
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,

@@ -52,7 +52,7 @@ def test_gemm_identity_asymmetric():
                                            (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2),
                                            (34, 1), (35, 1), (34, 2), (34, 3), (98, 1),
                                            (36, 1), (37, 1), (36, 2), (38, 1), (38, 2), (39, 1), (40, 1), (40, 3),
-                                           (41, 1), (41, 2), (12, 3), (31, 1), (42, 1), (42, 2), (42, 4), (43, 1), (43, 2)])
+                                           (41, 1), (41, 2), (12, 3), (31, 1)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
@@ -65,12 +65,11 @@ def test_gemm_shapes(M, N, K, config, splitk):
 
 
 @pytest.mark.parametrize("splitk", [1, 2, 4])
-@pytest.mark.parametrize("config", [3, 42])
-def test_gemm_splitk_epilogue(splitk, config):
+def test_gemm_splitk_epilogue(splitk):
     M, N, K = 512, 768, 3072
     x, w = _rand(M, K, seed=30), _rand(N, K, scale=0.02, seed=31)
     bias, res = _rand(N, scale=0.5, seed=32), _rand(M, N, seed=33)
-    y = ops.ext().gemm(x, w, bias, res, 1, 1.0, None, config, splitk)
+    y = ops.ext().gemm(x, w, bias, res, 1, 1.0, None, 3, splitk)
     ref = ops.ref_linear(x.cpu(), w.cpu(), bias.cpu(), "gelu", res.cpu())
     _close(y.cpu(), ref, 2e-2)
 
