@@ -989,7 +989,12 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
   // in-launch combine only while the last arriver's serial read of the other slices stays small
   // (cdna_hip_programming.md: ~1 us per 16 KB; Llama-3-8B's 256x128 split-4 tiles would read
   // 384 KB in one block, far slower than the reduce kernel)
-  const bool fixup = splitk > 1 && !rows && (splitk - 1) * C::BM * C::BN * 4 <= 64 * 1024;
+  // (DLS_FIXUP_MAX_KB: the largest slab read, in KiB, for which the combine stays in-launch)
+  static const int fixup_max = [] {
+    const char* e = std::getenv("DLS_FIXUP_MAX_KB");
+    return (e && *e ? std::atoi(e) : 64) * 1024;
+  }();
+  const bool fixup = splitk > 1 && !rows && (splitk - 1) * C::BM * C::BN * 4 <= fixup_max;
   const Epi ep{a.rope, a.stats_out, a.ext_stats, fixup ? a.tile_sem : nullptr};
   static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
   const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;

@@ -10,7 +10,7 @@ export DLS_SKIP_BUILD=1
 TAG=${TAG:-ab}
 for i in $(seq ${ROUNDS:-3}); do
   for e in $TABLES; do
-    t=${e%%@*}; ev=""; [ "$e" != "$t" ] && ev=${e#*@}   # entry: table[@VAR=VALUE]
+    t=${e%%@*}; ev=""; [ "$e" != "$t" ] && ev=${e#*@}; ev=${ev//,/ }   # entry: table[@VAR=VALUE[,VAR=VALUE]]
     env DLS_GEMM_TUNING="$t" $ev timeout -k 10 ${TMO:-200} python bench.py --no-extras --steps ${STEPS:-200} --warmup ${WARM:-10} ${BENCH_ARGS:-} > gpurun_out/abt/r.json 2> gpurun_out/abt/r.err || { tail -5 gpurun_out/abt/r.err; exit 3; }
     echo "$TAG $(basename $t) $ev $(python -c 'import json;print(json.load(open("gpurun_out/abt/r.json"))["ms_per_step"])')" | tee -a gpurun_out/abt/$TAG.txt
   done
