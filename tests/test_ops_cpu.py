@@ -43,3 +43,33 @@ def test_moe_route_and_gathered_grouped_gemm_cpu():
     a = ops.gemm_grouped(ops.moe_permute(x, src), ws, off, out=torch.zeros(R, F, dtype=torch.bfloat16))
     b = ops.gemm_grouped(x, ws, off, out=torch.zeros(R, F, dtype=torch.bfloat16), a_rows=src)
     assert torch.equal(a, b)
+
+
+def test_tuning_model_overrides(tmp_path, monkeypatch):
+    """A model's own choice for a GEMM shape it shares with other models (tuning
+    ``model_overrides``) wins while that model's executor runs, and in-DAG refinement of that
+    shape updates the override, not the shared entry."""
+    import json
+
+    from distributed_llm_scheduler_amd.ops import tuning
+
+    path = tmp_path / "t.json"
+    path.write_text(json.dumps({"gemm": {"512x6144x4096": [38, 1]}, "candidates": {}, "refined": {},
+                                "model_overrides": {"mixtral-8x7b": {"512x6144x4096": [0, 2]}}}))
+    monkeypatch.setattr(tuning, "_PATH", str(path))
+    monkeypatch.setattr(tuning, "_table", None)
+    monkeypatch.setattr(tuning, "_overrides", {})
+    monkeypatch.setattr(tuning, "_cands", {})
+    monkeypatch.setattr(tuning, "_refined", {})
+    monkeypatch.setattr(tuning, "_model", None)
+    assert tuning.lookup(512, 6144, 4096) == (38, 1)
+    tuning.set_model("mixtral-8x7b")
+    assert tuning.lookup(512, 6144, 4096) == (0, 2)
+    tuning.set_choice(512, 6144, 4096, "", (14, 4))
+    assert tuning.lookup(512, 6144, 4096) == (14, 4)
+    tuning.set_model("llama3-8b")
+    assert tuning.lookup(512, 6144, 4096) == (38, 1)
+    tuning.save()
+    doc = json.loads(path.read_text())
+    assert doc["gemm"]["512x6144x4096"] == [38, 1]
+    assert doc["model_overrides"]["mixtral-8x7b"]["512x6144x4096"] == [14, 4]
