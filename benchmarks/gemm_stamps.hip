@@ -1,5 +1,5 @@
 // In-kernel phase timing of one LDS-DMA GEMM config (diagnostic executable): compiles
-// csrc/kernels/gemm_glds_impl.h (configs 34, 24, 27, 17) into this translation unit with DLS_STAMP recording
+// csrc/kernels/gemm_glds_impl.h (configs 34, 24, 27, 17, 25, 22) into this translation unit with DLS_STAMP recording
 // s_memrealtime (100 MHz) per workgroup at: tile start, after the main loop, after the output
 // image is in LDS, after the store pass.
 //
@@ -23,12 +23,16 @@ DLS_GLDS_DEFINE(34)
 DLS_GLDS_DEFINE(24)
 DLS_GLDS_DEFINE(27)
 DLS_GLDS_DEFINE(17)
+DLS_GLDS_DEFINE(25)
+DLS_GLDS_DEFINE(22)
 // splitk = 1 only: the split-K reduce launcher of the library is stubbed out below
 static bool launch_gemm_glds_local(const GemmArgs& a, int cfg, int splitk) {
   switch (cfg) {
     case 24: return glds_launch_cfg24(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
     case 27: return glds_launch_cfg27(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
     case 17: return glds_launch_cfg17(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
+    case 25: return glds_launch_cfg25(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
+    case 22: return glds_launch_cfg22(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
     default: return glds_launch_cfg34(a, splitk, nullptr, 0, nullptr, 0, 1e-5f, nullptr, false);
   }
 }
