@@ -293,9 +293,16 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
     m = {"layernorm": 1, "rmsnorm": 2}[mode]
     a = ACT[act] if not isinstance(act, int) else act
     shp = x.shape[:-1] + (w_derived.shape[0] // 2 if a == SWIGLU else w_derived.shape[0],)
-    cfg, sk = tuning.lookup_fused(x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1], tuning.tag(a))
+    M, N, K = x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1]
+    cfg, sk = tuning.lookup_fused(M, N, K, tuning.tag(a))
     if ext_stats is None:
         sk = 1
+        if 0 <= cfg < tuning.REGSTAGE and tuning.kstep(cfg) != 64:
+            # in-loop row statistics need one K group: the fastest such candidate of the shape
+            # (GPT-2's first QKV, whose input comes straight from the embedding, takes the 32x48
+            # tile, not the kernel's generic 64x64 fallback: 11.6 vs 13.5 us)
+            cfg = next((int(c) for c, _ in tuning.runner_ups(M, N, K, tuning.tag(a), 8)
+                        if 0 <= c < tuning.REGSTAGE and tuning.kstep(c) == 64), -1)
     rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
     y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, sk, colsum,
                    m, float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols), None, ext_stats)
