@@ -3,10 +3,7 @@
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"; cd "$ROOT"; O=gpurun_out/pg; mkdir -p $O
 export DLS_SKIP_BUILD=1
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
-tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
-tail -1 $O/smoke.log
+timeout -k 10 300 python -u -m pytest tests/test_executor_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --no-extras --steps 200 --warmup 10 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 3; }
 python -c "import json;print(json.load(open('$O/bench.json'))['value'])"
