@@ -9,16 +9,18 @@ random-init bf16 weights, synthetic token ids. Weak scaling: one 512-token reque
 ``value`` is the step makespan in ms (max over ranks); lower is better.
 
 The same JSON line also carries (unless ``--no-extras``):
-  * ``capped``: the reference's memory-regime experiment (simulation.py:375, regime 0.8, its
-    0.5 GB-per-parameter cost model, schedulers.py:404-442 eviction) EXECUTED — GPT-2 at 80 %
-    of one request DAG's need per GPU, for the reference's MRU_spec and for EFT: tasks
-    completed, parameter bytes re-filled per step, measured ms per step;
+  * ``capped``: the reference's experiment (simulation.py:161-192, 375-376: regime 0.8, its
+    0.5 GB-per-parameter cost model, schedulers.py:404-442 eviction) EXECUTED — ONE GPT-2 DAG
+    spread over the N GPUs with the reference's node memory split, for MRU_spec, EFT and DFS:
+    tasks completed (reference at N = 1/2/4/8: MRU_spec 99, DFS 81/79/74/66), cross-GPU edges
+    and bytes, parameter bytes re-filled per step, measured ms per step; at N > 1 also
+    ``capped_replica`` (one request per GPU, each capped at 80 % of one DAG's need);
   * ``strong``: strong scaling with real cross-GPU DAG edges — a fixed batch of 8 GPT-2
     micro-batches pipeline-placed over the N GPUs (contiguous layer blocks; every block
     boundary an RCCL p2p send/recv): ms per step, cross-GPU edges and bytes;
   * ``rccl_world`` and ``per_rank_ms`` of the headline run.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W      # N > 1: starts its own N rank processes
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
     python bench.py --model gpt2-medium --gpus 2 --cap-gb 8 --replicas 1          # one DAG across 2 GPUs
     python bench.py --model mixtral-8x7b --gpus 8 --placement expert --replicas 1  # experts over 8 GPUs
@@ -57,6 +59,9 @@ class Ctx:
         if self.world > 1:
             dist.barrier()
 
+    def gather_list(self, v: float):
+        return self.gather(v)[1]
+
     def gather(self, v: float):
         """(max over ranks, per-rank list) of a host float."""
         if self.world == 1:
@@ -84,14 +89,48 @@ def regime_cap_gb(model, regime, batch, seq, cost_model) -> float:
     return round(need * regime, 6)
 
 
+def launch_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N rank processes of this script
+    (fresh children — nothing here has touched the GPU), one per GPU, rendezvous on 127.0.0.1;
+    rank 0 prints the JSON line. Any rank failing ends the job with its exit code."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log(f"[bench] rank {procs.index(p)} exited with {code}; stopping the other ranks")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas, batch, seq, cost_model,
         placement, tp=1, sp=1, fuse=True, use_graph=True, init="auto", refine=False, roctx=False,
-        profile=False, trace_out=None, tag="") -> dict:
+        profile=False, trace_out=None, tag="", node_speeds=None) -> dict:
     """Plan, build the rank's executor, warm up, time ``steps`` steps bracketed by a barrier +
     device synchronize on both sides; the step time is the MAX over ranks."""
     t0 = time.time()
     plan = runtime.plan(model, world=ctx.world, scheduler=scheduler, cap_gb=cap_gb, replicas=replicas, batch=batch,
-                        seq=seq, cost_model=cost_model, fuse=fuse, placement=placement, tp=tp, sp=sp)
+                        seq=seq, cost_model=cost_model, fuse=fuse, placement=placement, tp=tp, sp=sp,
+                        node_speeds=node_speeds)
     log(f"[bench{tag}] rank {ctx.rank}: planned {plan.stats['tasks_completed']}/{plan.stats['tasks_total']} tasks in "
         f"{(time.time() - t0) * 1e3:.1f} ms; {plan.stats}")
     dev_init = init == "device" or (init == "auto" and ctx.gpu and runtime.device_init_ok(plan, ctx.rank))
@@ -118,6 +157,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     elapsed = time.perf_counter() - t_start
     mine = elapsed / steps * 1e3
     ms, per_rank = ctx.gather(mine)
+    launches = ctx.gather_list(ex.launches if ex.launches is not None else -1)
     st = plan.stats
     res = {
         "ms_per_step": round(ms, 5),
@@ -127,7 +167,9 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
         "scheduler": plan.scheduler_name,
         "cross_gpu_edges": st["cross_gpu_edges"],
         "cross_gpu_bytes": st["cross_gpu_bytes"],
-        "kernels_per_rank": st["kernels_per_rank"],
+        "kernel_groups_per_rank": st["kernels_per_rank"],
+        # kernel launches of one step on this rank (counted in the captured hipGraphs; None if eager)
+        "launches_per_rank": [None if v < 0 else int(v) for v in launches],
         "refill_gb_per_step": round(sum(st["refill_gb_per_step_per_rank"]), 6),
         "peer_fill_gb_per_step": round(sum(st.get("peer_fill_gb_per_step_per_rank", [0.0])), 6),
         "param_loads_per_step": sum(1 for i in plan.programs[ctx.rank].instrs if i.op == "load"),
@@ -200,11 +242,14 @@ def main():
     ap.add_argument("--roctx", action="store_true", help="roctx range per DAG instruction (rocprofv3 --marker-trace)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # one rank process per GPU, before any GPU call
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"[bench] --gpus {args.gpus} but the job has WORLD_SIZE={world} ranks; refusing to report n_gpus={world}")
+        sys.exit(2)
     gpu = torch.cuda.is_available()
     device = torch.device(f"cuda:{local}") if gpu else torch.device("cpu")
     if gpu:
@@ -273,7 +318,8 @@ def main():
             "param_evictions_per_step": head["param_evictions_per_step"],
             "scheduler": head["scheduler"],
             "tokens_per_s": round(tokens / (ms / 1e3), 1),
-            "kernels_per_rank": head["kernels_per_rank"],
+            "kernel_groups_per_rank": head["kernel_groups_per_rank"],
+            "launches_per_rank": head["launches_per_rank"],
             "cross_gpu_edges": head["cross_gpu_edges"],
             "cross_gpu_bytes": head["cross_gpu_bytes"],
             "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
@@ -313,22 +359,41 @@ def main():
         threading.Thread(target=watchdog, daemon=True).start()
     if not args.no_extras:
         ew = min(args.warmup, 2)
-        # the reference's 80 % memory regime, executed (one request per GPU, each GPU capped at
-        # 80 % of one request DAG's need under the reference's cost model)
-        cap80 = regime_cap_gb(args.model, 0.8, args.batch, args.seq, "reference")
-        capped = {"memory_regime": 0.8, "cost_model": "reference", "mem_cap_gb_per_gpu": cap80}
+        # the reference's experiment (simulation.py:161-192, 375-376), executed: ONE request DAG
+        # spread over the N GPUs under its 80 % memory regime — the regime's memory split over the
+        # nodes as the reference splits it (60/40 at 2, 35/25/25/15 at 4, equal at 8), its
+        # 0.5 GB-per-parameter cost model; cross-GPU DAG edges are RCCL p2p transfers
+        from distributed_llm_scheduler_amd.eval.execute import regime_node_spec
+        nodes = regime_node_spec(args.model, 0.8, world, args.batch, args.seq)
+        capped = {"memory_regime": 0.8, "cost_model": "reference", "replicas": 1,
+                  "mem_cap_gb_per_gpu": [round(m, 6) for m, _ in nodes], "node_speeds": [round(v, 4) for _, v in nodes]}
         extras["capped"] = capped
+        keys = ("tasks_completed", "tasks_total", "ms_per_step", "refill_gb_per_step", "peer_fill_gb_per_step",
+                "param_loads_per_step", "param_evictions_per_step", "cross_gpu_edges", "cross_gpu_bytes", "issue_mode")
         for sched in ("MRU_spec", "EFT", "DFS"):
             try:
-                r = run(ctx, args.extra_steps, ew, scheduler=sched, cap_gb=cap80, replicas=world,
-                        cost_model="reference", placement="scheduler", tag=f":capped-{sched}", **common)
+                r = run(ctx, args.extra_steps, ew, scheduler=sched, cap_gb=[m for m, _ in nodes], replicas=1,
+                        node_speeds=[v for _, v in nodes], cost_model="reference", placement="scheduler",
+                        tag=f":capped-{sched}", **common)
             except Exception as e:  # noqa: BLE001 — recorded in the JSON line, the headline stands
                 log(f"[bench] capped {sched} failed: {e!r}")
                 capped[sched] = {"error": repr(e)[:300]}
                 continue
-            capped[sched] = {k: r[k] for k in ("tasks_completed", "tasks_total", "ms_per_step", "refill_gb_per_step",
-                                               "peer_fill_gb_per_step", "param_loads_per_step",
-                                               "param_evictions_per_step", "cross_gpu_edges")}
+            capped[sched] = {k: r[k] for k in keys}
+        if world > 1:
+            # one request per GPU, each GPU capped at 80 % of one request DAG's need
+            cap80 = regime_cap_gb(args.model, 0.8, args.batch, args.seq, "reference")
+            cr = {"memory_regime": 0.8, "cost_model": "reference", "replicas": world, "mem_cap_gb_per_gpu": cap80}
+            extras["capped_replica"] = cr
+            for sched in ("MRU_spec", "EFT", "DFS"):
+                try:
+                    r = run(ctx, args.extra_steps, ew, scheduler=sched, cap_gb=cap80, replicas=world,
+                            cost_model="reference", placement="scheduler", tag=f":capped_replica-{sched}", **common)
+                except Exception as e:  # noqa: BLE001
+                    log(f"[bench] capped_replica {sched} failed: {e!r}")
+                    cr[sched] = {"error": repr(e)[:300]}
+                    continue
+                cr[sched] = {k: r[k] for k in keys}
         # strong scaling with real cross-GPU edges: a fixed batch of micro-batches, pipeline
         # placement over the N GPUs (at N = 1: the same batch on one GPU)
         strong = {"micro_batches": args.strong_mb, "placement": f"pipeline over {world} GPU(s)", "scaling": "strong",

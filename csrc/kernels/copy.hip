@@ -37,3 +37,21 @@ void launch_host_pull(const void* src, void* dst, int64_t bytes, int blocks, hip
   int g = (int)(need < blocks ? need : blocks);
   host_pull_kernel<<<g, 256, 0, stream>>>(static_cast<const u32x4*>(src), static_cast<u32x4*>(dst), n16);
 }
+
+namespace {
+
+// One wave that spins for ``ticks`` of the 100 MHz constant clock (wall_clock64): the
+// single-GPU loopback transport (loopback.cpp) puts it in front of every transfer so that a
+// consumer which does not wait for the transfer's event reads the poisoned buffer, not data.
+__global__ __launch_bounds__(64) void delay_kernel(int64_t ticks) {
+  const int64_t t0 = (int64_t)wall_clock64();
+  while ((int64_t)wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+}  // namespace
+
+void launch_delay(double us, hipStream_t stream) {
+  if (us <= 0) return;
+  const int64_t ticks = (int64_t)(us * 100.0);  // wall_clock64 counts at 100 MHz
+  delay_kernel<<<1, 64, 0, stream>>>(ticks < 100000000 ? ticks : 100000000);  // at most 1 s
+}

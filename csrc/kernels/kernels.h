@@ -159,3 +159,4 @@ void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t*
 // dst (HBM) <- src (pinned host memory, device-accessible address); bytes % 16 == 0, both
 // 16-byte aligned; at most `blocks` workgroups of 256 lanes pull over the host link
 void launch_host_pull(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t s);
+void launch_delay(double us, hipStream_t s);  // one wave spinning for ``us`` microseconds (loopback.cpp)

@@ -13,8 +13,11 @@
 // hipMemcpyAsync; hipMemsetAsync; record / wait a runner-owned hipEvent on the compute or the
 // copy stream; post a p2p send / recv through the c10d ProcessGroup of the Python world (RCCL
 // on ROCm, gloo on the CPU test backend — the same ops ``dist.isend`` / ``dist.irecv`` call);
-// wait a posted p2p op (stream-side for RCCL). Every op still outstanding at the end of the
-// step is waited for, as the Python step does.
+// wait a posted p2p op (stream-side for RCCL); open / close a p2p GROUP (the ops posted between
+// are one ncclGroupStart/End through c10d coalescing where the backend supports it, and share
+// one work). Every op still outstanding at the end of the step is waited for, as the Python
+// step does. ``set_loopback`` routes the p2p actions through the single-GPU loopback hub
+// (loopback.h) instead of a ProcessGroup: several ranks in one process, one GPU.
 #include <torch/extension.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/utils/pybind.h>
@@ -24,10 +27,12 @@
 #include <vector>
 
 #include "kernels.h"
+#include "loopback.h"
 
 namespace {
 
-enum Kind : int { GRAPH = 0, PULL, MEMCPY, MEMSET, EV_RECORD, EV_WAIT, SEND, RECV, WORK_WAIT, PYCALL };
+enum Kind : int { GRAPH = 0, PULL, MEMCPY, MEMSET, EV_RECORD, EV_WAIT, SEND, RECV, WORK_WAIT, PYCALL, GROUP_BEGIN,
+                  GROUP_END };
 
 struct Action {
   Kind kind;
@@ -55,6 +60,10 @@ class StepRunner {
     pg_ = pg.is_none() ? c10::intrusive_ptr<c10d::ProcessGroup>() : pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
   }
   void set_copy_stream(uint64_t s) { copy_ = reinterpret_cast<hipStream_t>(s); }
+  void set_loopback(std::shared_ptr<LoopbackHub> hub, int64_t rank) {
+    hub_ = std::move(hub);
+    hub_rank_ = rank;
+  }
 
   void add_graph(uint64_t exec) {
     TORCH_CHECK(exec != 0, "null hipGraphExec");
@@ -111,6 +120,20 @@ class StepRunner {
     a.index = (int)w;
     acts_.push_back(a);
   }
+  // the p2p ops added until group_end form one group (one coalesced RCCL launch)
+  void add_group_begin() {
+    TORCH_CHECK(group_open_ < 0, "nested p2p group");
+    group_open_ = n_works_;
+    acts_.push_back(Action{GROUP_BEGIN});
+  }
+  void add_group_end() {
+    TORCH_CHECK(group_open_ >= 0, "p2p group end without a begin");
+    Action a{GROUP_END};
+    a.index = group_open_;  // first work index of the group; a.value = one past the last
+    a.value = n_works_;
+    group_open_ = -1;
+    acts_.push_back(a);
+  }
   // CPU backend only: a kernel group has no hipGraph there, the runner calls back
   void add_pycall(py::object fn) {
     Action a{PYCALL};
@@ -123,7 +146,11 @@ class StepRunner {
   void run() {
     const bool gpu = any_device_;
     hipStream_t cs = gpu ? c10::hip::getCurrentHIPStream().stream() : nullptr;
+    TORCH_CHECK(group_open_ < 0, "p2p group left open");
     std::vector<c10::intrusive_ptr<c10d::Work>> works(n_works_);
+    std::vector<int64_t> hub_ops(n_works_, -1);
+    bool coalescing = false;
+    const auto dev_type = gpu ? c10::DeviceType::CUDA : c10::DeviceType::CPU;
     for (auto& a : acts_) {
       hipStream_t s = a.stream == 1 && copy_ ? copy_ : cs;
       switch (a.kind) {
@@ -147,13 +174,33 @@ class StepRunner {
           break;
         case SEND:
         case RECV: {
+          if (hub_) {
+            hub_ops[a.value] = hub_->post(a.kind == SEND, a.tensor, hub_rank_, a.index);
+            break;
+          }
           TORCH_CHECK(pg_, "p2p action without a process group");
           std::vector<at::Tensor> ts{a.tensor};
           works[a.value] = a.kind == SEND ? pg_->send(ts, a.index, 0) : pg_->recv(ts, a.index, 0);
           break;
         }
+        case GROUP_BEGIN:
+          coalescing = !hub_ && pg_ && pg_->getBackend(dev_type)->supportsCoalescing();
+          if (coalescing) pg_->startCoalescing(dev_type);
+          break;
+        case GROUP_END:
+          if (coalescing) {  // ONE work for the whole group: every op of it waits on it
+            auto w = pg_->endCoalescing(dev_type);
+            for (int i = a.index; i < a.value; ++i) works[i] = w;
+            coalescing = false;
+          }
+          break;
         case WORK_WAIT:
-          if (works[a.index]) {
+          if (hub_) {
+            if (hub_ops[a.index] >= 0) {
+              hub_->wait(hub_ops[a.index]);  // the current stream waits for the hub's copy
+              hub_ops[a.index] = -1;
+            }
+          } else if (works[a.index]) {
             works[a.index]->wait();  // RCCL: the current stream waits; gloo: blocks
             works[a.index].reset();
           }
@@ -167,6 +214,8 @@ class StepRunner {
     }
     for (auto& w : works)  // the step's p2p ops are complete when it returns (as in Python)
       if (w) w->wait();
+    for (auto h : hub_ops)
+      if (h >= 0) hub_->wait(h);
   }
 
  private:
@@ -194,13 +243,37 @@ class StepRunner {
   std::vector<hipEvent_t> events_;
   hipStream_t copy_ = nullptr;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  std::shared_ptr<LoopbackHub> hub_;
+  int64_t hub_rank_ = 0;
   int n_works_ = 0;
+  int group_open_ = -1;
   bool any_device_ = false;
 };
 
+// kernel nodes of a captured hipGraph (torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()):
+// the launches one replay issues
+int64_t graph_kernel_nodes(uint64_t graph) {
+  size_t n = 0;
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph);
+  C10_HIP_CHECK(hipGraphGetNodes(g, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) C10_HIP_CHECK(hipGraphGetNodes(g, nodes.data(), &n));
+  int64_t k = 0;
+  for (auto nd : nodes) {
+    hipGraphNodeType t;
+    C10_HIP_CHECK(hipGraphNodeGetType(nd, &t));
+    if (t == hipGraphNodeTypeKernel) ++k;
+  }
+  return k;
+}
+
 }  // namespace
 
+void register_loopback(py::module& m);  // loopback.cpp
+
 void register_runner(py::module& m) {
+  register_loopback(m);
+  m.def("graph_kernel_nodes", &graph_kernel_nodes);
   py::class_<StepRunner>(m, "StepRunner")
       .def(py::init<>())
       .def("set_process_group", &StepRunner::set_process_group)
@@ -215,6 +288,9 @@ void register_runner(py::module& m) {
       .def("add_recv", &StepRunner::add_recv)
       .def("add_work_wait", &StepRunner::add_work_wait)
       .def("add_pycall", &StepRunner::add_pycall)
+      .def("add_group_begin", &StepRunner::add_group_begin)
+      .def("add_group_end", &StepRunner::add_group_end)
+      .def("set_loopback", &StepRunner::set_loopback)
       .def("size", &StepRunner::size)
       .def("run", &StepRunner::run, py::call_guard<py::gil_scoped_release>());
 }

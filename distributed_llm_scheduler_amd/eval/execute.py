@@ -113,6 +113,17 @@ def run_executed(model: str = "gpt2", schedulers: Optional[Sequence[str]] = None
     return rows
 
 
+def regime_node_spec(model: str, regime: float, world: int, batch: int = 1, seq: int = 512, seed: int = 0):
+    """[(memory GB, speed)] per GPU for ONE request DAG of ``model`` spread over ``world`` nodes:
+    the reference's memory regime over its total-need formula (simulation.py:194-214, its
+    0.5 GB-per-parameter cost model) split as the reference splits it (simulation.py:161-192:
+    60/40 at 2 nodes, 35/25/25/15 at 4, equal shares with seeded speeds otherwise)."""
+    tasks, _, _ = registry.build(model, batch=batch, seq=seq, cost_model="reference")
+    ev = ImprovedSchedulerEvaluator({}, seed=seed, verbose=False)
+    total = ev.calculate_total_memory_needed(tasks)
+    return _node_spec(ev, "reference" if world > 1 else "equal", total, regime, world, seed)
+
+
 def _node_spec(ev, mode, total, regime, world, seed):
     """[(memory GB, speed)] per device."""
     if mode == "equal":

@@ -116,14 +116,12 @@ def build_llama_dag(cfg: "ModelConfig | str" = "llama3-8b", batch: int = 1, seq:
                            {"expert": e, "n_experts": E, "top_k": K, "ffn": F}, shape),
                     6.0 * rows * H * F, extra=M * K * (H + 3 * F) * dtype_bytes)
                 experts.append(f"layer_{i}_expert_{e}")
-            # a cross-GPU edge into or out of an expert moves only its routed rows (M*K/E
-            # expected): the executor ships each expert GPU exactly its experts' token rows and
-            # returns their compact outputs (program.py routed transfers)
-            rows_b = int(round(M * K / E)) * H * dtype_bytes
-            byid = {t.id: t for t in tasks[-(E + 2):]}
-            byid[tid(f"layer_{i}_ffn_norm")].edge_bytes = rows_b
-            for x in experts:
-                byid[tid(x)].edge_bytes = rows_b
+            # a cross-GPU edge into or out of an expert moves the whole [M, H] buffer (the normed
+            # hidden state in, the expert's compact output rows back): fixed-size transfers that
+            # need no routing on the host, so an expert-parallel step replays like any other
+            # (each expert GPU routes locally from the router logits, which travel too). Per
+            # expert GPU this is never more than the worst case of the routed rows
+            # (M x min(top-k, experts there) rows).
             # combine = residual + gate-weighted gather of the experts' compact outputs; the
             # router edge carries the (tiny) logits so routing is known wherever this runs
             add(f"layer_{i}_output", 0.01, experts + [f"layer_{i}_router", f"layer_{i}_attn_residual"], [],

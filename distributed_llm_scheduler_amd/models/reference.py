@@ -35,8 +35,9 @@ def _attn(q, k, v, nh, nkv, D, causal=True):
 
 
 @torch.no_grad()
-def gpt2_forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor) -> torch.Tensor:
-    """tokens [B, S] -> logits [B, S, V] (fp32)."""
+def gpt2_forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor, hidden: list = None) -> torch.Tensor:
+    """tokens [B, S] -> logits [B, S, V] (fp32). ``hidden`` (if a list) receives the residual
+    stream after every block."""
     B, S = tokens.shape
     H, nh = cfg.n_embd, cfg.n_head
     x = _w(store, "wte")[tokens.long()] + _w(store, "wpe")[:S][None]
@@ -49,6 +50,8 @@ def gpt2_forward(cfg: ModelConfig, store: ParamStore, tokens: torch.Tensor) -> t
         h = F.layer_norm(x, (H,), _w(store, p + "ln_2.weight"), _w(store, p + "ln_2.bias"), cfg.norm_eps)
         h = F.gelu(h @ _w(store, p + "mlp.c_fc.weight").t() + _w(store, p + "mlp.c_fc.bias"), approximate="tanh")
         x = x + h @ _w(store, p + "mlp.c_proj.weight").t() + _w(store, p + "mlp.c_proj.bias")
+        if hidden is not None:
+            hidden.append(x.clone())
     x = F.layer_norm(x, (H,), _w(store, "ln_f.weight"), _w(store, "ln_f.bias"), cfg.norm_eps)
     return x @ _w(store, "wte").t()
 

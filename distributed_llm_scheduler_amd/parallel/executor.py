@@ -11,11 +11,14 @@ One process per GPU (``torch.distributed`` world, backend ``nccl`` = RCCL on ROC
   enqueued (hipEvent fork), and the compute stream waits for it only at the load's own
   position — parameter refills overlap the kernels in between (``DLS_PREFETCH=1``; default
   in order on the compute stream). A refill is ONE DMA of the group's pinned host image;
-* ``recv``/``send`` are RCCL point-to-point ops (``dist.irecv``/``dist.isend``): RCCL runs
-  them on its own stream ordered after the producing kernels, and the consumer waits
-  stream-side (``work.wait()``), so transfers overlap the next independent kernels; a
-  sent buffer is only overwritten (by a kernel or by a recv from another peer) after its
-  send completes (waits planned statically, ``Instr.wait_sends``);
+* ``recv``/``send`` are RCCL point-to-point ops (parallel/comm.py): the sends and receives a
+  rank posts at one program point go out as ONE group (``batch_isend_irecv``, one
+  ncclGroupStart/End); RCCL runs them on its own stream ordered after the producing kernels,
+  and the consumer waits stream-side (``work.wait()``), so transfers overlap the next
+  independent kernels; a sent buffer is only overwritten (by a kernel or by a recv from
+  another peer) after its send completes (waits planned statically, ``Instr.wait_sends``).
+  The same primitives also run over the single-GPU loopback hub (several ranks in one
+  process, parallel/loopback.py), which checks that stream ordering on one device;
 * ``run`` launches the (fused) kernel group through :mod:`ops` — HIP kernels on GPU;
 * programs without p2p ops are captured once into a hipGraph (``torch.cuda.CUDAGraph``)
   and replayed, removing per-kernel host launch cost from the step.
@@ -33,12 +36,13 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
-import torch.distributed as dist
 
 from .. import ops
 from ..core.task import Task
+from ..ops import tuning as _tuning
 from ..models.params import ParamStore, group_layout
 from ..utils.tracing import Roctx
+from .comm import make_comm
 from .program import Program
 
 
@@ -56,21 +60,6 @@ class StepStats:
     bytes_peer: int = 0
     timeline: List[Tuple[str, float, float]] = field(default_factory=list)  # (group, start_ms, end_ms)
     events: List[Tuple[str, str, float, float]] = field(default_factory=list)  # (name, category, start, end)
-
-
-class _Works:
-    """Several RCCL p2p works (the routed rows of one expert-parallel edge) waited as one; keeps
-    the sent / received views alive until then."""
-
-    def __init__(self, works, keep=()):
-        self.works = list(works)
-        self.keep = list(keep)
-
-    def wait(self):
-        for w in self.works:
-            w.wait()
-        self.works = []
-        self.keep = []
 
 
 class _REvent:
@@ -167,14 +156,19 @@ REFILL_BLOCKS = int(os.environ.get("DLS_REFILL_BLOCKS", "64"))
 class DAGExecutor:
     def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
                  model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True,
-                 trace: bool = False, debug: bool = False):
+                 trace: bool = False, debug: bool = False, model_name: Optional[str] = None):
         self.tasks = {t.id: t for t in tasks}
+        # the model whose per-model GEMM choices (ops/gemm_tuning.json model_overrides) this
+        # executor's launches use: set around each of its steps, captures and refinements, so
+        # executors of different models in one process do not change each other's choices
+        self.model_name = model_name if model_name is not None else getattr(model_cfg, "name", None)
         self.prog = program
         self.store = store
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
         self.cfg = model_cfg
         self.pg = pg
+        self.comm = make_comm(pg)  # p2p transport: torch.distributed (RCCL / gloo) or the loopback hub
         # whole-step hipGraph for comm-free programs without copy-stream refills; the others
         # replay hipGraph SEGMENTS (runs of kernel groups) between their eager RCCL / copy steps
         self.use_graph = use_graph and self.gpu
@@ -188,14 +182,17 @@ class DAGExecutor:
         self._params: Dict[str, Dict[str, torch.Tensor]] = {}  # pid -> {tensor name -> view}
         self._wflat: Dict[str, torch.Tensor] = {}               # tensor name -> resident view
         self._derived_cache: Dict[tuple, tuple] = {}             # (weight, ptr) -> (colsum, bias') for folded norms
-        # weights read by more than one task (GPT-2's tied wte: embedding gather + LM head) are
-        # never transformed in place: their folded form lives in a private buffer
+        # weights read by more than one KIND of op (GPT-2's tied wte: embedding gather + LM head)
+        # are never transformed in place: their folded form lives in a private buffer. Tasks of
+        # one kind reading one weight (request replicas, sequence chunks) apply the same
+        # transform and share it in place.
         self._side: Dict[str, torch.Tensor] = {}                 # weight -> private derived copy
-        self._w_users: Dict[str, int] = {}
+        kinds: Dict[str, set] = {}
         for t in tasks:
             if t.op is not None:
                 for v in set(x for x in t.op.weights.values() if isinstance(x, str)):
-                    self._w_users[v] = self._w_users.get(v, 0) + 1
+                    kinds.setdefault(v, set()).add(t.op.kind)
+        self._w_users: Dict[str, int] = {v: len(k) for v, k in kinds.items()}
         # GPU, host-image refills: a transformed weight's bytes are written back into a private
         # copy of its group's pinned image, so every later refill restores the TRANSFORMED
         # weight and its (colsum, bias') stay valid wherever the group lands (no re-derivation
@@ -215,20 +212,17 @@ class DAGExecutor:
         self._ext_stats: Dict[str, torch.Tensor] = {}   # the same buffers, by the tensor a norm reads
         self._stats_slab: Optional[torch.Tensor] = None
         self._moe_ptrs: Dict[tuple, torch.Tensor] = {}
-        # expert-parallel programs route eagerly (outside captured segments) while the expert
-        # kernels replay from a hipGraph: the routing then lives in fixed buffers per router
-        self._route_persist = any(i.route is not None for i in program.instrs)
-        self._route_bufs: Dict[str, tuple] = {}
         self._pending_sends: Dict[int, object] = {}  # send instruction index -> RCCL work
         self._param_recv: Dict[str, object] = {}     # group -> RCCL work of its peer fill
         self._started = False
         self._steps_done = 0
+        self.launches: Optional[int] = None  # kernel launches of one captured step (hipGraph kernel nodes)
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._setup()
         if autotune and self.gpu:
-            from ..ops import tuning
-            tuning.ensure_tuned(self.gemm_shapes(), self.device)
+            _tuning.set_model(self.model_name)
+            _tuning.ensure_tuned(self.gemm_shapes(), self.device)
 
     # ------------------------------------------------------------------ setup
     def _setup(self) -> None:
@@ -626,9 +620,10 @@ class DAGExecutor:
                 self._unmap(q)
 
     def _resident(self, pid: str) -> bool:
-        """Is group ``pid`` mapped AND do its arena bytes currently hold it?"""
+        """Is group ``pid`` mapped AND do its arena bytes currently hold it? (Not while a peer
+        fill of it is still in flight: its bytes are being written by the receive.)"""
         r = self._region.get(pid)
-        return r is not None and (r[0], r[1], pid) in self._valid
+        return r is not None and (r[0], r[1], pid) in self._valid and pid not in self._param_recv
 
     # --- device actions: executed, or recorded for the native step runner (self._rec) ---
     def _new_event(self, timing: bool = False, carry_load: Optional[int] = None):
@@ -653,12 +648,24 @@ class DAGExecutor:
     def _isend(self, buf, peer):
         if self._rec is not None:
             return _RWork(self._rec.r, self._rec.r.add_send(buf, peer))
-        return dist.isend(buf, dst=peer, group=self.pg)
+        return self.comm.isend(buf, peer)
 
     def _irecv(self, buf, peer):
         if self._rec is not None:
             return _RWork(self._rec.r, self._rec.r.add_recv(buf, peer))
-        return dist.irecv(buf, src=peer, group=self.pg)
+        return self.comm.irecv(buf, peer)
+
+    def _p2p_group(self, ops_):
+        """Post [(is_send, buffer, peer)] as ONE group (one ncclGroupStart/End); a work per op."""
+        if self._rec is not None:
+            r = self._rec.r
+            if len(ops_) > 1:
+                r.add_group_begin()
+            ws = [_RWork(r, r.add_send(b, p) if snd else r.add_recv(b, p)) for snd, b, p in ops_]
+            if len(ops_) > 1:
+                r.add_group_end()
+            return ws
+        return self.comm.batch(ops_)
 
     def _fill(self, off, total, layout, views, pid, stats: StepStats, dma: bool = False) -> bool:
         """Copy the group into its arena region unless the region already holds it. ``dma``:
@@ -942,47 +949,8 @@ class DAGExecutor:
             else:
                 idx, gate = ops.moe_router(logits, top_k)
                 r = (idx, gate) + tuple(ops.moe_align(idx, E))
-            if self._route_persist:
-                bufs = self._route_bufs.get(r_name)
-                if bufs is None or any(a.shape != b.shape for a, b in zip(bufs, r)):
-                    bufs = tuple(x.clone() for x in r)
-                    self._route_bufs[r_name] = bufs
-                else:
-                    for a, b in zip(bufs, r):
-                        a.copy_(b)
-                r = bufs
             self._moe_memo[key] = r
         return r
-
-    def _route_host(self, r_name: str, E: int, top_k: int) -> List[int]:
-        """Per-expert row offsets of router ``r_name``'s routing on the host (ONE device->host
-        sync per MoE layer and rank, at the first routed transfer that needs the counts)."""
-        key = ("host", r_name)
-        h = self._moe_memo.get(key)
-        if h is None:
-            h = [int(v) for v in self._moe_route(r_name, E, top_k)[4].tolist()]
-            self._moe_memo[key] = h
-        return h
-
-    def _routed_bufs(self, ins, recv: bool) -> List[torch.Tensor]:
-        """The views an expert-parallel edge moves (Instr.route): expert by expert, only the
-        routed rows — of the permuted hidden state (``rows``; on the receiver, straight into the
-        permuted-row buffer the local experts read) or of an expert's compact output (``out``)."""
-        kind, R, exps, E, K = ins.route
-        off = self._route_host(R, E, K)
-        if kind == "rows":
-            key = ("perm", ins.task, R)
-            if recv:
-                t = self.tasks[ins.task]
-                H = t.op.out_shape[-1]
-                M = math.prod(t.op.out_shape[:-1])
-                xp = self._scratch(f"moe_rows:{R}", (M * K, H))
-                self._moe_memo[key] = xp
-            else:
-                xp = self._moe_permuted(ins.task, R, E, K)
-            return [xp[off[e]:off[e + 1]] for e in exps if off[e + 1] > off[e]]
-        c = off[exps[0] + 1] - off[exps[0]]
-        return [self._flat(self._views[ins.task])[:c]] if c else []
 
     def _moe_permuted(self, h_name: str, r_name: str, E: int, top_k: int):
         key = ("perm", h_name, r_name)
@@ -990,10 +958,6 @@ class DAGExecutor:
         if xp is None:
             src = self._moe_route(r_name, E, top_k)[2]
             xp = ops.moe_permute(self._flat(self._x(h_name)), src)
-            if self._route_persist:  # a fixed buffer: captured expert kernels read it every step
-                buf = self._scratch(f"moe_perm:{h_name}", tuple(xp.shape))
-                buf.copy_(xp)
-                xp = buf
             self._moe_memo[key] = xp
         return xp
 
@@ -1164,7 +1128,7 @@ class DAGExecutor:
 
     def _step_body(self, stats: StepStats, events: Optional[list] = None) -> None:
         """Issue the program. ``events`` (profiling) collects (name, category, t0, t1) tokens."""
-        pg = self.pg
+        _tuning.set_model(self.model_name)
         tr = self.trace
         self._pending_sends = {}
         self._reset_step_state()
@@ -1242,36 +1206,18 @@ class DAGExecutor:
             elif ins.op == "evict":
                 self._await_fill(ins.param)
                 self._evict(ins.param)
-            elif ins.op == "recv":
-                self._wait_sends(ins)  # the recv buffer may still be read by a send to another peer
-                t0 = self._mark() if events is not None else None
-                if ins.route is not None:  # expert-parallel edge: only the routed rows
-                    if self._rec is not None:
-                        raise RuntimeError("step runner: routed transfers need the routing on the host")
-                    rw = recv_work.pop(ins.route[1], None)
-                    if rw is not None:  # the router's logits first: both ends route from them
-                        rw[0].wait()
-                    bufs = self._routed_bufs(ins, recv=True)
-                    recv_work[ins.task] = (_Works([dist.irecv(b, src=ins.peer, group=pg) for b in bufs], bufs), t0)
-                    stats.bytes_recv += sum(b.numel() * b.element_size() for b in bufs)
-                else:
-                    buf = self._views[ins.task]
-                    recv_work[ins.task] = (self._irecv(buf, ins.peer), t0)
-                    stats.bytes_recv += buf.numel() * buf.element_size()
-                stats.recvs += 1
-            elif ins.op == "send":
-                t0 = self._mark() if events is not None else None
-                if ins.route is not None:
-                    bufs = self._routed_bufs(ins, recv=False)
-                    w = _Works([dist.isend(b, dst=ins.peer, group=pg) for b in bufs], bufs)
-                else:
-                    bufs = [self._views[ins.task]]
-                    w = self._isend(bufs[0], ins.peer)
-                self._pending_sends[i] = w
-                if events is not None:
-                    events.append((f"{ins.task}->gpu{ins.peer}", "send", t0, self._mark()))
-                stats.sends += 1
-                stats.bytes_sent += sum(b.numel() * b.element_size() for b in bufs)
+            elif ins.op in ("send", "recv"):
+                # every send / recv posted at this program point: ONE p2p group
+                # (a recv whose buffer is still being sent by a send of the same group starts a
+                # new group: that send must complete before the recv is posted)
+                j = i
+                while j + 1 < n_ins and self.prog.instrs[j + 1].op in ("send", "recv") \
+                        and not any(i <= w <= j for w in self.prog.instrs[j + 1].wait_sends) \
+                        and not (hoist and (j in hoist or j in self._carry_at)) and not tr:
+                    j += 1
+                self._post_p2p(i, j + 1, recv_work, stats, events)
+                i = j
+                ins = self.prog.instrs[i]
             elif ins.op == "run":
                 self._pre_run(ins, recv_work, events)
                 if self._rec is not None:  # CPU runner: the group runs as a callback, with the
@@ -1307,6 +1253,32 @@ class DAGExecutor:
             w.wait()
         self._param_recv = {}
         self._steps_done += 1
+
+    def _post_p2p(self, a: int, b: int, recv_work, stats: StepStats, events) -> None:
+        """Instructions [a, b) (sends and recvs) posted as one group."""
+        ops_, idx = [], []
+        for k in range(a, b):
+            ins = self.prog.instrs[k]
+            if ins.op == "recv":
+                self._wait_sends(ins)  # the recv buffer may still be read by a send to another peer
+            buf = self._views[ins.task]
+            ops_.append((ins.op == "send", buf, ins.peer))
+            idx.append(k)
+        t0 = self._mark() if events is not None else None
+        works = self._p2p_group(ops_)
+        for k, (snd, buf, peer), w in zip(idx, ops_, works):
+            ins = self.prog.instrs[k]
+            nbytes = buf.numel() * buf.element_size()
+            if snd:
+                self._pending_sends[k] = w
+                if events is not None:
+                    events.append((f"{ins.task}->gpu{peer}", "send", t0, self._mark()))
+                stats.sends += 1
+                stats.bytes_sent += nbytes
+            else:
+                recv_work[ins.task] = (w, t0)
+                stats.recvs += 1
+                stats.bytes_recv += nbytes
 
     def _run_snapshot(self, i, ins, snap) -> None:
         self._params, self._wflat, self._region, self._valid = (dict(snap[0]), dict(snap[1]), dict(snap[2]),
@@ -1474,6 +1446,7 @@ class DAGExecutor:
         program without copy-stream refills, else its kernel-group segments (capture_segments)."""
         if not self.use_graph:
             return False
+        self._drop_runner()  # its hipGraphExec handles belong to the graphs a re-capture replaces
         if self._copy_stream is not None or self.prog.has_comm:
             return self.capture_segments()
         torch.cuda.synchronize(self.device)
@@ -1483,12 +1456,19 @@ class DAGExecutor:
             self._step_body(StepStats())  # warm the residency state on the capture stream
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(g):
             self._step_body(StepStats())
+        self.launches = ops.ext().graph_kernel_nodes(g.raw_cuda_graph())
+        g.instantiate()
         torch.cuda.synchronize(self.device)
         self._graph = g
         return True
+
+    def _drop_runner(self) -> None:
+        self._runner = None
+        self._runner_stats = None
+        self.issue_mode = None
 
     def _plan_segments(self) -> List[Tuple[int, int]]:
         """[start, end) ranges of consecutive ``run`` instructions that replay as one hipGraph.
@@ -1537,7 +1517,7 @@ class DAGExecutor:
         irecv / parameter send posted earlier in this step host-blocking — two ranks exchanging
         in opposite directions could then wait on each other at capture). The capture runs on
         a side stream ordered after the compute stream; the compute stream waits for it."""
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         cur = torch.cuda.current_stream(self.device)
         if self._cap_stream is None:
             self._cap_stream = torch.cuda.Stream(self.device)
@@ -1551,18 +1531,17 @@ class DAGExecutor:
                     self._issue_run(k, self.prog.instrs[k], stats, None)
             finally:
                 g.capture_end()
+            self.launches = (self.launches or 0) + ops.ext().graph_kernel_nodes(g.raw_cuda_graph())
+            g.instantiate()
         cur.wait_stream(cs)
         return g
 
     def _runner_ok(self) -> bool:
         """Can this rank's steady-state step be recorded for the native runner? Every run is in
-        a captured segment, no transfer needs the routing on the host (expert-parallel routed
-        rows), and every steady-state refill copies a host image."""
+        a captured segment and every steady-state refill copies a host image."""
         if not RUNNER or self.trace or self.debug:
             return False
         if not ((self.gpu and self._segments) or (not self.gpu and RUNNER_CPU)):
-            return False
-        if any(i.route is not None for i in self.prog.instrs):
             return False
         if self._refills() and self.gpu:
             for i in self.prog.instrs:
@@ -1584,7 +1563,9 @@ class DAGExecutor:
         r = ops.ext().StepRunner()
         if self._copy_stream is not None:
             r.set_copy_stream(self._copy_stream.cuda_stream)
-        if self.pg is not None:
+        if self.comm is not None and self.comm.kind == "loopback":
+            r.set_loopback(self.comm.hub, self.comm.rank)
+        elif self.pg is not None:
             r.set_process_group(self.pg)
         self._rec = _Recorder(r)
         stats = StepStats()
@@ -1613,8 +1594,12 @@ class DAGExecutor:
         pool, captured in program order during a steady-state step (the host bookkeeping of
         that step runs as usual; its segment kernels are recorded, not run)."""
         self._segments = {}
+        self.launches = None
         segs = [(a, b) for a, b in self._plan_segments()]
         if not segs:
+            if self.prog.has_comm:  # stay in p2p step with the ranks that capture (two steps below)
+                self.step()
+                self.step()
             return False
         torch.cuda.synchronize(self.device)
         self._capture_plan = {a: b for a, b in segs}
@@ -1622,7 +1607,13 @@ class DAGExecutor:
         self._step_body(StepStats())  # segments captured in order as the step reaches them
         self._capture_plan = None
         torch.cuda.synchronize(self.device)
-        if self._segments and self.build_runner() and RUNNER_MODE == "auto" and not self.prog.has_comm:
+        built = bool(self._segments) and self.build_runner()
+        if not built and self.prog.has_comm:
+            # build_runner executes the step it recorded; a rank that could not record one runs
+            # a step from the Python loop instead, so every rank of a p2p program has executed
+            # the same number of steps (their transfers pair step by step) whichever path it takes
+            self.step()
+        if built and RUNNER_MODE == "auto" and not self.prog.has_comm:
             self._pick_issue_mode()
         return bool(self._segments)
 

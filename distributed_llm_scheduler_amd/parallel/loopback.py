@@ -1,0 +1,137 @@
+"""Single-GPU multi-rank harness: a ``world``-rank job in ONE process on ONE device.
+
+Every rank is a real :class:`DAGExecutor` with its own program, arenas, compute stream and host
+thread; their DAG edges go through the loopback hub (``csrc/kernels/loopback.cpp``), which gives
+the p2p primitives RCCL's semantics — posts ordered after the rank's enqueued kernels, the copy
+on a separate stream, ``wait()`` making the consumer's stream wait — and adds two checks:
+
+* every transfer runs behind a spinning delay kernel (``delay_us``), so the copy lands well after
+  the consumer's next kernels would have started had they not been ordered after it;
+* every receive buffer is filled with 0xFF (bf16 NaN) when the receive is posted (``poison``),
+  so a consumer that reads it early computes NaN, and a producer that overwrites a buffer before
+  its send completed sends the wrong bytes.
+
+The same executor paths as a multi-process RCCL job run here — the eager Python issue loop,
+segment hipGraphs around the p2p points, the native step runner's SEND / RECV / WORK_WAIT and
+group actions, peer parameter fills — so a one-GPU box checks the multi-GPU path with real
+device asynchrony (a gloo job cannot: its ``wait()`` blocks the host). CPU tensors work too
+(copies at match time), for the CPU test suite.
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional
+
+import torch
+
+from .comm import loopback_groups
+
+
+@dataclass
+class LoopbackRun:
+    executors: list
+    stats: list                    # each rank's StepStats of its last step
+    hub: object
+    issue_modes: List[Optional[str]] = field(default_factory=list)
+    step_ms: List[float] = field(default_factory=list)
+
+
+def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = True, delay_us: float = 20.0,
+                 poison: bool = True, store=None, timeout_s: float = 120.0,
+                 before_steps: Optional[Callable] = None, cpu_runner: bool = False,
+                 sync_debug: bool = False) -> LoopbackRun:
+    """Build one executor per rank of ``plan`` on ``device``, then drive every rank from its own
+    thread: ``warmup`` eager steps, capture (segment hipGraphs + native runner for programs with
+    p2p), ``steps`` timed steps. ``before_steps(executors)`` may patch the executors first
+    (negative controls). ``cpu_runner``: on the CPU backend, replay the steps from the native
+    step runner (kernel groups as callbacks) instead of the Python issue loop. ``sync_debug``:
+    the timed steps run under torch's sync debug mode "error" (any device->host synchronising
+    call inside a step raises)."""
+    from . import executor as exm
+    from . import runtime
+
+    device = torch.device(device)
+    gpu = device.type == "cuda"
+    world = plan.world
+    groups = loopback_groups(world, delay_us=delay_us if gpu else 0.0, poison=poison, timeout_s=timeout_s)
+    store = store or runtime.make_store(plan)
+    # executors are built on this thread (autotuning and weight transforms are not thread-safe)
+    streams = [torch.cuda.Stream(device) for _ in range(world)] if gpu else [None] * world
+    exs = []
+    for r in range(world):
+        if gpu:
+            with torch.cuda.stream(streams[r]):
+                exs.append(runtime.make_executor(plan, r, device, store, pg=groups[r], use_graph=capture))
+        else:
+            exs.append(runtime.make_executor(plan, r, device, store, pg=groups[r], use_graph=False))
+    if gpu:
+        torch.cuda.synchronize(device)
+    if before_steps is not None:
+        before_steps(exs)
+    stats = [None] * world
+    ms = [0.0] * world
+    errors = []
+    start = threading.Barrier(world)
+
+    def drive(r):
+        import time
+
+        try:
+            if gpu:
+                torch.cuda.set_device(device)
+            ctx = torch.cuda.stream(streams[r]) if gpu else _Null()
+            with ctx:
+                ex = exs[r]
+                for _ in range(warmup):
+                    ex.step()
+                if capture and gpu:
+                    ex.capture()
+                elif cpu_runner and not gpu and not ex.build_runner():
+                    raise RuntimeError("CPU step runner refused the program")
+                start.wait()
+                if sync_debug and gpu and r == 0:
+                    torch.cuda.set_sync_debug_mode("error")
+                start.wait()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    stats[r] = ex.step()
+                start.wait()
+                if sync_debug and gpu and r == 0:
+                    torch.cuda.set_sync_debug_mode(0)
+                if gpu:
+                    streams[r].synchronize()
+                ms[r] = (time.perf_counter() - t0) / max(steps, 1) * 1e3
+        except BaseException as e:  # noqa: BLE001 — reported below, with the rank
+            errors.append((r, e))
+            start.abort()
+            if sync_debug and gpu:
+                torch.cuda.set_sync_debug_mode(0)
+
+    threads = [threading.Thread(target=drive, args=(r,), daemon=True) for r in range(world)]
+    saved = exm.RUNNER_CPU
+    exm.RUNNER_CPU = cpu_runner or saved
+    try:
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout_s * 2)
+    finally:
+        exm.RUNNER_CPU = saved
+    if any(t.is_alive() for t in threads):
+        raise RuntimeError("loopback harness: a rank thread did not finish (hung transfer?)")
+    if gpu:
+        torch.cuda.synchronize(device)
+    real = [(r, e) for r, e in errors if not isinstance(e, threading.BrokenBarrierError)]
+    if real or errors:
+        r, e = (real or errors)[0]
+        raise RuntimeError(f"loopback harness: rank {r} failed: {e!r}") from e
+    return LoopbackRun(exs, stats, groups[0].hub, [ex.issue_mode for ex in exs], ms)
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -54,12 +54,6 @@ class Instr:
     # run/recv: indices of earlier ``send`` instructions whose buffer this instruction's
     # output region overlaps — they must complete before it writes (see _plan_send_waits)
     wait_sends: Tuple[int, ...] = ()
-    # send/recv of an MoE expert-parallel edge that moves only routed token rows
-    # (_routed_edges): ("rows", router, experts, E, K) — the rows of ``task`` (the normed
-    # hidden state) routed to ``experts``, in expert order, issued right after the router's
-    # logits (both ends know the routing from them); ("out", router, (e,), E, K) — expert e's
-    # compact output rows only
-    route: Optional[tuple] = None
 
 
 @dataclass
@@ -147,43 +141,6 @@ def _fusion(tmap: Dict[str, Task], placement: Dict[str, int], order: Sequence[st
     return fused_into, group_of
 
 
-ROUTED_EP = os.environ.get("DLS_EP_ROUTED", "1") != "0"
-
-
-def _routed_edges(tmap, placement, order, consumers):
-    """Expert-parallel edges that carry routed rows instead of whole [M, H] buffers:
-    ``rows`` X -> {dst rank: (router, experts)} for a hidden state X whose consumers on dst are
-    all MoE experts routed by one router placed with X; ``out`` expert Y -> (router, e) for an
-    expert whose only remote consumer is the combine on the router's rank."""
-    rows: Dict[str, Dict[int, tuple]] = {}
-    out: Dict[str, tuple] = {}
-    if not ROUTED_EP:
-        return rows, out
-    for x in order:
-        cons = consumers.get(x, [])
-        for dst in sorted({placement[c] for c in cons if placement[c] != placement[x]}):
-            cs = [tmap[c] for c in cons if placement[c] == dst]
-            if not all(c.op is not None and c.op.kind == "moe_expert" and c.op.inputs[0] == x for c in cs):
-                continue
-            routers = {c.op.inputs[1] for c in cs}
-            if len(routers) != 1:
-                continue
-            r = routers.pop()
-            if placement.get(r) != placement[x]:
-                continue
-            a = cs[0].op.attrs
-            rows.setdefault(x, {})[dst] = (r, tuple(sorted(c.op.attrs["expert"] for c in cs)), a["n_experts"],
-                                           a["top_k"])
-        t = tmap[x]
-        if t.op is not None and t.op.kind == "moe_expert":
-            r = t.op.inputs[1]
-            far = [c for c in cons if placement[c] != placement[x]]
-            if far and all(tmap[c].op.kind == "moe_combine" and placement[c] == placement.get(r) for c in far):
-                a = t.op.attrs
-                out[x] = (r, a["expert"], a["n_experts"], a["top_k"])
-    return rows, out
-
-
 def _consumers(tmap, placement, order):
     consumers: Dict[str, List[str]] = defaultdict(list)
     for tid in order:
@@ -221,10 +178,6 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
     order = [t for t in order if t in placement]
     consumers = _consumers(tmap, placement, order)
     fused_into, group_of = _fusion(tmap, placement, order, consumers, pos, fuse)
-    routed_rows, routed_out = _routed_edges(tmap, placement, order, consumers)
-    rows_after: Dict[str, List[str]] = defaultdict(list)  # router -> hidden states shipped routed after it
-    for x, by_dst in routed_rows.items():
-        rows_after[next(iter(by_dst.values()))[0]].append(x)
 
     # --- parameter plan per node from the scheduler trace (load-on-first-use otherwise)
     load_before: Dict[str, List[Tuple[str, str]]] = defaultdict(list)  # task -> [(op, pid)] on its rank
@@ -369,30 +322,14 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                     if pid in where:
                         evict(pid)
                 dsts = sorted({placement[c] for c in consumers.get(grp[-1], []) if placement[c] != rank})
-                ro = routed_out.get(grp[-1])
                 for dst in dsts:
-                    if dst in routed_rows.get(grp[-1], {}):
-                        continue  # shipped as routed rows after its router (below)
-                    route = ("out", ro[0], (ro[1],), ro[2], ro[3]) if ro is not None else None
-                    ins.append(Instr("send", task=grp[-1], peer=dst, route=route))
-                for member in grp:  # hidden states routed by this router: each expert GPU's rows
-                    for x in rows_after.get(member, ()):
-                        for dst, (rr, exps, E, K) in sorted(routed_rows[x].items()):
-                            ins.append(Instr("send", task=x, peer=dst, route=("rows", rr, exps, E, K)))
+                    ins.append(Instr("send", task=grp[-1], peer=dst))
             else:
                 if tid in fused_into:
                     continue
-                if any(placement[c] == rank for c in consumers.get(tid, [])) and tid not in received \
-                        and rank not in routed_rows.get(tid, {}):
-                    ro = routed_out.get(tid)
-                    route = ("out", ro[0], (ro[1],), ro[2], ro[3]) if ro is not None else None
-                    ins.append(Instr("recv", task=tid, peer=r, route=route))
+                if any(placement[c] == rank for c in consumers.get(tid, [])) and tid not in received:
+                    ins.append(Instr("recv", task=tid, peer=r))
                     received.add(tid)
-                for x in rows_after.get(tid, ()):  # this router's routed hidden-state rows
-                    if rank in routed_rows[x] and x not in received:
-                        rr, exps, E, K = routed_rows[x][rank]
-                        ins.append(Instr("recv", task=x, peer=placement[x], route=("rows", rr, exps, E, K)))
-                        received.add(x)
         for x in ins[n0:]:
             x.gpos = len(order) - 1
         n0 = len(ins)

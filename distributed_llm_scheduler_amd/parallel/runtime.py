@@ -284,15 +284,14 @@ def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None
                   trace: bool = False, debug: bool = False):
     """``debug=True``: validate every rank's program first (parallel/validate.py) and run the
     executor with arena canaries and output finiteness checks."""
-    from ..ops import tuning
     from .executor import DAGExecutor
 
-    tuning.set_model(p.model)  # per-model GEMM choices (tuning.lookup) for this executor's steps
     if debug:
         from .validate import check_plan
 
         errs = check_plan(p)
         if errs:
             raise RuntimeError("invalid plan:\n  " + "\n  ".join(errs[:20]))
+    # per-model GEMM choices by the canonical preset name (aliases such as "mixtral" resolve to it)
     return DAGExecutor(p.tasks, p.programs[rank], store or make_store(p), device, model_cfg=p.cfg,
-                       use_graph=use_graph, pg=pg, trace=trace, debug=debug)
+                       use_graph=use_graph, pg=pg, trace=trace, debug=debug, model_name=p.cfg.name)

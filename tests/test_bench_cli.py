@@ -91,21 +91,70 @@ def test_bench_baseline_multi_gpu_configs(world, config):
 
 @pytest.mark.timeout(600)
 def test_bench_extras_two_ranks():
-    """Default extras over 2 gloo ranks: the executed 80 % regime (MRU_spec / EFT / DFS) and the
-    strong-scaling pipeline run with cross-GPU edges."""
+    """Default extras over 2 gloo ranks: the reference's experiment executed — ONE DAG over the
+    two ranks under the 80 % regime with the reference's 60/40 node split (MRU_spec / EFT / DFS,
+    real cross-GPU edges), the per-GPU-replica form, and the strong-scaling pipeline run."""
     lines = _torchrun(2, ["--model", "tiny-gpt2", "--seq", "16", "--steps", "1", "--warmup", "1",
                           "--extra-steps", "1", "--strong-mb", "4"])
     ln = lines[0]
     cap = ln["capped"]
-    assert cap["memory_regime"] == 0.8 and cap["cost_model"] == "reference"
+    assert cap["memory_regime"] == 0.8 and cap["cost_model"] == "reference" and cap["replicas"] == 1
+    assert len(cap["mem_cap_gb_per_gpu"]) == 2
+    assert abs(cap["mem_cap_gb_per_gpu"][0] / cap["mem_cap_gb_per_gpu"][1] - 1.5) < 1e-6  # 60 / 40
     for s in ("MRU_spec", "EFT", "DFS"):
-        assert cap[s]["ms_per_step"] > 0 and cap[s]["tasks_total"] > 0
-    assert cap["MRU_spec"]["tasks_completed"] == cap["MRU_spec"]["tasks_total"]
+        assert cap[s]["ms_per_step"] > 0 and cap[s]["tasks_total"] == 19
+    assert cap["MRU_spec"]["tasks_completed"] == 19 and cap["MRU_spec"]["cross_gpu_edges"] > 0
+    assert cap["MRU_spec"]["cross_gpu_bytes"] > 0
+    assert cap["DFS"]["tasks_completed"] < 19  # the reference's DFS fails tasks at 80 %
+    rep = ln["capped_replica"]
+    assert rep["replicas"] == 2
+    assert rep["MRU_spec"]["tasks_completed"] == rep["MRU_spec"]["tasks_total"]
     assert ln["strong"]["cross_gpu_edges"] > 0 and ln["strong"]["micro_batches"] == 4
     # EFT keeps different equal groups resident on the two replicas: a group one rank streams is
     # re-filled from the other rank's arena (RCCL p2p) rather than from the host
-    assert cap["EFT"]["peer_fill_gb_per_step"] > 0
-    assert cap["EFT"]["peer_fill_gb_per_step"] <= cap["EFT"]["refill_gb_per_step"]
+    assert rep["EFT"]["peer_fill_gb_per_step"] > 0
+    assert rep["EFT"]["peer_fill_gb_per_step"] <= rep["EFT"]["refill_gb_per_step"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_capped_one_dag_matches_reference_completions(world):
+    """The reference's experiment on the REAL GPT-2 DAG (99 tasks), planned as bench.py's capped
+    sub-result plans it: ONE DAG over N nodes at the 80 % regime with the reference's node split
+    and cost model. Completion counts equal what running the reference's own schedulers gives
+    for the same DAG and nodes (/root/reference/schedulers.py + simulation.py:161-214, measured:
+    MRU_spec 99 at every N; DFS 79 / 74 / 66 and Critical 79 / 77 / 73 at N = 2 / 4 / 8)."""
+    from distributed_llm_scheduler_amd.eval.execute import regime_node_spec
+    from distributed_llm_scheduler_amd.parallel import runtime
+
+    ref = {2: {"DFS": 79, "Critical": 79, "MRU_spec": 99}, 4: {"DFS": 74, "Critical": 77, "MRU_spec": 99},
+           8: {"DFS": 66, "Critical": 73, "MRU_spec": 99}}[world]
+    spec = regime_node_spec("gpt2", 0.8, world)
+    for sched, want in ref.items():
+        p = runtime.plan("gpt2", world=world, scheduler=sched, cap_gb=[m for m, _ in spec],
+                         node_speeds=[v for _, v in spec], cost_model="reference")
+        assert p.completed == want, (sched, p.completed, want)
+        assert p.stats["cross_gpu_edges"] > 0
+    p = runtime.plan("gpt2", world=world, scheduler="EFT", cap_gb=[m for m, _ in spec],
+                     node_speeds=[v for _, v in spec], cost_model="reference")
+    assert p.completed == 99
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no launcher starts its own 2 rank processes (rendezvous on
+    127.0.0.1) and reports n_gpus 2 from a 2-rank job."""
+    lines = _run([sys.executable, "bench.py", "--gpus", "2", *ARGS, "--no-extras"])
+    assert len(lines) == 1
+    _check(lines[0], 2)
+    assert lines[0]["rccl_world"] == 2 and len(lines[0]["per_rank_ms"]) == 2
+
+
+def test_bench_refuses_world_mismatch():
+    """A job whose world size is not --gpus exits non-zero instead of reporting another N."""
+    env = dict(os.environ, PYTHONPATH=REPO, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS, "--no-extras"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and not _json_lines(r.stdout)
 
 
 @pytest.mark.timeout(300)

@@ -241,3 +241,36 @@ def test_post_norm_under_memory_cap_on_gpu(monkeypatch, model):
     assert st.param_fills > 0
     torch.cuda.synchronize()
     _check(p, ex, store, 0.03)
+
+
+@pytest.mark.timeout(300)
+def test_gpt2_every_block_matches_reference():
+    """The real GPT-2-small DAG at S = 512 (the benchmarked shapes), block by block: the residual
+    stream after each of the 12 blocks (the ``layer_i_output`` groups: fc2 GEMM + bias +
+    residual, with the next block's folded-LN statistics handed over) against the fp32 reference
+    — an error confined to one layer's kernel cannot hide under the end-to-end tolerance."""
+    S = 512
+    p = runtime.plan("gpt2", world=1, seq=S, batch=1)
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=False)
+    ex.step()  # weights resident and transformed
+    got = {}
+    orig = ex._issue_run
+
+    def issue(i, ins, stats, events):
+        orig(i, ins, stats, events)
+        if ins.task.endswith("_output") and ins.task.startswith("layer_"):
+            got[int(ins.task.split("_")[1])] = ex._views[ins.task].float().clone()
+
+    ex._issue_run = issue
+    ex.step()
+    torch.cuda.synchronize()
+    tok = synthetic_tokens("@tokens", S, p.cfg.vocab_size).view(1, S)
+    hidden = []
+    reference.gpt2_forward(p.cfg, store, tok, hidden=hidden)
+    assert sorted(got) == list(range(12))
+    for i, ref in enumerate(hidden):
+        out = got[i].cpu().view_as(ref)
+        err = (out - ref).abs().max().item()
+        scale = ref.abs().max().item()
+        assert err < 0.02 * scale, (i, err, scale)

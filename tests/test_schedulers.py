@@ -323,3 +323,20 @@ def test_eft_lru_mode_still_available():
         s, _ = run(EFTScheduler, tasks, [Node("n", 1.6)], cyclic=cyc)
         loads[cyc] = sum(1 for e in s.events if e[1] == "LOAD")
     assert loads[True] < loads[False] == 12
+
+
+def test_native_core_failure_is_loud(monkeypatch):
+    """A broken native core build raises instead of silently handing every placement to the
+    pure-Python engine; DLS_NO_NATIVE=1 selects that engine on purpose."""
+    from distributed_llm_scheduler_amd import _build
+    from distributed_llm_scheduler_amd.core import native
+
+    def broken(*a, **k):
+        raise RuntimeError("compiler exploded")
+
+    monkeypatch.setattr(native, "_mod", None)
+    monkeypatch.setattr(_build, "build_core", broken)
+    with pytest.raises(native.NativeCoreError):
+        native.load()
+    monkeypatch.setenv("DLS_NO_NATIVE", "1")
+    assert native.load() is None and not native.available()
