@@ -10,6 +10,11 @@
 #   pmc    COUNTERS CMD   one rocprofv3 --pmc pass (<= the per-block counter limits) over CMD
 #   ab     VAR A B [ARGS] alternating bench runs under two values of an environment variable
 #   trees  ALT [ARGS]     alternating bench runs of another built source tree ALT against this one
+#   tables "T1 T2[@VAR=V]" [ARGS]  alternating bench runs under GEMM tuning tables (DLS_GEMM_TUNING)
+#   retune MODEL          exhaustive in-DAG GEMM refinement (benchmarks/refine_dag.py), then an A/B
+#                         of the original table against the refined one
+#   stamps                in-kernel phase stamps of the GPT-2 GEMM shapes (gpubin/gemm_stamps,
+#                         built from benchmarks/gemm_stamps.hip)
 # Output lands in gpurun_out/${TAG:-job}/.
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -78,6 +83,38 @@ case "$job" in
         echo "$t $(ms $O/t.json)"
       done
     done
+    ;;
+  tables)
+    tabs="$1"; shift
+    for i in $(seq ${ROUNDS:-3}); do
+      for e in $tabs; do
+        t=${e%%@*}; ev=""; [ "$e" != "$t" ] && ev=${e#*@}; ev=${ev//,/ }
+        env DLS_GEMM_TUNING="$t" $ev timeout -k 10 300 python bench.py --no-extras --steps ${STEPS:-200} --warmup 10 "$@" \
+          > $O/t.json 2> $O/t.err || { tail -5 $O/t.err; exit 3; }
+        echo "$(basename $t) $ev $(ms $O/t.json)" | tee -a $O/tables.txt
+      done
+    done
+    ;;
+  retune)
+    m="${1:-gpt2}"
+    cp distributed_llm_scheduler_amd/ops/gemm_tuning.json $O/orig.json
+    cp distributed_llm_scheduler_amd/ops/gemm_tuning.json $O/refined.json
+    DLS_GEMM_TUNING=$O/refined.json timeout -k 10 900 python benchmarks/refine_dag.py --model $m --reps ${REPS:-20} \
+      > $O/refine.json 2> $O/refine.err || { tail -20 $O/refine.err; exit 4; }
+    for i in 1 2; do
+      for t in refined orig; do
+        DLS_GEMM_TUNING=$O/$t.json timeout -k 10 300 python bench.py --model $m --steps 100 --warmup 5 --no-extras \
+          > $O/b_$t.json 2>/dev/null || exit 5
+        echo "$t $(ms $O/b_$t.json)"
+      done
+    done
+    ;;
+  stamps)
+    : > $O/stamps.txt
+    for shape in "24 512 2304 768" "27 512 768 768" "27 512 768 3072" "17 512 3072 768" "24 512 768 3072" "34 512 50304 768"; do
+      timeout -k 5 30 gpubin/gemm_stamps $shape >> $O/stamps.txt 2>&1 || { echo "FAILED $shape"; exit 3; }
+    done
+    cat $O/stamps.txt
     ;;
   *)
     echo "unknown job $job"; exit 2
