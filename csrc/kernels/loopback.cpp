@@ -1,9 +1,9 @@
-// Single-GPU multi-rank loopback transport: see loopback.h. Used by the executor's Python p2p
+// Single-GPU multi-rank loopback transport: see loopback.hpp. Used by the executor's Python p2p
 // path (parallel/loopback.py) and by the native step runner's SEND / RECV / WORK_WAIT actions
 // (runner.cpp, set_loopback), so one GPU exercises exactly the stream ordering an RCCL job
 // relies on: the producer's kernels before the send, the transfer, the consumer's kernels after
 // the receive, a sent buffer not overwritten before its send completed.
-#include "loopback.h"
+#include "loopback.hpp"
 
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/utils/pybind.h>
@@ -18,7 +18,7 @@ LoopbackHub::Done::~Done() {
 }
 
 LoopbackHub::LoopbackHub(int64_t world, double delay_us, bool poison, double timeout_s)
-    : world_(world), delay_us_(delay_us), poison_(poison), timeout_s_(timeout_s) {
+    : match_((int)world), delay_us_(delay_us), poison_(poison), timeout_s_(timeout_s) {
   TORCH_CHECK(world >= 1, "loopback: world size");
 }
 
@@ -29,51 +29,28 @@ LoopbackHub::~LoopbackHub() {
   }
 }
 
-int64_t LoopbackHub::outstanding() {
-  std::lock_guard<std::mutex> lk(mu_);
-  return (int64_t)ops_.size();
-}
-
 int64_t LoopbackHub::post(bool send, const at::Tensor& t, int64_t self, int64_t peer) {
-  TORCH_CHECK(self >= 0 && self < world_ && peer >= 0 && peer < world_ && peer != self,
-              "loopback: bad ranks ", self, " -> ", peer);
   TORCH_CHECK(t.is_contiguous(), "loopback: p2p buffers must be contiguous");
   Op op;
-  op.send = send;
   op.t = t;
-  op.self = (int)self;
-  op.peer = (int)peer;
   if (t.is_cuda()) {
-    const int dev = t.get_device();
-    hipStream_t cur = c10::hip::getCurrentHIPStream(dev).stream();
+    hipStream_t cur = c10::hip::getCurrentHIPStream(t.get_device()).stream();
     if (!send && poison_) C10_HIP_CHECK(hipMemsetAsync(t.data_ptr(), 0xFF, t.nbytes(), cur));
     C10_HIP_CHECK(hipEventCreateWithFlags(&op.ready, hipEventDisableTiming));
     C10_HIP_CHECK(hipEventRecord(op.ready, cur));  // the buffer is ready once cur gets here
   } else if (!send && poison_) {
     std::memset(t.data_ptr(), 0xFF, t.nbytes());
   }
-  std::lock_guard<std::mutex> lk(mu_);
-  const int64_t id = next_++;
-  auto key = send ? std::make_pair(op.self, op.peer) : std::make_pair(op.peer, op.self);
-  auto& other = send ? recvs_[key] : sends_[key];
-  auto& mine = send ? sends_[key] : recvs_[key];
-  ops_.emplace(id, std::move(op));
-  if (!other.empty()) {
-    const int64_t oid = other.front();
-    other.pop_front();
-    Op& a = ops_.at(id);
-    Op& b = ops_.at(oid);
-    match(send ? a : b, send ? b : a);
-    cv_.notify_all();
-  } else {
-    mine.push_back(id);
+  try {
+    return match_.post(send, (int)self, (int)peer, std::move(op), [this](Op& s, Op& r) { copy(s, r); });
+  } catch (const std::invalid_argument& e) {
+    TORCH_CHECK(false, "loopback: ", e.what());
   }
-  return id;
 }
 
-void LoopbackHub::match(Op& s, Op& r) {
-  TORCH_CHECK(s.t.nbytes() == r.t.nbytes(), "loopback: rank ", s.self, " sends ", s.t.nbytes(), " bytes, rank ",
-              r.self, " receives ", r.t.nbytes());
+void LoopbackHub::copy(Op& s, Op& r) {
+  TORCH_CHECK(s.t.nbytes() == r.t.nbytes(), "loopback: a send of ", s.t.nbytes(), " bytes met a receive of ",
+              r.t.nbytes());
   TORCH_CHECK(s.t.is_cuda() == r.t.is_cuda(), "loopback: send and recv on different device kinds");
   auto done = std::make_shared<Done>();
   if (s.t.is_cuda()) {
@@ -95,31 +72,21 @@ void LoopbackHub::match(Op& s, Op& r) {
     std::memcpy(r.t.data_ptr(), s.t.data_ptr(), s.t.nbytes());
   }
   s.done = r.done = done;
-  s.matched = r.matched = true;
-  transfers_ += 1;
   bytes_ += (int64_t)s.t.nbytes();
 }
 
 void LoopbackHub::wait(int64_t id) {
-  std::shared_ptr<Done> done;
-  at::Tensor t;
-  {
-    std::unique_lock<std::mutex> lk(mu_);
-    auto it = ops_.find(id);
-    TORCH_CHECK(it != ops_.end(), "loopback: unknown or already waited op ", id);
-    const bool ok = cv_.wait_for(lk, std::chrono::duration<double>(timeout_s_), [&] { return ops_.at(id).matched; });
-    if (!ok) {
-      const Op& op = ops_.at(id);
-      TORCH_CHECK(false, "loopback: rank ", op.self, "'s ", op.send ? "send to " : "recv from ", op.peer,
-                  " was never matched within ", timeout_s_, " s (mismatched or deadlocked p2p program)");
-    }
-    done = ops_.at(id).done;
-    t = ops_.at(id).t;
-    ops_.erase(id);
+  Op op;
+  if (!match_.wait(id, timeout_s_, &op)) {
+    int self = -1, peer = -1;
+    bool send = false;
+    match_.describe(id, &self, &peer, &send);
+    TORCH_CHECK(false, "loopback: rank ", self, "'s ", send ? "send to " : "recv from ", peer,
+                " was never matched within ", timeout_s_, " s (mismatched or deadlocked p2p program)");
   }
-  if (t.is_cuda() && done->ev) {
-    hipStream_t cur = c10::hip::getCurrentHIPStream(t.get_device()).stream();
-    C10_HIP_CHECK(hipStreamWaitEvent(cur, done->ev, 0));  // stream-side, as RCCL's work.wait()
+  if (op.t.is_cuda() && op.done && op.done->ev) {
+    hipStream_t cur = c10::hip::getCurrentHIPStream(op.t.get_device()).stream();
+    C10_HIP_CHECK(hipStreamWaitEvent(cur, op.done->ev, 0));  // stream-side, as RCCL's work.wait()
   }
 }
 

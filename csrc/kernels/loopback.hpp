@@ -1,17 +1,15 @@
-// Single-GPU multi-rank loopback transport (loopback.cpp).
+// Single-GPU multi-rank loopback transport (loopback.cpp); the pairing logic is dls::P2PMatcher
+// (csrc/runtime/p2p_match.h), also run under ASan / TSan by the native selftest.
 #pragma once
 
 #include <torch/extension.h>
 
-#include <condition_variable>
-#include <deque>
-#include <map>
+#include <atomic>
 #include <memory>
-#include <mutex>
-#include <unordered_map>
-#include <utility>
 
 #include <hip/hip_runtime.h>
+
+#include "../runtime/p2p_match.h"
 
 // Several ranks of one job living in ONE process on ONE GPU (each with its own compute stream,
 // each driven by its own host thread) exchange DAG edges through this hub with RCCL's p2p
@@ -32,10 +30,10 @@ class LoopbackHub {
 
   int64_t post(bool send, const at::Tensor& t, int64_t self, int64_t peer);
   void wait(int64_t id);
-  int64_t world() const { return world_; }
-  int64_t transfers() const { return transfers_; }
+  int64_t world() const { return match_.world(); }
+  int64_t transfers() { return match_.matched_pairs(); }
   int64_t bytes() const { return bytes_; }
-  int64_t outstanding();
+  int64_t outstanding() { return match_.outstanding(); }
 
  private:
   struct Done {
@@ -43,25 +41,17 @@ class LoopbackHub {
     ~Done();
   };
   struct Op {
-    bool send = false;
     at::Tensor t;
-    int self = 0, peer = 0;
     hipEvent_t ready = nullptr;
     std::shared_ptr<Done> done;
-    bool matched = false;
   };
-  void match(Op& s, Op& r);
+  void copy(Op& s, Op& r);  // runs under the matcher's lock when a send meets its receive
 
-  int64_t world_;
+  dls::P2PMatcher<Op> match_;
   double delay_us_;
   bool poison_;
   double timeout_s_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::map<std::pair<int, int>, std::deque<int64_t>> sends_, recvs_;  // unmatched, by (src, dst)
-  std::unordered_map<int64_t, Op> ops_;
-  int64_t next_ = 0;
-  int64_t transfers_ = 0, bytes_ = 0;
+  std::atomic<int64_t> bytes_{0};
   hipStream_t stream_ = nullptr;
   int device_ = -1;
 };

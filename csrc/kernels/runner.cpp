@@ -17,7 +17,9 @@
 // are one ncclGroupStart/End through c10d coalescing where the backend supports it, and share
 // one work). Every op still outstanding at the end of the step is waited for, as the Python
 // step does. ``set_loopback`` routes the p2p actions through the single-GPU loopback hub
-// (loopback.h) instead of a ProcessGroup: several ranks in one process, one GPU.
+// (loopback.hpp) instead of a ProcessGroup: several ranks in one process, one GPU. The action
+// loop itself is dls::run_actions (csrc/runtime/p2p_match.h), which the native selftest also
+// runs under ASan / TSan against a CPU backend.
 #include <torch/extension.h>
 #include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/csrc/utils/pybind.h>
@@ -27,25 +29,66 @@
 #include <vector>
 
 #include "kernels.h"
-#include "loopback.h"
+#include "loopback.hpp"
 
 namespace {
 
-enum Kind : int { GRAPH = 0, PULL, MEMCPY, MEMSET, EV_RECORD, EV_WAIT, SEND, RECV, WORK_WAIT, PYCALL, GROUP_BEGIN,
-                  GROUP_END };
+using Action = dls::StepAction<at::Tensor, py::object>;
+using dls::ActKind;
 
-struct Action {
-  Kind kind;
-  int stream = 0;  // 0 compute (torch's current stream at run()), 1 the copy stream
-  uint64_t exec = 0;
-  void* dst = nullptr;
-  const void* src = nullptr;
-  size_t bytes = 0;
-  int blocks = 0;
-  int value = 0;
-  int index = 0;  // event index / work index / peer rank
-  at::Tensor tensor;
-  py::object fn;
+// a posted p2p op: a c10d work (RCCL / gloo) or a loopback hub op
+struct RunnerWork {
+  c10::intrusive_ptr<c10d::Work> w;
+  int64_t hub = -1;
+  explicit operator bool() const { return (bool)w || hub >= 0; }
+};
+
+// the runner's device / transport side of dls::run_actions (csrc/runtime/p2p_match.h)
+struct Backend {
+  using Work = RunnerWork;
+  hipStream_t cs = nullptr, copy = nullptr;
+  c10d::ProcessGroup* pg = nullptr;
+  LoopbackHub* hub = nullptr;
+  int64_t hub_rank = 0;
+  c10::DeviceType dev_type = c10::DeviceType::CPU;
+  const std::vector<hipEvent_t>* events = nullptr;
+
+  hipStream_t on(const Action& a) const { return a.stream == 1 && copy ? copy : cs; }
+  void graph(const Action& a) { C10_HIP_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(a.exec), cs)); }
+  void pull(const Action& a) { launch_host_pull(a.src, a.dst, (int64_t)a.bytes, a.blocks, on(a)); }
+  void memcpy(const Action& a) { C10_HIP_CHECK(hipMemcpyAsync(a.dst, a.src, a.bytes, hipMemcpyDefault, on(a))); }
+  void memset(const Action& a) { C10_HIP_CHECK(hipMemsetAsync(a.dst, a.value, a.bytes, on(a))); }
+  void record(const Action& a) { C10_HIP_CHECK(hipEventRecord((*events)[a.index], on(a))); }
+  void wait_event(const Action& a) { C10_HIP_CHECK(hipStreamWaitEvent(on(a), (*events)[a.index], 0)); }
+  void pycall(const Action& a) {
+    py::gil_scoped_acquire g;
+    a.fn();
+  }
+  Work post(const Action& a) {
+    Work w;
+    if (hub) {
+      w.hub = hub->post(a.kind == dls::SEND, a.tensor, hub_rank, a.index);
+      return w;
+    }
+    TORCH_CHECK(pg, "p2p action without a process group");
+    std::vector<at::Tensor> ts{a.tensor};
+    w.w = a.kind == dls::SEND ? pg->send(ts, a.index, 0) : pg->recv(ts, a.index, 0);
+    return w;
+  }
+  bool group_begin() {
+    const bool co = !hub && pg && pg->getBackend(dev_type)->supportsCoalescing();
+    if (co) pg->startCoalescing(dev_type);
+    return co;
+  }
+  Work group_end() {
+    Work w;
+    w.w = pg->endCoalescing(dev_type);
+    return w;
+  }
+  void wait(Work& w) {
+    if (w.hub >= 0) hub->wait(w.hub);  // the current stream waits for the hub's copy
+    else w.w->wait();                  // RCCL: the current stream waits; gloo: blocks
+  }
 };
 
 class StepRunner {
@@ -68,7 +111,7 @@ class StepRunner {
   void add_graph(uint64_t exec) {
     TORCH_CHECK(exec != 0, "null hipGraphExec");
     any_device_ = true;
-    Action a{GRAPH};
+    Action a{dls::GRAPH};
     a.exec = exec;
     acts_.push_back(a);
   }
@@ -82,7 +125,7 @@ class StepRunner {
     TORCH_CHECK(hipHostGetDevicePointer(&dev_src, src.data_ptr(), 0) == hipSuccess && dev_src != nullptr,
                 "pull: pinned host image is not mapped into the GPU address space");
     any_device_ = true;
-    Action a{PULL, (int)stream};
+    Action a{dls::PULL, (int)stream};
     a.dst = dst.data_ptr();
     a.src = dev_src;
     a.bytes = bytes;
@@ -93,7 +136,7 @@ class StepRunner {
   void add_memcpy(const at::Tensor& dst, const at::Tensor& src, int64_t bytes, int64_t stream) {
     TORCH_CHECK(dst.nbytes() >= (size_t)bytes && src.nbytes() >= (size_t)bytes, "memcpy: byte count exceeds a buffer");
     any_device_ = true;
-    Action a{MEMCPY, (int)stream};
+    Action a{dls::MEMCPY, (int)stream};
     a.dst = dst.data_ptr();
     a.src = src.data_ptr();
     a.bytes = bytes;
@@ -102,21 +145,21 @@ class StepRunner {
   }
   void add_memset(const at::Tensor& dst, int64_t value, int64_t stream) {
     any_device_ = true;
-    Action a{MEMSET, (int)stream};
+    Action a{dls::MEMSET, (int)stream};
     a.dst = dst.data_ptr();
     a.bytes = dst.nbytes();
     a.value = (int)value;
     acts_.push_back(a);
   }
   // runner-owned events, addressed by index (created on first use)
-  void add_event_record(int64_t ev, int64_t stream) { acts_.push_back(event_action(EV_RECORD, ev, stream)); }
-  void add_event_wait(int64_t ev, int64_t stream) { acts_.push_back(event_action(EV_WAIT, ev, stream)); }
+  void add_event_record(int64_t ev, int64_t stream) { acts_.push_back(event_action(dls::EV_RECORD, ev, stream)); }
+  void add_event_wait(int64_t ev, int64_t stream) { acts_.push_back(event_action(dls::EV_WAIT, ev, stream)); }
   // p2p ops get work indices in the order they are added
-  int64_t add_send(const at::Tensor& t, int64_t peer) { return add_p2p(SEND, t, peer); }
-  int64_t add_recv(const at::Tensor& t, int64_t peer) { return add_p2p(RECV, t, peer); }
+  int64_t add_send(const at::Tensor& t, int64_t peer) { return add_p2p(dls::SEND, t, peer); }
+  int64_t add_recv(const at::Tensor& t, int64_t peer) { return add_p2p(dls::RECV, t, peer); }
   void add_work_wait(int64_t w) {
     TORCH_CHECK(w >= 0 && w < n_works_, "unknown p2p work ", w);
-    Action a{WORK_WAIT};
+    Action a{dls::WORK_WAIT};
     a.index = (int)w;
     acts_.push_back(a);
   }
@@ -124,11 +167,11 @@ class StepRunner {
   void add_group_begin() {
     TORCH_CHECK(group_open_ < 0, "nested p2p group");
     group_open_ = n_works_;
-    acts_.push_back(Action{GROUP_BEGIN});
+    acts_.push_back(Action{dls::GROUP_BEGIN});
   }
   void add_group_end() {
     TORCH_CHECK(group_open_ >= 0, "p2p group end without a begin");
-    Action a{GROUP_END};
+    Action a{dls::GROUP_END};
     a.index = group_open_;  // first work index of the group; a.value = one past the last
     a.value = n_works_;
     group_open_ = -1;
@@ -136,7 +179,7 @@ class StepRunner {
   }
   // CPU backend only: a kernel group has no hipGraph there, the runner calls back
   void add_pycall(py::object fn) {
-    Action a{PYCALL};
+    Action a{dls::PYCALL};
     a.fn = fn;
     acts_.push_back(a);
   }
@@ -144,82 +187,20 @@ class StepRunner {
   int64_t size() const { return (int64_t)acts_.size(); }
 
   void run() {
-    const bool gpu = any_device_;
-    hipStream_t cs = gpu ? c10::hip::getCurrentHIPStream().stream() : nullptr;
     TORCH_CHECK(group_open_ < 0, "p2p group left open");
-    std::vector<c10::intrusive_ptr<c10d::Work>> works(n_works_);
-    std::vector<int64_t> hub_ops(n_works_, -1);
-    bool coalescing = false;
-    const auto dev_type = gpu ? c10::DeviceType::CUDA : c10::DeviceType::CPU;
-    for (auto& a : acts_) {
-      hipStream_t s = a.stream == 1 && copy_ ? copy_ : cs;
-      switch (a.kind) {
-        case GRAPH:
-          C10_HIP_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(a.exec), cs));
-          break;
-        case PULL:
-          launch_host_pull(a.src, a.dst, (int64_t)a.bytes, a.blocks, s);
-          break;
-        case MEMCPY:
-          C10_HIP_CHECK(hipMemcpyAsync(a.dst, a.src, a.bytes, hipMemcpyDefault, s));
-          break;
-        case MEMSET:
-          C10_HIP_CHECK(hipMemsetAsync(a.dst, a.value, a.bytes, s));
-          break;
-        case EV_RECORD:
-          C10_HIP_CHECK(hipEventRecord(event(a.index), s));
-          break;
-        case EV_WAIT:
-          C10_HIP_CHECK(hipStreamWaitEvent(s, event(a.index), 0));
-          break;
-        case SEND:
-        case RECV: {
-          if (hub_) {
-            hub_ops[a.value] = hub_->post(a.kind == SEND, a.tensor, hub_rank_, a.index);
-            break;
-          }
-          TORCH_CHECK(pg_, "p2p action without a process group");
-          std::vector<at::Tensor> ts{a.tensor};
-          works[a.value] = a.kind == SEND ? pg_->send(ts, a.index, 0) : pg_->recv(ts, a.index, 0);
-          break;
-        }
-        case GROUP_BEGIN:
-          coalescing = !hub_ && pg_ && pg_->getBackend(dev_type)->supportsCoalescing();
-          if (coalescing) pg_->startCoalescing(dev_type);
-          break;
-        case GROUP_END:
-          if (coalescing) {  // ONE work for the whole group: every op of it waits on it
-            auto w = pg_->endCoalescing(dev_type);
-            for (int i = a.index; i < a.value; ++i) works[i] = w;
-            coalescing = false;
-          }
-          break;
-        case WORK_WAIT:
-          if (hub_) {
-            if (hub_ops[a.index] >= 0) {
-              hub_->wait(hub_ops[a.index]);  // the current stream waits for the hub's copy
-              hub_ops[a.index] = -1;
-            }
-          } else if (works[a.index]) {
-            works[a.index]->wait();  // RCCL: the current stream waits; gloo: blocks
-            works[a.index].reset();
-          }
-          break;
-        case PYCALL: {
-          py::gil_scoped_acquire g;
-          a.fn();
-          break;
-        }
-      }
-    }
-    for (auto& w : works)  // the step's p2p ops are complete when it returns (as in Python)
-      if (w) w->wait();
-    for (auto h : hub_ops)
-      if (h >= 0) hub_->wait(h);
+    Backend b;
+    b.cs = any_device_ ? c10::hip::getCurrentHIPStream().stream() : nullptr;
+    b.copy = copy_;
+    b.pg = pg_.get();
+    b.hub = hub_.get();
+    b.hub_rank = hub_rank_;
+    b.dev_type = any_device_ ? c10::DeviceType::CUDA : c10::DeviceType::CPU;
+    b.events = &events_;
+    dls::run_actions(acts_, n_works_, b);
   }
 
  private:
-  Action event_action(Kind k, int64_t ev, int64_t stream) {
+  Action event_action(ActKind k, int64_t ev, int64_t stream) {
     TORCH_CHECK(ev >= 0 && ev < 4096, "event index");
     if ((size_t)ev >= events_.size()) events_.resize(ev + 1, nullptr);
     if (!events_[ev]) C10_HIP_CHECK(hipEventCreateWithFlags(&events_[ev], hipEventDisableTiming));
@@ -228,8 +209,7 @@ class StepRunner {
     a.index = (int)ev;
     return a;
   }
-  hipEvent_t event(int i) { return events_[i]; }
-  int64_t add_p2p(Kind k, const at::Tensor& t, int64_t peer) {
+  int64_t add_p2p(ActKind k, const at::Tensor& t, int64_t peer) {
     Action a{k};
     a.tensor = t;
     a.index = (int)peer;

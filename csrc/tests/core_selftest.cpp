@@ -23,6 +23,7 @@
 
 #include "../core/scheduler.h"
 #include "../runtime/arena.h"
+#include "../runtime/p2p_match.h"
 
 namespace {
 
@@ -176,6 +177,132 @@ void worker(int id, int instances, unsigned seed) {
 
 }  // namespace
 
+// ---- the step runner's action loop + the loopback pairing, one thread per rank (TSan: the
+// matcher's lock / condition variable; ASan: work indices, buffers, group bookkeeping)
+struct CpuWork {
+  int64_t id = -1;
+  explicit operator bool() const { return id >= 0; }
+};
+using CpuAction = dls::StepAction<std::vector<float>*, std::function<void()>>;
+struct CpuOp {
+  std::vector<float>* buf = nullptr;
+};
+
+struct CpuBackend {
+  using Work = CpuWork;
+  dls::P2PMatcher<CpuOp>* m = nullptr;
+  int rank = 0;
+  bool coalesce = false;
+  void graph(const CpuAction&) {}
+  void pull(const CpuAction&) {}
+  void memcpy(const CpuAction&) {}
+  void memset(const CpuAction&) {}
+  void record(const CpuAction&) {}
+  void wait_event(const CpuAction&) {}
+  void pycall(const CpuAction& a) { a.fn(); }
+  Work post(const CpuAction& a) {
+    CpuOp op;
+    op.buf = a.tensor;
+    Work w;
+    w.id = m->post(a.kind == dls::SEND, rank, a.index, op, [](CpuOp& s, CpuOp& r) {
+      if (s.buf->size() != r.buf->size()) throw std::runtime_error("size mismatch");
+      std::copy(s.buf->begin(), s.buf->end(), r.buf->begin());
+    });
+    return w;
+  }
+  bool group_begin() { return false; }  // one work per op (the gloo behaviour)
+  Work group_end() { return Work{}; }
+  void wait(Work& w) {
+    if (!m->wait(w.id, 30.0)) {
+      std::fprintf(stderr, "rank %d: p2p op %lld never matched\n", rank, (long long)w.id);
+      g_failures.fetch_add(1);
+    }
+  }
+};
+
+// A pipeline of `world` ranks, `mb` micro-batches, each a vector of `n` floats: rank r receives
+// micro-batch k from r-1 (rank 0 makes it), adds r+1, sends it on; the last rank checks it. Every
+// rank's step is a recorded action list (grouped recv of k+1 with the send of k, waits before
+// the compute callbacks) replayed `steps` times — the step runner's shape, run by run_actions.
+void p2p_pipeline(int world, int mb, int n, int steps) {
+  dls::P2PMatcher<CpuOp> m(world);
+  std::vector<std::vector<std::vector<float>>> in(world, std::vector<std::vector<float>>(mb, std::vector<float>(n)));
+  std::vector<std::vector<std::vector<float>>> out(world, std::vector<std::vector<float>>(mb, std::vector<float>(n)));
+  std::vector<std::thread> ranks;
+  for (int r = 0; r < world; ++r) {
+    ranks.emplace_back([&, r] {
+      std::vector<CpuAction> acts;
+      int works = 0;
+      std::vector<int> recv_w(mb, -1), send_w(mb, -1);
+      auto add_p2p = [&](dls::ActKind k, std::vector<float>* b, int peer) {
+        CpuAction a{k};
+        a.tensor = b;
+        a.index = peer;
+        a.value = works;
+        acts.push_back(a);
+        return works++;
+      };
+      auto add_wait = [&](int w) {
+        CpuAction a{dls::WORK_WAIT};
+        a.index = w;
+        acts.push_back(a);
+      };
+      auto step_no = std::make_shared<int>(0);
+      {
+        CpuAction a{dls::PYCALL};
+        a.fn = [step_no] { ++*step_no; };
+        acts.push_back(a);
+      }
+      if (r > 0) recv_w[0] = add_p2p(dls::RECV, &in[r][0], r - 1);
+      for (int k = 0; k < mb; ++k) {
+        if (r > 0) add_wait(recv_w[k]);
+        CpuAction c{dls::PYCALL};
+        c.fn = [&, r, k, step_no] {
+          for (int i = 0; i < n; ++i) {
+            const float base = r == 0 ? (float)(k * 1000 + i + *step_no) : in[r][k][i];
+            out[r][k][i] = base + (float)(r + 1);
+          }
+        };
+        acts.push_back(c);
+        const bool grp = r + 1 < world && r > 0 && k + 1 < mb;
+        if (grp) acts.push_back(CpuAction{dls::GROUP_BEGIN});
+        const int g0 = works;
+        if (r + 1 < world) send_w[k] = add_p2p(dls::SEND, &out[r][k], r + 1);
+        if (r > 0 && k + 1 < mb) recv_w[k + 1] = add_p2p(dls::RECV, &in[r][k + 1], r - 1);
+        if (grp) {
+          CpuAction e{dls::GROUP_END};
+          e.index = g0;
+          e.value = works;
+          acts.push_back(e);
+        }
+      }
+      if (r + 1 == world) {  // the last rank checks every micro-batch of this step
+        CpuAction c{dls::PYCALL};
+        c.fn = [&, r, step_no] {
+          for (int k = 0; k < mb; ++k)
+            for (int i = 0; i < n; ++i) {
+              const float want = (float)(k * 1000 + i + *step_no) + (float)(world * (world + 1) / 2);
+              if (out[r][k][i] != want) {
+                g_failures.fetch_add(1);
+                std::fprintf(stderr, "p2p pipeline: step %d mb %d [%d] = %f, want %f\n", *step_no, k, i,
+                             out[r][k][i], want);
+                return;
+              }
+            }
+        };
+        acts.push_back(c);
+      }
+      CpuBackend b;
+      b.m = &m;
+      b.rank = r;
+      for (int s = 0; s < steps; ++s) dls::run_actions(acts, works, b);
+    });
+  }
+  for (auto& t : ranks) t.join();
+  CHECK(m.outstanding() == 0, "p2p: %lld ops left unwaited", (long long)m.outstanding());
+  CHECK(m.matched_pairs() == (int64_t)steps * mb * (world - 1), "p2p: %lld transfers", (long long)m.matched_pairs());
+}
+
 int main(int argc, char** argv) {
   int instances = 200, threads = 1;
   unsigned seed = 1;
@@ -204,6 +331,8 @@ int main(int argc, char** argv) {
     for (int t = 0; t < T; ++t) n += r.completed[t] != 0;
     CHECK(n == T, "deep chain completed %d of %d", n, T);
   }
+  // the step runner's action loop over the loopback pairing: 2 / 4 / 8 rank threads
+  for (int world : {2, 4, 8}) p2p_pipeline(world, 4, 257, 20);
   std::vector<std::thread> pool;
   for (int t = 0; t < threads; ++t) pool.emplace_back(worker, t, instances, seed);
   for (auto& th : pool) th.join();

@@ -148,19 +148,23 @@ def build_ops(force: bool = False, verbose: bool = False, jobs: int = 8) -> str:
     """Compile every csrc/kernels/*.hip for gfx950 and link the torch op library."""
     kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
-    # host C++ against torch: the op bindings and the native step runner (runner.cpp)
+    # host C++ against torch: the op bindings, the native step runner (runner.cpp) and the
+    # loopback hub; their own headers (*.hpp, csrc/runtime/p2p_match.h) are host-only, so editing
+    # them does not recompile the kernels
     hosts = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.cpp")))
-    if not force and not _stale(OPS_SO, kern + hdrs + hosts):
+    host_hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hpp"))) + [os.path.join(CSRC, "runtime", "p2p_match.h")]
+    srcs = kern + hdrs + hosts + host_hdrs
+    if not force and not _stale(OPS_SO, srcs):
         return OPS_SO
     with _BuildLock("ops"):
-        if not force and not _stale(OPS_SO, kern + hdrs + hosts):
+        if not force and not _stale(OPS_SO, srcs):
             return OPS_SO  # another process built it while we waited
-        return _build_ops(kern, hdrs, hosts, force, verbose, jobs)
+        return _build_ops(kern, hdrs, hosts, host_hdrs, force, verbose, jobs)
 
 
-def _build_ops(kern, hdrs, hosts, force, verbose, jobs) -> str:
+def _build_ops(kern, hdrs, hosts, host_hdrs, force, verbose, jobs) -> str:
     os.makedirs(BUILD_DIR, exist_ok=True)
-    d0 = _digest(kern + hdrs + hosts)
+    d0 = _digest(kern + hdrs + hosts + host_hdrs)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     inc, defs, libs = _torch_flags()
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
@@ -183,18 +187,19 @@ def _build_ops(kern, hdrs, hosts, force, verbose, jobs) -> str:
 
     def compile_host(src):
         obj = os.path.join(BUILD_DIR, os.path.splitext(os.path.basename(src))[0] + ".o")
-        if force or _stale(obj, [src] + hdrs):
-            d = _digest([src] + hdrs)
+        deps = [src] + hdrs + host_hdrs
+        if force or _stale(obj, deps):
+            d = _digest(deps)
             _run([hipcc, "-O2", "-std=c++17", "-fPIC", *inc, *defs, f"-I{os.path.join(CSRC, 'kernels')}",
                   f"-I{ROCM}/include", "-x", "c++", "-c", src, "-o", obj], verbose)
-            _record(obj, [src] + hdrs, d)
+            _record(obj, deps, d)
         return obj
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(compile_kernel, kern)) + list(ex.map(compile_host, hosts))
     _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, *libs, "-o", OPS_SO + ".tmp"], verbose)
     os.replace(OPS_SO + ".tmp", OPS_SO)
-    _record(OPS_SO, kern + hdrs + hosts, d0)
+    _record(OPS_SO, kern + hdrs + hosts + host_hdrs, d0)
     return OPS_SO
 
 

@@ -1,6 +1,8 @@
 """The native core under AddressSanitizer + UndefinedBehaviorSanitizer and ThreadSanitizer
 (host code only — GPU sanitizers are not used on this pool). Builds csrc/tests/
-core_selftest.cpp with the scheduler core and the HBM arena, cached by source hash."""
+core_selftest.cpp with the scheduler core, the HBM arena, and the step runner's action loop over
+the loopback p2p pairing (csrc/runtime/p2p_match.h: one thread per rank, 2 / 4 / 8 ranks),
+cached by source hash."""
 import hashlib
 import os
 import shutil
@@ -10,7 +12,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRCS = ["csrc/tests/core_selftest.cpp", "csrc/core/scheduler.cpp", "csrc/runtime/arena.cpp"]
-HDRS = ["csrc/core/scheduler.h", "csrc/runtime/arena.h"]
+HDRS = ["csrc/core/scheduler.h", "csrc/runtime/arena.h", "csrc/runtime/p2p_match.h"]
 FLAGS = {
     "asan": ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
     "tsan": ["-O1", "-g", "-fsanitize=thread"],
