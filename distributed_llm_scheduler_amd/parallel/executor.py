@@ -1400,7 +1400,7 @@ class DAGExecutor:
             self._step_body(stats, ev)
             if ev is not None:
                 if self.gpu:
-                    torch.cuda.synchronize(self.device)
+                    self._sync()
                     el = lambda a: t_begin.elapsed_time(a)  # noqa: E731
                 else:
                     el = lambda a: (a - t_begin) * 1e3  # noqa: E731
@@ -1415,7 +1415,7 @@ class DAGExecutor:
         """Debug mode: every arena's trailing canary is intact and the rank's outputs are
         finite (a kernel writing past its planned region or producing NaN fails loudly)."""
         if self.gpu:
-            torch.cuda.synchronize(self.device)
+            self._sync()
         for name, full in (("activation", self._act_full), ("parameter", self._param_full),
                            ("workspace", self._ws_full)):
             tail = full[-GUARD_BYTES:]
@@ -1449,21 +1449,41 @@ class DAGExecutor:
         self._drop_runner()  # its hipGraphExec handles belong to the graphs a re-capture replaces
         if self._copy_stream is not None or self.prog.has_comm:
             return self.capture_segments()
-        torch.cuda.synchronize(self.device)
+        self._sync()
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             self._step_body(StepStats())  # warm the residency state on the capture stream
         torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
+        self._sync()
+        # captured on a side stream without torch.cuda.graph's device-wide synchronize (ranks
+        # sharing one GPU may be capturing their own graphs meanwhile)
         g = torch.cuda.CUDAGraph(keep_graph=True)
-        with torch.cuda.graph(g):
-            self._step_body(StepStats())
+        cur = torch.cuda.current_stream(self.device)
+        if self._cap_stream is None:
+            self._cap_stream = torch.cuda.Stream(self.device)
+        self._cap_stream.wait_stream(cur)
+        with torch.cuda.stream(self._cap_stream):
+            g.capture_begin(capture_error_mode="thread_local")
+            try:
+                self._step_body(StepStats())
+            finally:
+                g.capture_end()
+        cur.wait_stream(self._cap_stream)
         self.launches = ops.ext().graph_kernel_nodes(g.raw_cuda_graph())
         g.instantiate()
-        torch.cuda.synchronize(self.device)
+        self._sync()
         self._graph = g
         return True
+
+    def _sync(self) -> None:
+        """Wait for this executor's own streams (compute, copy, capture). Not a device-wide
+        synchronize: ranks sharing one GPU (parallel/loopback.py) may be capturing hipGraphs on
+        their streams meanwhile, and a device synchronize is illegal during any capture."""
+        torch.cuda.current_stream(self.device).synchronize()
+        for st in (self._copy_stream, self._cap_stream):
+            if st is not None:
+                st.synchronize()
 
     def _drop_runner(self) -> None:
         self._runner = None
@@ -1559,7 +1579,7 @@ class DAGExecutor:
         if not self._runner_ok():
             return False
         if self.gpu:
-            torch.cuda.synchronize(self.device)  # the previous steps' cross-step fills are complete
+            self._sync()  # the previous steps' cross-step fills are complete
         r = ops.ext().StepRunner()
         if self._copy_stream is not None:
             r.set_copy_stream(self._copy_stream.cuda_stream)
@@ -1582,7 +1602,7 @@ class DAGExecutor:
         """Back to the Python issue loop (a profiled step): the runner's cross-step fills become
         plain completed work."""
         if self.gpu:
-            torch.cuda.synchronize(self.device)
+            self._sync()
         self._runner = None
         self._carry = {}
         self._await = {}
@@ -1601,12 +1621,12 @@ class DAGExecutor:
                 self.step()
                 self.step()
             return False
-        torch.cuda.synchronize(self.device)
+        self._sync()
         self._capture_plan = {a: b for a, b in segs}
         self._seg_pool = torch.cuda.graph_pool_handle()
         self._step_body(StepStats())  # segments captured in order as the step reaches them
         self._capture_plan = None
-        torch.cuda.synchronize(self.device)
+        self._sync()
         built = bool(self._segments) and self.build_runner()
         if not built and self.prog.has_comm:
             # build_runner executes the step it recorded; a rank that could not record one runs
@@ -1623,11 +1643,11 @@ class DAGExecutor:
         The loop paces the issue of copy-stream fills at host speed, which on copy-bound steps
         can beat issuing the whole step at once."""
         def timed():
-            torch.cuda.synchronize(self.device)
+            self._sync()
             t0 = time.perf_counter()
             for _ in range(n):
                 self.step()
-            torch.cuda.synchronize(self.device)
+            self._sync()
             return (time.perf_counter() - t0) / n
         t_runner = timed()
         self._leave_runner()

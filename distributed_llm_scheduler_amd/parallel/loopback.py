@@ -40,14 +40,15 @@ class LoopbackRun:
 def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = True, delay_us: float = 20.0,
                  poison: bool = True, store=None, timeout_s: float = 120.0,
                  before_steps: Optional[Callable] = None, cpu_runner: bool = False,
-                 sync_debug: bool = False) -> LoopbackRun:
+                 sync_debug: bool = False, autotune: bool = False) -> LoopbackRun:
     """Build one executor per rank of ``plan`` on ``device``, then drive every rank from its own
     thread: ``warmup`` eager steps, capture (segment hipGraphs + native runner for programs with
     p2p), ``steps`` timed steps. ``before_steps(executors)`` may patch the executors first
     (negative controls). ``cpu_runner``: on the CPU backend, replay the steps from the native
     step runner (kernel groups as callbacks) instead of the Python issue loop. ``sync_debug``:
     the timed steps run under torch's sync debug mode "error" (any device->host synchronising
-    call inside a step raises)."""
+    call inside a step raises). ``autotune``: tune GEMM shapes missing from the table first (off:
+    the kernel's heuristic config — the harness checks ordering and numerics, not speed)."""
     from . import executor as exm
     from . import runtime
 
@@ -62,7 +63,8 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     for r in range(world):
         if gpu:
             with torch.cuda.stream(streams[r]):
-                exs.append(runtime.make_executor(plan, r, device, store, pg=groups[r], use_graph=capture))
+                exs.append(runtime.make_executor(plan, r, device, store, pg=groups[r], use_graph=capture,
+                                                 autotune=autotune))
         else:
             exs.append(runtime.make_executor(plan, r, device, store, pg=groups[r], use_graph=False))
     if gpu:

@@ -281,9 +281,10 @@ def device_init_ok(p: Plan, rank: int) -> bool:
 
 
 def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None, pg=None, use_graph: bool = True,
-                  trace: bool = False, debug: bool = False):
+                  trace: bool = False, debug: bool = False, autotune: bool = True):
     """``debug=True``: validate every rank's program first (parallel/validate.py) and run the
-    executor with arena canaries and output finiteness checks."""
+    executor with arena canaries and output finiteness checks. ``autotune=False``: GEMM shapes
+    missing from the tuning table run the kernel's heuristic config instead of being tuned first."""
     from .executor import DAGExecutor
 
     if debug:
@@ -294,4 +295,4 @@ def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None
             raise RuntimeError("invalid plan:\n  " + "\n  ".join(errs[:20]))
     # per-model GEMM choices by the canonical preset name (aliases such as "mixtral" resolve to it)
     return DAGExecutor(p.tasks, p.programs[rank], store or make_store(p), device, model_cfg=p.cfg,
-                       use_graph=use_graph, pg=pg, trace=trace, debug=debug, model_name=p.cfg.name)
+                       use_graph=use_graph, pg=pg, trace=trace, debug=debug, model_name=p.cfg.name, autotune=autotune)

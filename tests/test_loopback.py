@@ -28,15 +28,17 @@ CASES = {
 }
 
 
-def _plan(case, world, seq):
+def _plan(case, world, seq, batch=1, gpu=False):
     model, kw, ids = CASES[case]
+    if gpu:  # the smallest shapes the GPU kernels take (head_dim 64)
+        model = model.replace("tiny-", "mini-")
     kw = dict(kw)
     if case == "sequence" and world == 4:
         kw["sp"] = 4
     if "regime" in kw:
-        spec = regime_node_spec(model, kw.pop("regime"), world, seq=seq)
+        spec = regime_node_spec(model, kw.pop("regime"), world, batch=batch, seq=seq)
         kw.update(cap_gb=[m for m, _ in spec], node_speeds=[v for _, v in spec], cost_model="reference")
-    return runtime.plan(model, world=world, seq=seq, batch=1, **kw), ids
+    return runtime.plan(model, world=world, seq=seq, batch=batch, **kw), ids
 
 
 def _logits(p, run, ids):
@@ -56,8 +58,15 @@ def _check(p, run, store, ids, tol):
         assert torch.isfinite(out).all(), f"{rid}: non-finite logits (a consumer read a poisoned receive buffer)"
         B, S = out.shape[0], out.shape[1]
         tok = synthetic_tokens(f"{rid}@tokens", B * S, p.cfg.vocab_size).view(B, S)
-        ref = reference.forward(p.cfg, store, tok)
-        worst = max(worst, (out - ref).abs().max().item() / ref.abs().max().item())
+        margins = []
+        ref = reference.forward(p.cfg, store, tok, router_margins=margins)
+        scale = ref.abs().max().item()
+        row = (out - ref).abs().amax(-1) / scale
+        if margins:  # MoE: only rows whose k-th / (k+1)-th router logits nearly tie may route
+            risky = torch.stack([m.abs() < 0.05 for m in margins]).any(0)  # differently in bf16
+            assert (row[risky] > tol).float().mean().item() < 0.5 if risky.any() else True
+            row = row[~risky]
+        worst = max(worst, row.max().item())
     assert worst < tol, worst
     return worst
 
@@ -81,7 +90,7 @@ gpu = pytest.mark.gpu
 
 
 def _gpu_plan(case, world, seq=64):
-    return _plan(case, world, seq)
+    return _plan(case, world, seq, batch=2, gpu=True)
 
 
 @gpu
