@@ -229,7 +229,9 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
 // Joint rings (BXS == 0): A and W rows of a K-tile share one stage and one DMA batch.
 // GATHER: A row r is row arows[r] of A (MoE token gather) — a compile-time switch: a runtime
 // null check in every launch's prologue cost the GPT-2 GEMMs ~5 %.
-template <class C, bool GATHER = false>
+// APOL: cache policy of the A rows' DMA (sc1 = 16: A was written in this launch by other
+// workgroups' write-through stores — gemm_fused.hip; every other launch keeps 0)
+template <class C, bool GATHER = false, int APOL = 0>
 __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                                int kbeg, int nk, int lane, int wave, int kgrp, int wm, int wn,
@@ -256,10 +258,23 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
     }
     dst[j] = sub * C::SUB + r8 * 64;
   }
+  bool is_a[C::PW];  // wave-uniform: a DMA instruction covers 8 rows of one operand
+#pragma unroll
+  for (int j = 0; j < C::PW; ++j) {
+    const int gi = C::EVEN ? wave * C::PW + j : min(wave * C::PW + j, C::INSTR * C::KG - 1);
+    is_a[j] = 8 * (gi % C::INSTR) < C::BM;
+  }
   auto issue = [&](int kt) {
     bf16x8* stage = smem + (kt % C::STAGES) * C::STAGE;
 #pragma unroll
     for (int j = 0; j < C::PW; ++j) {
+      if constexpr (APOL != 0) {
+        if (is_a[j]) {
+          __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * (C::BK * C::KG)),
+                                           (__attribute__((address_space(3))) void*)(stage + dst[j]), 16, 0, APOL);
+          continue;
+        }
+      }
       __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * (C::BK * C::KG)),
                                        (__attribute__((address_space(3))) void*)(stage + dst[j]), 16, 0, 0);
     }
@@ -502,7 +517,10 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 // they come from ep.ext_stats).
 // WPOL: cache policy of the split rings' weight DMA (0 default, kPolStream = nt for weights
 // read exactly once per step, e.g. MoE experts far larger than the MALL)
-template <class C, int LN, int WPOL = 0, bool SKIP = false, bool GATHER = false>
+// APOL: the A rows' DMA cache policy (joint rings; mainloop_joint); PUB: the output tile is
+// stored write-through (sc1) so workgroups of the SAME launch on other XCDs can read it after
+// an agent-scope arrival count (gemm_fused.hip) — both 0 / false in every ordinary launch
+template <class C, int LN, int WPOL = 0, bool SKIP = false, bool GATHER = false, int APOL = 0, bool PUB = false>
 __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                           const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
                                           const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
@@ -537,8 +555,8 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     mainloop_split<C, WPOL, SKIP, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
                                   st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), arows);
   else
-    mainloop_joint<C, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc, st_s,
-                      st_q, arows);
+    mainloop_joint<C, GATHER, APOL>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc,
+                                    st_s, st_q, arows);
   DLS_STAMP(1)
   if constexpr (C::KG > 1) {
     // sum the K groups' accumulators into group 0 (lane-contiguous 16-B records)
@@ -851,7 +869,13 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(o[e]) + bf2f(r8[e]));
         }
-        *reinterpret_cast<bf16x8*>(Cp + (size_t)row * ldc + col) = o;
+        if constexpr (PUB) {  // write-through: the row segment leaves the XCD's L2 for memory
+          const auto rs = __builtin_amdgcn_make_buffer_rsrc(Cp, 0, 0x7fffffff, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&o), rs,
+                                                 (int)(((size_t)row * ldc + col) * 2), 0, 16);
+        } else {
+          *reinterpret_cast<bf16x8*>(Cp + (size_t)row * ldc + col) = o;
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float y = bf2f(o[e]);
@@ -1094,6 +1118,11 @@ using C40 = Cfg<128, 64, 2, 2, 3, 0, 0, 2>;    // two K groups of wave 64 x 32, 
 // MoE experts (192 routed rows, cold weights): the W ring TWO tiles deeper than the A ring —
 // 3 x 24 KiB A + 5 x 16 KiB W = 152 KiB, four weight tiles (64 KiB) in flight per CU (C33: 3)
 using C41 = Cfg<192, 128, 4, 2, 3, 0, 2>;
+// 256 x 144 tiles of 8 waves (wave 32 x 144): the TAIL of a wide GEMM whose first columns ran
+// as one whole round of 256 x 256 tiles — the GPT-2 LM head's last 17,489 columns as 244 tiles
+// (one round) instead of 138 more 256 x 256 tiles that leave 118 CUs idle (ops.linear_norm
+// column split, ops/gemm_tuning.json "col_splits"). 3 x 50 KiB joint stages.
+using C42 = Cfg<256, 144, 8, 1, 3>;
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,

@@ -159,4 +159,36 @@ void launch_moe_gather_combine(const unsigned long long* eo_ptrs, const int32_t*
 // dst (HBM) <- src (pinned host memory, device-accessible address); bytes % 16 == 0, both
 // 16-byte aligned; at most `blocks` workgroups of 256 lanes pull over the host link
 void launch_host_pull(const void* src, void* dst, int64_t bytes, int blocks, hipStream_t s);
-void launch_delay(double us, hipStream_t s);  // one wave spinning for ``us`` microseconds (loopback.cpp)
+void launch_delay(double us, hipStream_t s);
+
+// GPT-2 MLP block in one launch (gemm_fused.hip): h = act1(LN(x) W1'^T + b1) (folded norm with
+// handed-over row statistics), out = h W2^T + b2 + R (+ row statistics of out into stats_out)
+struct MlpFusedArgs {
+  const void* x;
+  int ldx;
+  const void* w1;
+  int ldw1;
+  const void* b1;
+  const float* colsum1;
+  const float* ext_stats;
+  int ln_mode;
+  float ln_eps;
+  int act1;
+  void* h;
+  int ldh;
+  const void* w2;
+  int ldw2;
+  const void* b2;
+  const void* R;
+  int ldr;
+  void* out;
+  int ldo;
+  float* stats_out;
+  int M, H, F, Hout;
+  int* ready;  // [M / 64] arrival counters, zero before the launch (reset by the launch itself)
+  int* done;   // [M / 64]
+  int* err;    // set if a poll exceeded spin_limit
+  int spin_limit;
+};
+bool mlp_fused_supported(int M, int H, int F, int Hout, int cus);
+void launch_mlp_fused(const MlpFusedArgs& p, hipStream_t s);  // one wave spinning for ``us`` microseconds (loopback.cpp)

@@ -310,6 +310,66 @@ at::Tensor swiglu(const at::Tensor& gu_in, const c10::optional<at::Tensor>& out)
   return y;
 }
 
+// GPT-2 MLP block as one launch (gemm_fused.hip): h = GELU(LN(x) W1'^T + b1') with the folded
+// LayerNorm's statistics handed over (ext_stats), out = h W2^T + b2 + residual (+ stats_out).
+// sync: int32 [2 * M / 64 + 1] zeroed once (arrival / consumer counters, error word).
+int64_t mlp_fused_cus() {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return cus;
+}
+
+bool mlp_fused_ok(int64_t M, int64_t H, int64_t F, int64_t Hout) {
+  return mlp_fused_supported((int)M, (int)H, (int)F, (int)Hout, (int)mlp_fused_cus());
+}
+
+void mlp_fused(const at::Tensor& x_in, const at::Tensor& w1, const c10::optional<at::Tensor>& b1,
+               const at::Tensor& colsum1, const at::Tensor& ext_stats, int64_t ln_mode, double eps, int64_t act1,
+               const at::Tensor& h_in, const at::Tensor& w2, const c10::optional<at::Tensor>& b2,
+               const at::Tensor& res_in, const at::Tensor& out_in, const c10::optional<at::Tensor>& stats_out,
+               const at::Tensor& sync, int64_t spin_limit) {
+  at::Tensor x = as2d(x_in), h = as2d(h_in), r = as2d(res_in), o = as2d(out_in);
+  for (auto* t : {&x, &h, &r, &o}) check_bf16(*t, "mlp_fused operand");
+  check_bf16(w1, "w1");
+  check_bf16(w2, "w2");
+  for (auto* t : {&x, &h, &r, &o}) check_rows(*t, "mlp_fused operand");
+  check_rows(w1, "w1");
+  check_rows(w2, "w2");
+  const int64_t M = x.size(0), H = x.size(1), F = w1.size(0), Hout = w2.size(0);
+  TORCH_CHECK(w1.size(1) == H && w2.size(1) == F && h.size(0) == M && h.size(1) == F && r.size(0) == M &&
+                  r.size(1) == Hout && o.size(0) == M && o.size(1) == Hout,
+              "mlp_fused: x [M][H], w1 [F][H], h [M][F], w2 [Hout][F], residual / out [M][Hout]");
+  TORCH_CHECK(mlp_fused_ok(M, H, F, Hout), "mlp_fused: shape not supported by the one-launch MLP (M ", M, ", H ", H,
+              ", F ", F, ", Hout ", Hout, ")");
+  TORCH_CHECK(ln_mode == 1 || ln_mode == 2, "mlp_fused: ln_mode 1 LayerNorm, 2 RMSNorm");
+  auto f32 = [&](const at::Tensor& t, int64_t n, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n, name,
+                " must be a contiguous fp32 GPU tensor of ", n, " elements");
+  };
+  f32(colsum1, F, "colsum1");
+  f32(ext_stats, 2 * M, "ext_stats");
+  if (stats_out.has_value()) f32(*stats_out, 2 * M, "stats_out");
+  for (auto* b : {&b1, &b2})
+    if (b->has_value()) {
+      check_bf16(**b, "bias");
+      TORCH_CHECK((*b)->is_contiguous(), "bias must be contiguous");
+    }
+  TORCH_CHECK(!b1.has_value() || b1->numel() == F, "b1 must be [F]");
+  TORCH_CHECK(!b2.has_value() || b2->numel() == Hout, "b2 must be [Hout]");
+  const int64_t rb = M / 64;
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kInt && sync.is_contiguous() && sync.numel() >= 2 * rb + 1,
+              "sync must be a zeroed int32 GPU tensor of >= 2 * M / 64 + 1 elements");
+  MlpFusedArgs p{x.data_ptr(), (int)x.stride(0), w1.data_ptr(), (int)w1.stride(0),
+                 b1.has_value() ? b1->data_ptr() : nullptr, colsum1.data_ptr<float>(), ext_stats.data_ptr<float>(),
+                 (int)ln_mode, (float)eps, (int)act1, h.data_ptr(), (int)h.stride(0), w2.data_ptr(),
+                 (int)w2.stride(0), b2.has_value() ? b2->data_ptr() : nullptr, r.data_ptr(), (int)r.stride(0),
+                 o.data_ptr(), (int)o.stride(0), stats_out.has_value() ? stats_out->data_ptr<float>() : nullptr,
+                 (int)M, (int)H, (int)F, (int)Hout, sync.data_ptr<int>(), sync.data_ptr<int>() + rb,
+                 sync.data_ptr<int>() + 2 * rb, (int)spin_limit};
+  launch_mlp_fused(p, cur_stream());
+}
+
 at::Tensor embedding(const at::Tensor& tokens, const at::Tensor& wte, const c10::optional<at::Tensor>& wpe, int64_t S,
                      const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& zero) {
   TORCH_CHECK(tokens.is_cuda() && tokens.scalar_type() == at::kInt && tokens.is_contiguous(),
@@ -647,6 +707,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu", &gelu, py::arg("x"), py::arg("out") = py::none());
   m.def("add", &add, py::arg("a"), py::arg("b"), py::arg("out") = py::none());
   m.def("swiglu", &swiglu, py::arg("gate_up"), py::arg("out") = py::none());
+  m.def("mlp_fused", &mlp_fused);
+  m.def("mlp_fused_ok", &mlp_fused_ok);
   m.def("embedding", &embedding, py::arg("tokens"), py::arg("wte"), py::arg("wpe") = py::none(), py::arg("S") = 1,
         py::arg("out") = py::none(), py::arg("zero") = py::none());
   m.def("rope_", &rope_);

@@ -294,6 +294,20 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
     a = ACT[act] if not isinstance(act, int) else act
     shp = x.shape[:-1] + (w_derived.shape[0] // 2 if a == SWIGLU else w_derived.shape[0],)
     M, N, K = x.numel() // x.shape[-1], w_derived.shape[0], w_derived.shape[1]
+    split = tuning.col_split(M, N, K, tuning.tag(a)) if ext_stats is not None and rope is None and a != SWIGLU \
+        else None
+    if split:
+        # one launch per column range (e.g. the LM head: a whole round of 256 x 256 tiles, then
+        # the remaining columns as one round of 256 x 144 tiles) into column views of ``out``
+        if out is None:
+            out = torch.empty(shp, dtype=x.dtype, device=x.device)
+        o2 = out.view(M, N)
+        r2 = residual.reshape(M, N) if residual is not None else None
+        for n0, n1, c, k in split:
+            ext().gemm(x, w_derived[n0:n1], bias_derived[n0:n1] if bias_derived is not None else None,
+                       r2[:, n0:n1] if r2 is not None else None, a, 1.0, o2[:, n0:n1], int(c), int(k),
+                       colsum[n0:n1], m, float(eps), None, False, None, None, 1, 2, 0, None, ext_stats)
+        return out
     cfg, sk = tuning.lookup_fused(M, N, K, tuning.tag(a))
     if ext_stats is None:
         sk = 1
@@ -306,6 +320,27 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
     y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, sk, colsum,
                    m, float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols), None, ext_stats)
     return y.view(shp) if out is None else out
+
+
+def mlp_fused_ok(M, H, F, Hout) -> bool:
+    """Does the one-launch MLP block (gemm_fused.hip) take this shape on this GPU?"""
+    return bool(ext().mlp_fused_ok(int(M), int(H), int(F), int(Hout)))
+
+
+def mlp_fused(x, w1_derived, b1_derived, colsum1, ext_stats, mode, eps, h, w2, b2, residual, out, stats_out=None,
+              sync=None, spin_limit=1 << 22):
+    """A pre-norm transformer MLP block as ONE launch (GPU): ``h = GELU(W1'.norm(x) + b1')``
+    (norm folded as in :func:`linear_norm`, row statistics handed over in ``ext_stats``) and
+    ``out = h W2^T + b2 + residual`` (+ each output row's statistics into ``stats_out``), the two
+    GEMMs linked inside the launch (fc1 tiles publish write-through, fc2 tiles start when their
+    rows' fc1 tiles have arrived). ``sync``: zeroed int32 [2 * M / 64 + 1]; its last word is set
+    if a wait gave up (never expected). ``h`` is written too (it is the DAG's activation)."""
+    m = {"layernorm": 1, "rmsnorm": 2}[mode]
+    if sync is None:
+        sync = torch.zeros(2 * (x.numel() // x.shape[-1]) // 64 + 1, dtype=torch.int32, device=x.device)
+    ext().mlp_fused(x, w1_derived, b1_derived, colsum1, ext_stats, m, float(eps), ACT["gelu"], h, w2, b2, residual,
+                    out, stats_out, sync, int(spin_limit))
+    return out
 
 
 def layernorm(x, w, b, eps=1e-5, residual=None, out=None, sum_out=None):

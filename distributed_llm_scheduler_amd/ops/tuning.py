@@ -24,6 +24,10 @@ _lock = threading.Lock()
 _table: Optional[Dict[str, Tuple[int, int]]] = None
 _cands: Dict[str, list] = {}     # key -> runner-up (cfg, splitk) by microbenchmark time (for in-DAG refinement)
 _refined: Dict[str, bool] = {}   # key -> chosen by whole-step timing inside a DAG
+# key -> [(first column, end column, config, splitk), ...]: the GEMM runs as one launch per
+# column range (a wide GEMM whose tile count is 1.5 rounds of the 256 CUs: a whole round of big
+# tiles, then the remaining columns as ONE round of narrower tiles)
+_col_splits: Dict[str, list] = {}
 # model -> {key: choice}: a model whose step measured faster with another config for a shape it
 # shares with other models (Mixtral-8x7B's QKV GEMM after the MoE layer vs Llama-3-8B's)
 _overrides: Dict[str, Dict[str, Tuple[int, int]]] = {}
@@ -56,6 +60,7 @@ def table() -> Dict[str, Tuple[int, int]]:
                     _table = {k: tuple(v) for k, v in doc.get("gemm", {}).items()}
                     _cands.update({k: [tuple(c) for c in v] for k, v in doc.get("candidates", {}).items()})
                     _refined.update(doc.get("refined", {}))
+                    _col_splits.update({k: [tuple(x) for x in v] for k, v in doc.get("col_splits", {}).items()})
                     _overrides.update({m: {k: tuple(v) for k, v in t.items()}
                                        for m, t in doc.get("model_overrides", {}).items()})
                 except (OSError, ValueError):
@@ -85,6 +90,15 @@ def lookup(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
     return v if v is not None else (-1, 0)
 
 
+def col_split(M: int, N: int, K: int, tg: str = ""):
+    """[(n0, n1, config, splitk), ...] if (M, N, K[, variant]) runs as several column-range
+    launches (``col_splits`` of the table; ``DLS_COL_SPLIT=0`` disables), else None."""
+    if os.environ.get("DLS_COL_SPLIT", "1") == "0":
+        return None
+    table()
+    return _col_splits.get(_key(M, N, K, tg))
+
+
 def lookup_fused(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
     """Like :func:`lookup`, for a GEMM with a fused epilogue (which the vendor library cannot
     run): if the tuned choice is ``LIB``, the fastest HIP-kernel candidate of the same
@@ -108,6 +122,7 @@ def _save() -> None:
             json.dump({"device": "MI355X (gfx950)", "gemm": {k: list(v) for k, v in sorted(table().items())},
                        "candidates": {k: [list(c) for c in v] for k, v in sorted(_cands.items())},
                        "refined": dict(sorted(_refined.items())),
+                       "col_splits": {k: [list(x) for x in v] for k, v in sorted(_col_splits.items())},
                        "model_overrides": {m: {k: list(v) for k, v in sorted(t.items())}
                                            for m, t in sorted(_overrides.items())}}, f, indent=1)
         os.replace(tmp, _PATH)
@@ -145,9 +160,9 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
 
 
 # csrc gemm_glds kKStep: K granularity per LDS-DMA config id (64; 128 / 256 for two / four K groups)
-_KSTEP = [64] * 16 + [128] * 4 + [256] * 2 + [64] * 3 + [128] * 4 + [64, 128, 64, 64, 64] + [64, 64] + [64, 64, 64, 128, 128, 64]
+_KSTEP = [64] * 16 + [128] * 4 + [256] * 2 + [64] * 3 + [128] * 4 + [64, 128, 64, 64, 64] + [64, 64] + [64, 64, 64, 128, 128, 64] + [64]
 # configs whose 48- / 112- / 144-column wave tiles cannot pair SwiGLU gate/up fragments
-SWIGLU_BAD = frozenset(range(22, 28)) | {36, 38, 39}
+SWIGLU_BAD = frozenset(range(22, 28)) | {36, 38, 39, 42}
 
 
 def kstep(cfg: int) -> int:

@@ -150,6 +150,9 @@ REFILL = os.environ.get("DLS_REFILL", "pull")
 # overwritten before the group is loaded again at the same offset
 VICTIM_REUSE = os.environ.get("DLS_VICTIM_REUSE", "0") == "1"
 REFILL_BLOCKS = int(os.environ.get("DLS_REFILL_BLOCKS", "64"))
+# a pre-norm MLP block (folded norm + fc1 + GELU, then fc2 + residual) as ONE launch
+# (ops.mlp_fused, csrc/kernels/gemm_fused.hip) where the shape fits its grid (GPU)
+MLP_FUSED = os.environ.get("DLS_MLP_FUSED", "0") == "1"
 
 
 
@@ -300,6 +303,7 @@ class DAGExecutor:
         self._pn_done: Optional[str] = None    # the norm the last producer actually wrote
         if POST_NORM not in ("0", False) and self._copy_stream is None:
             self._plan_post_norm()  # (pairs are adjacent runs: no p2p between producer and consumer)
+        self._plan_mlp_fused()
 
     def _plan_post_norm(self) -> None:
         """Pair each norm that the next group would run as its own pass (its width is above
@@ -401,6 +405,59 @@ class DAGExecutor:
                 if MOE_FUSED_ROUTE:  # the layer's router node computes its logits AND the routing
                     self._gate_route[t0.op.inputs[1]] = (E, t0.op.attrs["top_k"])
             i = j
+
+    def _plan_mlp_fused(self) -> None:
+        """Pairs (fc1 group i, fc2 group j) of a pre-norm MLP block that run as ONE launch:
+        ``norm+linear+gelu`` followed by ``linear+residual`` reading its output, the norm's row
+        statistics handed over by its input's producer, only parameter loads between the two
+        (applied at i: a program without evictions or peer loads, whose regions never move)."""
+        self._mlp_fused: Dict[int, int] = {}
+        self._mlp_skip: set = set()
+        self._mlp_loads: Dict[int, List[int]] = {}
+        self._mlp_sync = None
+        ins = self.prog.instrs
+        if not (self.gpu and MLP_FUSED) or any(x.op == "evict" or (x.op == "load" and x.peer >= 0) for x in ins):
+            return
+        for i in range(len(ins) - 1):
+            a = ins[i]
+            if a.op != "run" or a.kind != "layernorm+linear+gelu":
+                continue
+            j = i + 1
+            while j < len(ins) and ins[j].op == "load":
+                j += 1
+            if j >= len(ins):
+                continue
+            b = ins[j]
+            if b.op != "run" or b.kind != "linear+residual":
+                continue
+            g1, g2 = [self.tasks[t] for t in a.group], [self.tasks[t] for t in b.group]
+            if g2[0].dependencies != [a.task] or b.wait_sends or j in self._post_norm \
+                    or self._ext_stats.get(g1[0].op.inputs[0]) is None:
+                continue
+            x_shape, h_shape = g1[0].op.out_shape, g1[-1].op.out_shape
+            M = math.prod(x_shape[:-1])
+            if not ops.mlp_fused_ok(M, x_shape[-1], h_shape[-1], g2[-1].op.out_shape[-1]):
+                continue
+            self._mlp_fused[i] = j
+            self._mlp_skip.add(j)
+            self._mlp_loads[i] = list(range(i + 1, j))
+            if self._mlp_sync is None or self._mlp_sync.numel() < 2 * M // 64 + 1:
+                self._mlp_sync = torch.zeros(2 * M // 64 + 1, dtype=torch.int32, device=self.device)
+
+    def _run_mlp_fused(self, i: int) -> None:
+        for ld in self._mlp_loads[i]:  # fixed regions (no evictions): fc2's groups mapped up front
+            self._load(ld, self.prog.instrs[ld].param, StepStats())
+        a, b = self.prog.instrs[i], self.prog.instrs[self._mlp_fused[i]]
+        norm, fc1 = self.tasks[a.group[0]], self.tasks[a.group[1]]
+        fc2, tail = self.tasks[b.group[0]], self.tasks[b.group[-1]]
+        src = norm.op.inputs[0]
+        W1, cs, b1 = self._prep(fc1.op.weights["w"], norm, fc1.op.weights.get("b"))
+        W2 = self._w(fc2.op.weights["w"])
+        b2 = self._w(fc2.op.weights["b"]) if "b" in fc2.op.weights else None
+        res = self._flat(self._x([d for d in tail.op.inputs if d != fc2.id][0]))
+        ops.mlp_fused(self._flat(self._x(src)), W1, b1, cs, self._ext_stats[src], norm.op.kind,
+                      norm.op.attrs.get("eps", 1e-5), self._flat(self._views[a.task]), W2, b2, res,
+                      self._flat(self._views[tail.id]), self._stats_out.get(tail.id), self._mlp_sync)
 
     def _run_moe_batch(self, i: int, stats: StepStats) -> None:
         members, loads = self._moe_batch[i]
@@ -1320,8 +1377,10 @@ class DAGExecutor:
         run = self._run_group
         if i in self._moe_batch:  # the layer's experts in one grouped launch pair
             run = lambda _ins, _i=i: self._run_moe_batch(_i, stats)  # noqa: E731
-        elif i in self._moe_skip:  # ran with its layer's batch
+        elif i in self._moe_skip or i in self._mlp_skip:  # ran with its layer's batch / MLP block
             run = None
+        elif i in self._mlp_fused:  # fc1 + fc2 of the MLP block in one launch
+            run = lambda _ins, _i=i: self._run_mlp_fused(_i)  # noqa: E731
         if run is not None and events is not None:
             t0 = self._mark()
             run(ins)

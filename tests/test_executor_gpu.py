@@ -244,23 +244,29 @@ def test_post_norm_under_memory_cap_on_gpu(monkeypatch, model):
 
 
 @pytest.mark.timeout(300)
-def test_gpt2_every_block_matches_reference():
+@pytest.mark.parametrize("mlp_fused", [False, True])
+def test_gpt2_every_block_matches_reference(mlp_fused, monkeypatch):
     """The real GPT-2-small DAG at S = 512 (the benchmarked shapes), block by block: the residual
     stream after each of the 12 blocks (the ``layer_i_output`` groups: fc2 GEMM + bias +
     residual, with the next block's folded-LN statistics handed over) against the fp32 reference
     — an error confined to one layer's kernel cannot hide under the end-to-end tolerance."""
+    from distributed_llm_scheduler_amd.parallel import executor as exm
+
+    monkeypatch.setattr(exm, "MLP_FUSED", mlp_fused)  # fc1 + fc2 of every block as ONE launch
     S = 512
     p = runtime.plan("gpt2", world=1, seq=S, batch=1)
     store = runtime.make_store(p)
     ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=False)
+    assert len(ex._mlp_fused) == (12 if mlp_fused else 0)
     ex.step()  # weights resident and transformed
     got = {}
     orig = ex._issue_run
 
     def issue(i, ins, stats, events):
         orig(i, ins, stats, events)
-        if ins.task.endswith("_output") and ins.task.startswith("layer_"):
-            got[int(ins.task.split("_")[1])] = ex._views[ins.task].float().clone()
+        tid = ex.prog.instrs[ex._mlp_fused[i]].task if i in ex._mlp_fused else ins.task
+        if tid.endswith("_output") and tid.startswith("layer_"):
+            got[int(tid.split("_")[1])] = ex._views[tid].float().clone()
 
     ex._issue_run = issue
     ex.step()

@@ -52,7 +52,7 @@ def test_gemm_identity_asymmetric():
                                            (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2),
                                            (34, 1), (35, 1), (34, 2), (34, 3), (98, 1),
                                            (36, 1), (37, 1), (36, 2), (38, 1), (38, 2), (39, 1), (40, 1), (40, 3),
-                                           (41, 1), (41, 2), (12, 3), (31, 1)])
+                                           (41, 1), (41, 2), (12, 3), (31, 1), (42, 1)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
@@ -517,7 +517,8 @@ def test_gemm_emits_row_stats(config, splitk, N):
 @pytest.mark.parametrize("mode", ["layernorm", "rmsnorm"])
 @pytest.mark.parametrize("config,splitk,act", [(3, 1, 0), (3, 4, 1), (0, 2, 0), (8, 1, 0), (12, 2, 0), (3, 1, 4),
                                                (34, 1, 0), (34, 2, 1), (35, 1, 0),
-                                               (36, 1, 0), (37, 1, 4), (38, 1, 0), (39, 2, 0), (40, 1, 1)])
+                                               (36, 1, 0), (37, 1, 4), (38, 1, 0), (39, 2, 0), (40, 1, 1),
+                                               (42, 1, 0)])
 def test_gemm_folded_norm_external_stats(mode, config, splitk, act):
     M, N, K = 256, 1024, 2048
     x = _rand(M, K, scale=2.0, seed=110) + 0.3
@@ -593,3 +594,64 @@ def test_moe_gather_combine_post_norm():
     torch.cuda.synchronize()
     assert torch.equal(out, plain)
     _close(yn.cpu().float(), ref_n.cpu().float(), 2e-2)
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_lm_head_column_split(split, monkeypatch):
+    """The GPT-2 LM head as the DAG runs it (512 x 50257 x 768, final LayerNorm folded, row
+    statistics handed over, logits written into rows padded to 50304): one round of 256 x 256
+    tiles over the first 32,768 columns and the rest as one round of 256 x 144 tiles
+    (the ops/gemm_tuning.json col_splits mechanism; not enabled for the step, where it measured no
+    gain: profiles/r4_ab/lmhead_col_split.txt), against the fp32 reference and the unsplit launch."""
+    M, N, K = 512, 50257, 768
+    monkeypatch.setenv("DLS_COL_SPLIT", "1" if split else "0")
+    ops.tuning.table()
+    monkeypatch.setitem(ops.tuning._col_splits, ops.tuning._key(M, N, K), [(0, 32768, 13, 1), (32768, N, 42, 1)])
+    x = _rand(M, K, scale=2.0, seed=210) + 0.3
+    w = _rand(N, K, scale=0.05, seed=211)
+    nw = (1 + 0.2 * _rand(K, seed=212).float()).to(torch.bfloat16)
+    nb = _rand(K, scale=0.1, seed=213)
+    xf = x.cpu().float()
+    st = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).to(DEV)
+    wd, cs, bd = ops.derive_norm_gemm(w, nw, nb, None)
+    ob = torch.full((1, M, 50304), float("nan"), device=DEV, dtype=torch.bfloat16)
+    out = ob[:, :, :N]
+    if split:
+        assert ops.tuning.col_split(M, N, K) is not None
+    ops.linear_norm(x.view(1, M, K), wd, cs, bd, "layernorm", out=out, ext_stats=st)
+    torch.cuda.synchronize()
+    ref = ops.ref_linear(ops.ref_layernorm(x.cpu(), nw.cpu(), nb.cpu()), w.cpu()).float()
+    _close(out[0].cpu(), ref, 3e-2)
+    assert torch.isnan(ob[:, :, N:].float()).all()  # the padding columns stay untouched
+
+
+def test_mlp_fused_one_launch():
+    """The GPT-2 MLP block as ONE launch (gemm_fused.hip): folded LayerNorm-2 + fc1 + GELU, then
+    fc2 + bias + residual + the next norm's row statistics, linked by in-launch arrival counters —
+    against the fp32 reference, three launches in a row on one counter buffer (each launch resets
+    its counters), no wait ever gave up."""
+    M, H, F = 512, 768, 3072
+    assert ops.mlp_fused_ok(M, H, F, H)
+    x = _rand(M, H, scale=2.0, seed=300) + 0.2
+    w1, b1 = _rand(F, H, scale=0.04, seed=301), _rand(F, scale=0.1, seed=302)
+    w2, b2 = _rand(H, F, scale=0.02, seed=303), _rand(H, scale=0.1, seed=304)
+    nw = (1 + 0.2 * _rand(H, seed=305).float()).to(torch.bfloat16)
+    nb = _rand(H, scale=0.1, seed=306)
+    res = _rand(M, H, seed=307)
+    xf = x.cpu().float()
+    st = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).to(DEV)
+    wd, cs, bd = ops.derive_norm_gemm(w1, nw, nb, b1)
+    h = torch.empty(M, F, device=DEV, dtype=torch.bfloat16)
+    out = torch.empty(M, H, device=DEV, dtype=torch.bfloat16)
+    sync = torch.zeros(2 * M // 64 + 1, dtype=torch.int32, device=DEV)
+    for _ in range(3):
+        so = torch.zeros(M, 2, device=DEV)
+        ops.mlp_fused(x, wd, bd, cs, st, "layernorm", 1e-5, h, w2, b2, res, out, stats_out=so, sync=sync)
+    torch.cuda.synchronize()
+    hr = ops.ref_linear(ops.ref_layernorm(x.cpu(), nw.cpu(), nb.cpu()), w1.cpu(), b1.cpu(), act="gelu")
+    ref = ops.ref_linear(hr, w2.cpu(), b2.cpu(), residual=res.cpu()).float()
+    _close(h.cpu(), hr.float(), 3e-2)
+    _close(out.cpu(), ref, 3e-2)
+    of = out.cpu().float()
+    _close(so.cpu(), torch.stack([of.sum(1), (of * of).sum(1)], 1), 1e-2)
+    assert int(sync[-1]) == 0 and int(sync[:-1].abs().sum()) == 0  # no timeout; counters reset
