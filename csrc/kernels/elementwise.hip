@@ -57,7 +57,8 @@ __global__ __launch_bounds__(256) void swiglu_kernel(const bf16* __restrict__ gu
 __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restrict__ tok,
                                                         const bf16* __restrict__ wte,
                                                         const bf16* __restrict__ wpe, bf16* __restrict__ y, int M,
-                                                        int S, int H, float* __restrict__ zbuf, int zn) {
+                                                        int S, int H, float* __restrict__ zbuf, int zn,
+                                                        float* __restrict__ stats) {
   for (int i = blockIdx.x * 256 + threadIdx.x; i < zn; i += gridDim.x * 256) zbuf[i] = 0.f;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -66,6 +67,7 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
   const bf16x8* er = reinterpret_cast<const bf16x8*>(wte + (size_t)t * H);
   const bf16x8* pr = wpe ? reinterpret_cast<const bf16x8*>(wpe + (size_t)(row % S) * H) : nullptr;
   bf16x8* yr = reinterpret_cast<bf16x8*>(y + (size_t)row * H);
+  float s1 = 0.f, s2 = 0.f;
   for (int c = lane; c < H / 8; c += 64) {
     bf16x8 a = er[c];
     if (pr) {
@@ -74,6 +76,22 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int32_t* __restric
       for (int e = 0; e < 8; ++e) a[e] = f2bf(bf2f(a[e]) + bf2f(p[e]));
     }
     yr[c] = a;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = bf2f(a[e]);
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  // the row's (sum, sum of squares) for the next folded norm (the wave owns the row: plain
+  // stores into a region the zeroing above does not cover)
+  if (stats) {
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      stats[2 * row] = s1;
+      stats[2 * row + 1] = s2;
+    }
   }
 }
 
@@ -134,9 +152,9 @@ void launch_swiglu(const void* gu, void* y, int M, int F, hipStream_t s) {
 }
 
 void launch_embedding(const int32_t* tokens, const void* wte, const void* wpe, void* y, int M, int S, int H,
-                      hipStream_t s, float* zbuf, int zn) {
+                      hipStream_t s, float* zbuf, int zn, float* stats) {
   hipLaunchKernelGGL(embedding_kernel, dim3((M + 3) / 4), dim3(256), 0, s, tokens, (const bf16*)wte,
-                     (const bf16*)wpe, (bf16*)y, M, S, H, zbuf, zn);
+                     (const bf16*)wpe, (bf16*)y, M, S, H, zbuf, zn, stats);
 }
 
 void launch_rope(void* qkv, int ld, int M, int S, int n_head, int n_kv_head, int D, int k_col, const float* cos_t,

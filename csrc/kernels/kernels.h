@@ -122,7 +122,7 @@ void launch_gelu(const void* x, void* y, int64_t n, hipStream_t s);
 void launch_add(const void* a, const void* b, void* y, int64_t n, hipStream_t s);
 void launch_swiglu(const void* gu, void* y, int M, int F, hipStream_t s);  // gu [M][2F] (gate|up)
 void launch_embedding(const int32_t* tokens, const void* wte, const void* wpe, void* y, int M, int S, int H,
-                      hipStream_t s, float* zbuf = nullptr, int zn = 0);
+                      hipStream_t s, float* zbuf = nullptr, int zn = 0, float* stats = nullptr);
 // in-place rotary embedding on the q and k head slices of a packed qkv row buffer
 void launch_rope(void* qkv, int ld, int M, int S, int n_head, int n_kv_head, int D, int k_col, const float* cos_t,
                  const float* sin_t, hipStream_t s);

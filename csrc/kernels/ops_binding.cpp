@@ -371,7 +371,8 @@ void mlp_fused(const at::Tensor& x_in, const at::Tensor& w1, const c10::optional
 }
 
 at::Tensor embedding(const at::Tensor& tokens, const at::Tensor& wte, const c10::optional<at::Tensor>& wpe, int64_t S,
-                     const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& zero) {
+                     const c10::optional<at::Tensor>& out, const c10::optional<at::Tensor>& zero,
+                     const c10::optional<at::Tensor>& stats) {
   TORCH_CHECK(tokens.is_cuda() && tokens.scalar_type() == at::kInt && tokens.is_contiguous(),
               "tokens must be contiguous int32 on the GPU");
   check_bf16(wte, "wte");
@@ -392,8 +393,20 @@ at::Tensor embedding(const at::Tensor& tokens, const at::Tensor& wte, const c10:
     zb = zero->data_ptr<float>();
     zn = (int)zero->numel();
   }
+  float* st = nullptr;
+  if (stats.has_value()) {
+    TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kFloat && stats->is_contiguous() &&
+                    stats->numel() >= 2 * M,
+                "stats must be a contiguous fp32 GPU tensor of >= 2 * rows");
+    st = stats->data_ptr<float>();
+    if (zb) {  // the kernel zeroes zero[] while other workgroups write stats[]: disjoint only
+      const float* z0 = zb;
+      const float* s0 = st;
+      TORCH_CHECK(s0 + 2 * M <= z0 || z0 + zn <= s0, "stats must not overlap the zeroed buffer");
+    }
+  }
   launch_embedding(tokens.data_ptr<int32_t>(), wte.data_ptr(), wpe.has_value() ? wpe->data_ptr() : nullptr,
-                   y.data_ptr(), (int)M, (int)S, (int)H, cur_stream(), zb, zn);
+                   y.data_ptr(), (int)M, (int)S, (int)H, cur_stream(), zb, zn, st);
   return y;
 }
 
@@ -710,7 +723,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_fused", &mlp_fused);
   m.def("mlp_fused_ok", &mlp_fused_ok);
   m.def("embedding", &embedding, py::arg("tokens"), py::arg("wte"), py::arg("wpe") = py::none(), py::arg("S") = 1,
-        py::arg("out") = py::none(), py::arg("zero") = py::none());
+        py::arg("out") = py::none(), py::arg("zero") = py::none(), py::arg("stats") = py::none());
   m.def("rope_", &rope_);
   m.def("moe_router", &moe_router);
   m.def("moe_gather_combine", &moe_gather_combine, py::arg("experts"), py::arg("ptrs"), py::arg("idx"),

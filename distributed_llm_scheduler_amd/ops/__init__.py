@@ -417,10 +417,12 @@ def swiglu(gate_up, out=None):
     return out.copy_(y) if out is not None else y
 
 
-def embedding(tokens, wte, wpe=None, S=1, out=None, zero=None):
-    """``wte[tokens] (+ wpe[pos % S])``; ``zero`` (GPU fp32) is cleared by the same kernel."""
+def embedding(tokens, wte, wpe=None, S=1, out=None, zero=None, stats=None):
+    """``wte[tokens] (+ wpe[pos % S])``; ``zero`` (GPU fp32) is cleared by the same kernel;
+    ``stats`` (fp32 [rows, 2], disjoint from ``zero``) receives each output row's (sum, sum of
+    squares) for the next folded norm."""
     if _gpu(wte):
-        return ext().embedding(tokens.to(torch.int32).contiguous(), wte, wpe, int(S), out, zero)
+        return ext().embedding(tokens.to(torch.int32).contiguous(), wte, wpe, int(S), out, zero, stats)
     if zero is not None:
         zero.zero_()
     t = tokens.reshape(-1).long()
@@ -428,6 +430,9 @@ def embedding(tokens, wte, wpe=None, S=1, out=None, zero=None):
     if wpe is not None:
         y = y + wpe.float()[torch.arange(t.numel()) % S]
     y = y.to(wte.dtype)
+    if stats is not None:
+        yf = y.float()
+        stats.view(-1, 2).copy_(torch.stack([yf.sum(1), (yf * yf).sum(1)], 1))
     return out.copy_(y) if out is not None else y
 
 

@@ -125,6 +125,9 @@ HANDOFF_MAX_K = int(os.environ.get("DLS_HANDOFF_MAX_K", str(FOLD_MAX_K)))
 GUARD_BYTES, GUARD_VALUE = 4096, 0xA5  # debug-mode canary after each arena slab
 # producer GEMMs emit row statistics for the next folded norm (GPU); DLS_STATS_HANDOFF=0 disables
 STATS_HANDOFF = os.environ.get("DLS_STATS_HANDOFF", "1") != "0"
+# the embedding kernel hands layer 0's folded norm its rows' statistics too (0: that norm's GEMM
+# accumulates them in its main loop)
+EMBED_STATS = os.environ.get("DLS_EMBED_STATS", "1") != "0"
 # parameter refills on a side copy stream, hoisted to the earliest safe point (GPU), and the
 # step then runs eagerly (the branches of a captured hipGraph execute one after the other on
 # this stack, benchmarks/bench_graph_concurrency.py). "auto" (default): for planned-residency
@@ -273,10 +276,12 @@ class DAGExecutor:
         if self.gpu and STATS_HANDOFF:
             self._plan_stats_handoff()
         self._zero_in_embedding = False
+        self._zero_run = None  # the run whose embedding launch zeroes the statistics slab
         if self._stats_slab is not None:
             runs = [i for i in p.instrs if i.op == "run"]
             first = self.tasks[runs[0].group[0]] if runs else None
             self._zero_in_embedding = first is not None and first.op.kind == "embedding"
+            self._zero_run = runs[0] if self._zero_in_embedding else None
         self._plan_moe_batches()
         self._hoist: Dict[int, List[int]] = {}
         self._await: Dict[str, object] = {}  # group -> copy-stream event its first reader waits on
@@ -550,6 +555,8 @@ class DAGExecutor:
             head = grp[1] if lead_norm else grp[0]
             if head.op.kind in ("attention", "attn_sp", "swiglu_mlp"):
                 return True
+            if head.op.kind == "embedding" and len(grp) == 1:
+                return EMBED_STATS  # the embedding kernel writes its rows' statistics (a wave per row)
             # a plain GEMM group writes its output with an un-folded, non-SwiGLU GEMM
             return head.op.kind == "linear" and not lead_norm and head.op.attrs.get("act") != "swiglu"
 
@@ -570,6 +577,9 @@ class DAGExecutor:
                     need.append(src)
         if not need:
             return
+        # an embedding's statistics lead the slab: the embedding kernel zeroes the rest of it
+        # in the same launch (regions written there must not be zeroed there)
+        need.sort(key=lambda t: 0 if self.tasks[t].op.kind == "embedding" else 1)
         rows = {t: math.prod(self.tasks[t].op.out_shape[:-1]) for t in need}
         self._stats_slab = torch.zeros(sum(2 * r for r in rows.values()), dtype=torch.float32, device=self.device)
         off = 0
@@ -1079,8 +1089,12 @@ class DAGExecutor:
                 tok = tok.reshape(-1) if B == 1 else tok.contiguous().view(-1)
                 if wpe is not None:
                     wpe = wpe[c * S:(c + 1) * S]
-            zero = self._stats_slab if self._zero_in_embedding else None
-            ops.embedding(tok, self._w(W["wte"]), wpe, S, out=self._flat(out), zero=zero)
+            zero = self._stats_slab if (self._zero_in_embedding and ins is self._zero_run) else None
+            if st_out is not None and zero is not None:
+                if st_out.data_ptr() != zero.data_ptr():
+                    raise RuntimeError("an embedding's row statistics must lead the statistics slab")
+                zero = zero[st_out.numel():]
+            ops.embedding(tok, self._w(W["wte"]), wpe, S, out=self._flat(out), zero=zero, stats=st_out)
         elif k in ("layernorm", "rmsnorm") and self._pn_given == head.id:
             pass  # written by the producer of its input (_plan_post_norm)
         elif k == "layernorm":
