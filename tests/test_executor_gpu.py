@@ -280,3 +280,18 @@ def test_gpt2_every_block_matches_reference(mlp_fused, monkeypatch):
         err = (out - ref).abs().max().item()
         scale = ref.abs().max().item()
         assert err < 0.02 * scale, (i, err, scale)
+
+
+def test_replicas_share_transformed_weights_in_place():
+    """request replicas read the same weights with the same op kinds; only a weight
+    read by two KINDS of op (GPT-2's tied wte: embedding gather + LM head) gets a private
+    transformed copy (``_side``), so the folded / permuted weights stay inside the parameter arena
+    the scheduler accounts for."""
+    p = runtime.plan("mini-gpt2", world=1, seq=64, batch=1, replicas=2)
+    store = runtime.make_store(p)
+    ex = runtime.make_executor(p, 0, torch.device("cuda:0"), store, use_graph=False)
+    ex.step()
+    torch.cuda.synchronize()
+    assert set(ex._side) <= {"wte"}, sorted(ex._side)
+    for rid in ("r0/", "r1/"):
+        _check(p, ex, store, 0.03, rid)

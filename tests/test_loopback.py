@@ -147,3 +147,21 @@ def test_loopback_gpu_expert_parallel_no_host_sync():
     run = run_loopback(p, "cuda:0", steps=3, warmup=2, capture=False, store=store, sync_debug=True)
     assert all(s is not None for s in run.stats)
     _check(p, run, store, ids, 0.03)
+
+
+@gpu
+@pytest.mark.timeout(240)
+def test_loopback_gpu_mixed_issue_modes():
+    """ranks that disagree on the native runner stay in p2p step. Rank 1 cannot record
+    a runner (forced), rank 0 can: build_runner executes the recorded step on rank 0, and rank 1
+    runs one Python-loop step in its place, so their transfers still pair step by step."""
+    p, ids = _gpu_plan("pipeline", 2)
+    store = runtime.make_store(p)
+
+    def refuse_on_rank1(exs):
+        exs[1]._runner_ok = lambda: False
+
+    run = run_loopback(p, "cuda:0", steps=3, warmup=2, store=store, delay_us=50.0, before_steps=refuse_on_rank1)
+    assert run.issue_modes[0] == "runner" and run.issue_modes[1] != "runner", run.issue_modes
+    assert run.hub.outstanding() == 0
+    _check(p, run, store, ids, 0.03)
