@@ -243,6 +243,10 @@ def main():
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        visible = torch.cuda.device_count()  # (counting devices does not initialise the GPU)
+        if 0 < visible < args.gpus:
+            log(f"[bench] --gpus {args.gpus} but only {visible} GPU(s) are visible")
+            sys.exit(2)
         sys.exit(launch_ranks(args.gpus))  # one rank process per GPU, before any GPU call
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

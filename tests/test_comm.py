@@ -1,0 +1,96 @@
+"""The executor's p2p transports (parallel/comm.py): torch.distributed groups (gloo here, RCCL on
+the GPU: one ncclGroupStart/End per program point) and the single-process loopback hub with its
+FIFO pairing per (src, dst), size checks and unmatched-op timeouts."""
+import os
+import socket
+import threading
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from distributed_llm_scheduler_amd.parallel.comm import DistComm, LoopComm, loopback_groups, make_comm
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = make_comm(dist.group.WORLD)
+        assert isinstance(c, DistComm)
+        nxt, prv = (rank + 1) % world, (rank - 1) % world
+        out = torch.full((64,), float(rank))
+        got = torch.zeros(64)
+        back = torch.zeros(8)
+        # a send and two receives from different peers posted as ONE group
+        ws = c.batch([(True, out, nxt), (False, got, prv), (False, back, nxt)]) if world > 2 else \
+            c.batch([(True, out, nxt), (False, got, prv)])
+        ws2 = c.batch([(True, torch.full((8,), 10.0 + rank), prv)]) if world > 2 else []
+        for w in ws + ws2:
+            w.wait()
+        ok = bool((got == prv).all()) and (world == 2 or bool((back == 10.0 + nxt).all()))
+        q.put((rank, ok, len(ws)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_comm_batch_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_batch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in ps)
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert all(ok for _, ok, _ in res)
+    assert all(n == (3 if world > 2 else 2) for _, _, n in res)  # gloo: one work per op
+
+
+def test_loopback_fifo_pairing_and_checks():
+    g = loopback_groups(3, poison=False, timeout_s=2.0)
+    c0, c1, c2 = (LoopComm(x) for x in g)
+    a, b = torch.zeros(4), torch.zeros(4)
+    # two messages 0 -> 1 pair in posting order, whatever order the receives are waited in
+    r1, r2 = c1.irecv(a, 0), c1.irecv(b, 0)
+    s1, s2 = c0.isend(torch.ones(4), 1), c0.isend(torch.full((4,), 2.0), 1)
+    for w in (r2, r1, s1, s2):
+        w.wait()
+    assert torch.equal(a, torch.ones(4)) and torch.equal(b, torch.full((4,), 2.0))
+    assert g[0].hub.transfers == 2 and g[0].hub.outstanding() == 0
+    # a receive posted from another thread than the send completes (ranks are threads)
+    got = torch.zeros(2)
+    t = threading.Thread(target=lambda: c2.irecv(got, 1).wait())
+    t.start()
+    c1.isend(torch.tensor([5.0, 6.0]), 2).wait()
+    t.join(5)
+    assert torch.equal(got, torch.tensor([5.0, 6.0]))
+    # sizes must match (like ncclSend / ncclRecv), and an op nobody matches times out
+    c0.irecv(torch.zeros(3), 2)
+    with pytest.raises(RuntimeError, match="bytes"):
+        c2.isend(torch.zeros(5), 0)
+    lone = c1.irecv(torch.zeros(1), 2)
+    with pytest.raises(RuntimeError, match="never matched"):
+        lone.wait()
+
+
+def test_loopback_poison_marks_receive_buffers():
+    g = loopback_groups(2, poison=True)
+    buf = torch.zeros(4)
+    w = LoopComm(g[1]).irecv(buf, 0)
+    assert torch.isnan(buf).all()  # poisoned when posted, until the matching send lands
+    LoopComm(g[0]).isend(torch.arange(4.0), 1).wait()
+    w.wait()
+    assert torch.equal(buf, torch.arange(4.0))
