@@ -25,6 +25,9 @@ CASES = {
     "expert": ("tiny-mixtral", dict(placement="expert", replicas=1), ["output_projection"]),
     # the reference's experiment: ONE DAG over the nodes under its 80 % regime (bench.py capped)
     "capped_one_dag": ("tiny-gpt2", dict(scheduler="MRU_spec", regime=0.8), ["output_projection"]),
+    # capped replicas: steady-state refills of a group a peer holds come from the peer's HBM
+    # (program.plan_peer_fills, the xGMI path); the cap is a fraction of the model's parameters
+    "peer_fill": ("tiny-gpt2", dict(replicas="world", cap_frac=0.7, cost_model="bytes"), "replicas"),
 }
 
 
@@ -38,7 +41,20 @@ def _plan(case, world, seq, batch=1, gpu=False):
     if "regime" in kw:
         spec = regime_node_spec(model, kw.pop("regime"), world, batch=batch, seq=seq)
         kw.update(cap_gb=[m for m, _ in spec], node_speeds=[v for _, v in spec], cost_model="reference")
+    if kw.get("replicas") == "world":
+        kw["replicas"] = world
+    if "cap_frac" in kw:
+        total = sum(runtime.plan(model, world=1, seq=seq, batch=batch).param_bytes.values())
+        kw["cap_gb"] = kw.pop("cap_frac") * total / 1e9
+    if ids == "replicas":
+        ids = [f"r{k}/output_projection" for k in range(world)]
     return runtime.plan(model, world=world, seq=seq, batch=batch, **kw), ids
+
+
+def _p2p_work(p):
+    """Cross-rank traffic the plan carries: DAG edges plus parameter groups filled from a peer."""
+    peer = sum(1 for pr in p.programs for i in pr.instrs if i.op == "load" and i.peer >= 0)
+    return p.stats["cross_gpu_edges"] + peer
 
 
 def _logits(p, run, ids):
@@ -76,10 +92,12 @@ def _check(p, run, store, ids, tol):
 @pytest.mark.parametrize("cpu_runner", [False, True])
 def test_loopback_cpu(case, world, cpu_runner):
     p, ids = _plan(case, world, 32 if case == "sequence" else 16)
-    assert p.stats["cross_gpu_edges"] > 0 and p.completed == p.total
+    assert _p2p_work(p) > 0 and p.completed == p.total
     store = runtime.make_store(p)
     run = run_loopback(p, "cpu", steps=2, warmup=2, store=store, cpu_runner=cpu_runner)
     assert run.hub.transfers > 0 and run.hub.outstanding() == 0
+    if case == "peer_fill":
+        assert sum(s.peer_fills for s in run.stats) > 0, "no parameter group came from a peer"
     if cpu_runner:
         assert all(m == "runner" for m in run.issue_modes)
     _check(p, run, store, ids, 0.03)
@@ -102,12 +120,14 @@ def test_loopback_gpu(case, world):
     runner on every rank, 50 us of delay in front of every transfer, poisoned receive buffers —
     the logits match fp32."""
     p, ids = _gpu_plan(case, world)
-    assert p.stats["cross_gpu_edges"] > 0
+    assert _p2p_work(p) > 0
     store = runtime.make_store(p)
     run = run_loopback(p, "cuda:0", steps=3, warmup=2, store=store, delay_us=50.0)
     assert run.hub.transfers > 0 and run.hub.outstanding() == 0
     comm_ranks = [r for r in range(world) if p.programs[r].has_comm]
     assert comm_ranks and all(run.issue_modes[r] == "runner" for r in comm_ranks), run.issue_modes
+    if case == "peer_fill":
+        assert sum(s.peer_fills for s in run.stats) > 0, "no parameter group came from a peer"
     _check(p, run, store, ids, 0.03)
 
 
