@@ -520,7 +520,8 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
 // APOL: the A rows' DMA cache policy (joint rings; mainloop_joint); PUB: the output tile is
 // stored write-through (sc1) so workgroups of the SAME launch on other XCDs can read it after
 // an agent-scope arrival count (gemm_fused.hip) — both 0 / false in every ordinary launch
-template <class C, int LN, int WPOL = 0, bool SKIP = false, bool GATHER = false, int APOL = 0, bool PUB = false>
+template <class C, int LN, int WPOL = 0, bool SKIP = false, bool GATHER = false, int APOL = 0, bool PUB = false,
+          int SPOL = 0>
 __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                           const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp, int ldc,
                                           const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
@@ -869,10 +870,11 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(o[e]) + bf2f(r8[e]));
         }
-        if constexpr (PUB) {  // write-through: the row segment leaves the XCD's L2 for memory
+        if constexpr (PUB || SPOL != 0) {  // PUB: write-through, the row segment leaves the XCD's
+          // L2 for memory; SPOL: the store's cache policy (nt: streaming output)
           const auto rs = __builtin_amdgcn_make_buffer_rsrc(Cp, 0, 0x7fffffff, 0x00020000);
           __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&o), rs,
-                                                 (int)(((size_t)row * ldc + col) * 2), 0, 16);
+                                                 (int)(((size_t)row * ldc + col) * 2), 0, PUB ? 16 : SPOL);
         } else {
           *reinterpret_cast<bf16x8*>(Cp + (size_t)row * ldc + col) = o;
         }
@@ -913,7 +915,9 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 
 // LN / RANGED are compile-time switches: a kernel instance carries only the epilogue and
 // tile walk it needs (the folded-norm statistics and the row-range loop cost registers).
-template <class C, int LN, int RANGED>
+// POL (plain tiles only): streaming (nt) cache policy of the weight DMA (bit 0, split rings)
+// and of the output stores (bit 1) — GemmArgs::stream_pol
+template <class C, int LN, int RANGED, int POL = 0>
 __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
                                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
                                                          int ldc, const bf16* __restrict__ bias,
@@ -975,8 +979,9 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   const int ks = bid / ntile, tile = bid % ntile;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
   if constexpr (!RANGED) {
-    glds_tile<C, LN>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn,
-                     ln_colsum, (LN || ep.ext_stats) ? ln_mode : 0, ln_eps, ep);
+    glds_tile<C, LN, (POL & 1) ? kPolStream : 0, false, false, 0, false, (POL & 2) ? kPolStream : 0>(
+        smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn, ln_colsum,
+        (LN || ep.ext_stats) ? ln_mode : 0, ln_eps, ep);
     return;
   }
   // device-side row range (MoE expert): the host launched ONE tile row (tiles_m == 1) — no
@@ -1025,8 +1030,8 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
   const int kslice = a.K / splitk;
   const int total = tiles_m * tiles_n * splitk;
   dim3 grid(total), block(C::T);
-#define DLS_K(LN_, RG_)                                                                                           \
-  hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
+#define DLS_K(LN_, RG_, ...)                                                                                      \
+  hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_, ##__VA_ARGS__>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
                      a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
                      a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows, ep)
   const bool ln_in = ln_mode != 0 && !a.ext_stats;
@@ -1043,7 +1048,16 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     }
   } else if (ln_in) {
     if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) DLS_K(1, 0);  // 256x256: no registers left for it
-  } else DLS_K(0, 0);
+  } else {
+    int pol = 0;
+    if constexpr (C::BXS > 0 && !C::RING) pol = a.stream_pol & 3;  // split rings: own kernel per policy
+    switch (pol) {
+      case 1: DLS_K(0, 0, 1); break;
+      case 2: DLS_K(0, 0, 2); break;
+      case 3: DLS_K(0, 0, 3); break;
+      default: DLS_K(0, 0);
+    }
+  }
 #undef DLS_K
   if (splitk > 1 && !ep.tile_sem) return glds_reduce(a, splitk, ws, s, ln_colsum, ln_mode, ln_eps, rows, ep);
   return false;

@@ -50,6 +50,11 @@ struct GemmArgs {
   int norm_mode = 0;
   float norm_eps = 1e-5f;
   int ldn = 0;
+  // cache policy of a plain split-ring launch (LN 0): bit 0 the weight DMA streams (nt), bit 1
+  // the output stores stream (nt) — for a weight read once per step and a write-once output
+  // (the LM head's 77 MB weight and 51 MB of logits) that should not displace the layer
+  // weights from the Infinity Cache
+  int stream_pol = 0;
 };
 
 // epilogue extras carried down to the tile code

@@ -70,7 +70,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
                 int64_t rope_D, int64_t rope_cols, const c10::optional<at::Tensor>& stats_out,
                 const c10::optional<at::Tensor>& ext_stats, const c10::optional<at::Tensor>& norm_out,
                 const c10::optional<at::Tensor>& norm_w, const c10::optional<at::Tensor>& norm_b, int64_t norm_mode,
-                double norm_eps) {
+                double norm_eps, int64_t stream_pol) {
   check_bf16(a_in, "A");
   check_bf16(w, "W");
   at::Tensor a = as2d(a_in);
@@ -119,6 +119,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
   GemmArgs g{a.data_ptr(), (int)a.stride(0), w.data_ptr(), (int)w.stride(0), c.data_ptr(), (int)c.stride(0),
              bptr, rptr, ldr, (int)M, (int)N, (int)K, (int)act, (float)alpha, -1,
              (compact_rows && rows.has_value()) ? (int)c.size(0) : 0};
+  g.stream_pol = (int)stream_pol;
   // post-norm for the next (unfolded) norm: a split-K launch writes it from its row-owning
   // reduce; every other path runs the norm kernel on the output right after the GEMM
   at::Tensor y_n;
@@ -699,7 +700,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rope_sin") = py::none(), py::arg("rope_S") = 1, py::arg("rope_D") = 2, py::arg("rope_cols") = 0,
         py::arg("stats_out") = py::none(), py::arg("ext_stats") = py::none(), py::arg("norm_out") = py::none(),
         py::arg("norm_w") = py::none(), py::arg("norm_b") = py::none(), py::arg("norm_mode") = 0,
-        py::arg("norm_eps") = 1e-5);
+        py::arg("norm_eps") = 1e-5, py::arg("stream_pol") = 0);
   m.attr("REGSTAGE") = kRegStage;
   m.attr("PERSIST") = kGemmPersist;
   m.def("gemm_pick_config", &gemm_pick_config);

@@ -26,6 +26,13 @@ from . import tuning
 ACT = {None: 0, "none": 0, "gelu": 1, "gelu_tanh": 1, "silu": 2, "relu": 3, "swiglu": 4}
 SWIGLU = 4
 SWIGLU_BLOCK = 16  # gate/up interleave granularity of a SwiGLU-epilogue weight (csrc common.h)
+# cache policy of vocabulary-sized projections (the LM head: a weight read once per step and a
+# write-once logits tensor; GemmArgs::stream_pol): bit 0 weight DMA nt, bit 1 output stores nt.
+# Streaming both keeps GPT-2's 170 MB of layer weights resident in the 256 MB Infinity Cache
+# from step to step (its 77 MB LM-head weight and 51 MB of logits otherwise push them out):
+# step 0.639 vs 0.689 ms (profiles/r4_ab/lmhead_stream_policy.txt)
+LMHEAD_POL = int(os.environ.get("DLS_LMHEAD_POL", "3"))
+LMHEAD_MIN_N = 32000
 
 _lock = threading.Lock()
 _ext = None
@@ -317,8 +324,10 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
             cfg = next((int(c) for c, _ in tuning.runner_ups(M, N, K, tuning.tag(a), 8)
                         if 0 <= c < tuning.REGSTAGE and tuning.kstep(c) == 64), -1)
     rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
+    pol = LMHEAD_POL if N >= LMHEAD_MIN_N else 0
     y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, sk, colsum,
-                   m, float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols), None, ext_stats)
+                   m, float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols), None, ext_stats,
+                   stream_pol=pol)
     return y.view(shp) if out is None else out
 
 

@@ -625,6 +625,48 @@ def test_lm_head_column_split(split, monkeypatch):
     assert torch.isnan(ob[:, :, N:].float()).all()  # the padding columns stay untouched
 
 
+@pytest.mark.parametrize("pol", [1, 2, 3])
+def test_lm_head_stream_policy(pol, monkeypatch):
+    """The LM head with streaming (nt) cache policies (GemmArgs::stream_pol: bit 0 the weight
+    DMA, bit 1 the logits stores; ops.LMHEAD_POL) computes exactly what the default policy
+    does, and matches the fp32 reference."""
+    M, N, K = 512, 50257, 768
+    x = _rand(M, K, scale=2.0, seed=220) + 0.3
+    w = _rand(N, K, scale=0.05, seed=221)
+    nw = (1 + 0.2 * _rand(K, seed=222).float()).to(torch.bfloat16)
+    nb = _rand(K, scale=0.1, seed=223)
+    xf = x.cpu().float()
+    st = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).to(DEV)
+    wd, cs, bd = ops.derive_norm_gemm(w, nw, nb, None)
+    outs = {}
+    for p_ in (0, pol):
+        monkeypatch.setattr(ops, "LMHEAD_POL", p_)
+        ob = torch.full((1, M, 50304), float("nan"), device=DEV, dtype=torch.bfloat16)
+        ops.linear_norm(x.view(1, M, K), wd, cs, bd, "layernorm", out=ob[:, :, :N], ext_stats=st)
+        torch.cuda.synchronize()
+        assert torch.isnan(ob[:, :, N:].float()).all()
+        outs[p_] = ob[0, :, :N].cpu()
+    assert torch.equal(outs[0], outs[pol])
+    ref = ops.ref_linear(ops.ref_layernorm(x.cpu(), nw.cpu(), nb.cpu()), w.cpu()).float()
+    _close(outs[pol], ref, 3e-2)
+
+
+@pytest.mark.parametrize("config", [12, 14, 31])
+def test_gemm_stream_policy_plain(config):
+    """stream_pol on plain split-ring GEMMs (bias + residual epilogue) is bit-identical to the
+    default policy."""
+    M, N, K = 384, 1024, 512
+    x, w = _rand(M, K, seed=230), _rand(N, K, scale=0.05, seed=231)
+    b, r = _rand(N, scale=0.1, seed=232), _rand(M, N, seed=233)
+    e = ops.ext()
+    ys = [e.gemm(x, w, b, r, 0, 1.0, None, config, 1, stream_pol=p_) for p_ in (0, 1, 2, 3)]
+    torch.cuda.synchronize()
+    for y in ys[1:]:
+        assert torch.equal(ys[0], y)
+    ref = ops.ref_linear(x.cpu(), w.cpu(), b.cpu()).float() + r.cpu().float()
+    _close(ys[3].cpu(), ref, 2e-2)
+
+
 def test_mlp_fused_one_launch():
     """The GPT-2 MLP block as ONE launch (gemm_fused.hip): folded LayerNorm-2 + fc1 + GELU, then
     fc2 + bias + residual + the next norm's row statistics, linked by in-launch arrival counters —
