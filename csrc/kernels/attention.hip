@@ -88,7 +88,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
                                                        const bf16* __restrict__ Kp, int ldk,
                                                        const bf16* __restrict__ Vp, int ldv, bf16* __restrict__ O,
                                                        int ldo, int S, int n_head, int n_kv_head, float scale_log2,
-                                                       int causal, int n_qtiles, int Sq, int q_off) {
+                                                       int causal, int n_qtiles, int Sq, int q_off, int wt) {
   using C = AttnCfg<D, NW, ST, KS>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave_id = tid >> 6;
@@ -274,12 +274,19 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
   if (my_q < Sq) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     bf16* orow = O + (qtok0 + my_q) * ldo + h * D;
+    // wt: write-through (sc1) stores — the tile leaves the XCD's L2 as it is written, so the
+    // kernel boundary has no dirty lines of it to write back (AttnArgs::store_wt)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(O, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int dn = 0; dn < C::ND; ++dn) {
       bf16x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dn][i] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 16 * dn + 4 * g) = v;
+      if (wt)
+        __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<const u32x2*>(&v), rs,
+                                              (int)(((qtok0 + my_q) * ldo + h * D + 16 * dn + 4 * g) * 2), 0, 16);
+      else
+        *reinterpret_cast<bf16x4*>(orow + 16 * dn + 4 * g) = v;
     }
   }
 }
@@ -295,7 +302,7 @@ static void launch_attn(const AttnArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((attn_fwd_kernel<D, NW, ST, KS>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
                      static_cast<const bf16*>(a.k), a.ldk, static_cast<const bf16*>(a.v), a.ldv,
                      static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq, Sq,
-                     a.Sq > 0 ? a.q_off : 0);
+                     a.Sq > 0 ? a.q_off : 0, a.store_wt);
 }
 
 template <int D>

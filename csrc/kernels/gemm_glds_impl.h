@@ -231,7 +231,7 @@ __device__ __forceinline__ void mma_tile(const bf16x8* sA, const bf16x8* sB, int
 // null check in every launch's prologue cost the GPT-2 GEMMs ~5 %.
 // APOL: cache policy of the A rows' DMA (sc1 = 16: A was written in this launch by other
 // workgroups' write-through stores — gemm_fused.hip; every other launch keeps 0)
-template <class C, bool GATHER = false, int APOL = 0>
+template <class C, bool GATHER = false, int APOL = 0, int WPOL = 0>
 __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                                const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                                int kbeg, int nk, int lane, int wave, int kgrp, int wm, int wn,
@@ -268,12 +268,14 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
     bf16x8* stage = smem + (kt % C::STAGES) * C::STAGE;
 #pragma unroll
     for (int j = 0; j < C::PW; ++j) {
-      if constexpr (APOL != 0) {
-        if (is_a[j]) {
+      if constexpr (APOL != 0 || WPOL != 0) {
+        if (is_a[j])
           __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * (C::BK * C::KG)),
                                            (__attribute__((address_space(3))) void*)(stage + dst[j]), 16, 0, APOL);
-          continue;
-        }
+        else
+          __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * (C::BK * C::KG)),
+                                           (__attribute__((address_space(3))) void*)(stage + dst[j]), 16, 0, WPOL);
+        continue;
       }
       __builtin_amdgcn_global_load_lds((const void*)(src[j] + kt * (C::BK * C::KG)),
                                        (__attribute__((address_space(3))) void*)(stage + dst[j]), 16, 0, 0);
@@ -443,6 +445,7 @@ __device__ __forceinline__ void mainloop_ring(bf16x8* smem, const bf16* __restri
 }
 
 constexpr int kPolStream = 2;  // gfx950 CPol NT (streaming) bit of the DMA's aux operand
+constexpr int kPolWT = 16;     // sc1: write-through (the line leaves the XCD's L2 at the store)
 
 // Split rings (BXS > 0): issue order B0 [A0 B1] [A1 B2] ... — iteration t issues
 // A(t + SA - 1) then B(t + SB - 1). Waiting for A(t) then leaves a = min(SA-2, nk-1-t)
@@ -556,7 +559,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
     mainloop_split<C, WPOL, SKIP, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
                                   st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), arows);
   else
-    mainloop_joint<C, GATHER, APOL>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc,
+    mainloop_joint<C, GATHER, APOL, WPOL>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, kgrp, wm, wn, ln_acc, acc,
                                     st_s, st_q, arows);
   DLS_STAMP(1)
   if constexpr (C::KG > 1) {
@@ -979,7 +982,8 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
   const int ks = bid / ntile, tile = bid % ntile;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
   if constexpr (!RANGED) {
-    glds_tile<C, LN, (POL & 1) ? kPolStream : 0, false, false, 0, false, (POL & 2) ? kPolStream : 0>(
+    glds_tile<C, LN, (POL & 1) ? kPolStream : 0, false, false, 0, false,
+              ((POL & 2) ? kPolStream : 0) | ((POL & 4) ? kPolWT : 0)>(
         smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn, ln_colsum,
         (LN || ep.ext_stats) ? ln_mode : 0, ln_eps, ep);
     return;
@@ -1050,11 +1054,13 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) DLS_K(1, 0);  // 256x256: no registers left for it
   } else {
     int pol = 0;
-    if constexpr (C::BXS > 0 && !C::RING) pol = a.stream_pol & 3;  // split rings: own kernel per policy
+    if constexpr (!C::RING) pol = a.stream_pol & 7;  // own kernel per policy (not the ring main loop)
     switch (pol) {
       case 1: DLS_K(0, 0, 1); break;
       case 2: DLS_K(0, 0, 2); break;
       case 3: DLS_K(0, 0, 3); break;
+      case 4: DLS_K(0, 0, 4); break;
+      case 5: DLS_K(0, 0, 5); break;
       default: DLS_K(0, 0);
     }
   }

@@ -33,6 +33,21 @@ SWIGLU_BLOCK = 16  # gate/up interleave granularity of a SwiGLU-epilogue weight 
 # step 0.639 vs 0.689 ms (profiles/r4_ab/lmhead_stream_policy.txt)
 LMHEAD_POL = int(os.environ.get("DLS_LMHEAD_POL", "3"))
 LMHEAD_MIN_N = 32000
+# weights of at least this many MB DMA'd with the nt policy (0: off) — for models whose weights
+# stream from HBM every step anyway (A/B knob)
+WEIGHT_NT_MB = float(os.environ.get("DLS_WEIGHT_NT_MB", "0"))
+# cache policy bits of every other GEMM launch (A/B knob): 2 output stores nt, 4 output stores
+# write-through (sc1: nothing left dirty in the XCD's L2 at the kernel boundary)
+ACT_POL = int(os.environ.get("DLS_ACT_POL", "0"))
+# attention output stores write-through (A/B knob)
+ATTN_WT = int(os.environ.get("DLS_ATTN_WT", "0"))
+
+
+def _stream_pol(N: int, K: int) -> int:
+    pol = LMHEAD_POL if N >= LMHEAD_MIN_N else ACT_POL
+    if WEIGHT_NT_MB > 0 and N * K * 2 >= WEIGHT_NT_MB * 1e6:
+        pol |= 1
+    return pol
 
 _lock = threading.Lock()
 _ext = None
@@ -254,6 +269,7 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
         rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
         y = ext().gemm(x, w, bias, residual, a, float(alpha), out, cfg, sk, None, 0, 1e-5, rows, bool(compact),
                        rc, rs_, int(rS), int(rD), int(rcols), stats_out, None,
+                       stream_pol=_stream_pol(w.shape[0], w.shape[1]) if rows is None else 0,
                        **(_post_norm_args(post_norm) if post_norm is not None else {}))
         return y.view(shp) if out is None else out
     if rows is not None:
@@ -324,7 +340,7 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
             cfg = next((int(c) for c, _ in tuning.runner_ups(M, N, K, tuning.tag(a), 8)
                         if 0 <= c < tuning.REGSTAGE and tuning.kstep(c) == 64), -1)
     rc, rs_, rS, rD, rcols = rope if rope is not None else (None, None, 1, 2, 0)
-    pol = LMHEAD_POL if N >= LMHEAD_MIN_N else 0
+    pol = _stream_pol(N, K)
     y = ext().gemm(x, w_derived, bias_derived, residual, a, 1.0, out, cfg if cfg < tuning.REGSTAGE else -1, sk, colsum,
                    m, float(eps), None, False, rc, rs_, int(rS), int(rD), int(rcols), None, ext_stats,
                    stream_pol=pol)
@@ -395,7 +411,7 @@ def attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=Non
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
     if _gpu(q):
         return ext().attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, float(scale), out, 0,
-                               int(Sq or 0), int(q_off))
+                               int(Sq or 0), int(q_off), int(ATTN_WT))
     y = ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, scale, Sq=Sq, q_off=q_off)
     if out is not None:
         out.copy_(y)
