@@ -89,6 +89,13 @@ def regime_cap_gb(model, regime, batch, seq, cost_model) -> float:
     return round(need * regime, 6)
 
 
+def _cache_policy() -> dict:
+    """The cache policies the step's kernels ran with (ops: DLS_LMHEAD_POL / DLS_ACT_POL /
+    DLS_ATTN_WT): stream_pol bits 1 weight DMA nt, 2 output stores nt, 4 write-through."""
+    from distributed_llm_scheduler_amd import ops
+    return {"lm_head": ops.LMHEAD_POL, "gemm": ops.ACT_POL, "attention_write_through": bool(ops.ATTN_WT)}
+
+
 def launch_ranks(n: int) -> int:
     """``python bench.py --gpus N`` without a launcher: start N rank processes of this script
     (fresh children — nothing here has touched the GPU), one per GPU, rendezvous on 127.0.0.1;
@@ -330,6 +337,7 @@ def main():
             "per_rank_ms": head["per_rank_ms"],
             "hip_graph": head["hip_graph"],
             "issue_mode": head["issue_mode"],
+            "cache_policy": _cache_policy(),
             "weights": "random-init",
             "baseline_note": "vs_baseline is null: the reference only simulates (abstract seconds from per-task "
                              "constants, dependency-free makespan; BASELINE.md), so it has no wall-clock number in "

@@ -26,6 +26,29 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+// Vector stores with an explicit cache policy (aux bits: 2 nt, 16 sc1 = write-through) at a
+// per-lane byte offset from a workgroup-uniform base (the buffer resource lives in SGPRs).
+// Write-through leaves no dirty line of the output in the XCD's L2 for the kernel boundary to
+// write back. POL 0: a plain store.
+template <int POL>
+__device__ __forceinline__ void store16_pol(void* base, size_t off, u32x4 v) {
+  if constexpr (POL == 0) {
+    *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(base) + off) = v;
+  } else {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, POL);
+  }
+}
+template <int POL>
+__device__ __forceinline__ void store8_pol(void* base, size_t off, u32x2 v) {
+  if constexpr (POL == 0) {
+    *reinterpret_cast<u32x2*>(reinterpret_cast<char*>(base) + off) = v;
+  } else {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, (int)off, 0, POL);
+  }
+}
+
 #define DLS_WAVE 64
 
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }

@@ -112,7 +112,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
         }
       }
     }
-    *reinterpret_cast<bf16x8*>(C + (size_t)(compact_rows ? m - r0 : m) * ldc + c) = o;
+    const size_t off = ((size_t)(compact_rows ? m - r0 : m) * ldc + c) * 2;
+    if (ep.w_stream & 4) store16_pol<16>(C, off, *reinterpret_cast<const u32x4*>(&o));
+    else store16_pol<0>(C, off, *reinterpret_cast<const u32x4*>(&o));
   }
 }
 
@@ -150,7 +152,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_rows_kernel(const float* __
       s1 += y;
       s2 += y * y;
     }
-    *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + c) = o;
+    if (ep.w_stream & 4) store16_pol<16>(C, ((size_t)m * ldc + c) * 2, *reinterpret_cast<const u32x4*>(&o));
+    else store16_pol<0>(C, ((size_t)m * ldc + c) * 2, *reinterpret_cast<const u32x4*>(&o));
   }
   s1 = wave_sum(s1);
   s2 = wave_sum(s2);
@@ -236,7 +239,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_norm_kernel(const float* __
       y[u][e] = c < N ? bf2f(o[e]) : 0.f;
       s1 += y[u][e];
     }
-    if (c < N) *reinterpret_cast<bf16x8*>(C + (size_t)m * ldc + c) = o;
+    if (c < N) {
+      if (ep.w_stream & 4) store16_pol<16>(C, ((size_t)m * ldc + c) * 2, *reinterpret_cast<const u32x4*>(&o));
+      else store16_pol<0>(C, ((size_t)m * ldc + c) * 2, *reinterpret_cast<const u32x4*>(&o));
+    }
   }
   bf16x8 wv[VPT], bv[VPT];  // the norm's weights, requested before the two reductions
 #pragma unroll
@@ -272,7 +278,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_norm_kernel(const float* __
       if (nb) t += bf2f(bv[u][e]);
       o[e] = f2bf(t);
     }
-    *reinterpret_cast<bf16x8*>(Y + (size_t)m * ldy + c) = o;
+    if (ep.w_stream & 4) store16_pol<16>(Y, ((size_t)m * ldy + c) * 2, *reinterpret_cast<const u32x4*>(&o));
+    else store16_pol<0>(Y, ((size_t)m * ldy + c) * 2, *reinterpret_cast<const u32x4*>(&o));
   }
 }
 

@@ -710,7 +710,10 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
       for (int j = 0; j < C::FN; ++j) {
         const int col = n0 + wn * C::WTN + j * 16 + g4;
         if (N % 4 == 0 && col + 3 < N) {
-          *reinterpret_cast<f32x4*>(P + (size_t)row * N + col) = acc[i][j];
+          const f32x4 v = acc[i][j];
+          store16_pol<SPOL>(P, ((size_t)row * N + col) * 4,
+                            u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                  __float_as_uint(v[3])});
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -760,7 +763,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
           o[e] = f2bf(silu(g + bg[e]) * (u + bu[e]));
         }
         if (vec_ok && ocol + 3 < NO) {
-          *reinterpret_cast<bf16x4*>(Cp + (size_t)row * ldc + ocol) = o;
+          store8_pol<SPOL>(Cp, ((size_t)row * ldc + ocol) * 2, *reinterpret_cast<const u32x2*>(&o));
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -1028,7 +1031,9 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     return (e && *e ? std::atoi(e) : 64) * 1024;
   }();
   const bool fixup = splitk > 1 && !rows && (splitk - 1) * C::BM * C::BN * 4 <= fixup_max;
-  const Epi ep{a.rope, a.stats_out, a.ext_stats, fixup ? a.tile_sem : nullptr};
+  // ep.w_stream carries the store policy to the split-K reduce kernels (grouped launches alone
+  // read it as the weight policy)
+  const Epi ep{a.rope, a.stats_out, a.ext_stats, fixup ? a.tile_sem : nullptr, nullptr, nullptr, a.stream_pol & 4};
   static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
   const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;

@@ -36,9 +36,12 @@ LMHEAD_MIN_N = 32000
 # weights of at least this many MB DMA'd with the nt policy (0: off) — for models whose weights
 # stream from HBM every step anyway (A/B knob)
 WEIGHT_NT_MB = float(os.environ.get("DLS_WEIGHT_NT_MB", "0"))
-# cache policy bits of every other GEMM launch (A/B knob): 2 output stores nt, 4 output stores
-# write-through (sc1: nothing left dirty in the XCD's L2 at the kernel boundary)
-ACT_POL = int(os.environ.get("DLS_ACT_POL", "0"))
+# cache policy bits of every other GEMM launch: 2 output stores nt, 4 output stores
+# write-through (sc1) — bf16 outputs, split-K partial slabs and their reduce kernels' outputs
+# leave the XCD's L2 as they are written, so the kernel boundary has no dirty lines to write
+# back: GPT-2 0.620 vs 0.640 ms, Llama-3-8B 9.46 vs 9.49 ms (profiles/r4_ab/write_through.txt);
+# nt output stores cost GPT-2 5 %
+ACT_POL = int(os.environ.get("DLS_ACT_POL", "4"))
 # attention output stores write-through (A/B knob)
 ATTN_WT = int(os.environ.get("DLS_ATTN_WT", "0"))
 

@@ -651,20 +651,50 @@ def test_lm_head_stream_policy(pol, monkeypatch):
     _close(outs[pol], ref, 3e-2)
 
 
-@pytest.mark.parametrize("config", [12, 14, 31])
+@pytest.mark.parametrize("config", [12, 14, 17, 25, 27, 31, 38])
 def test_gemm_stream_policy_plain(config):
-    """stream_pol on plain split-ring GEMMs (bias + residual epilogue) is bit-identical to the
+    """stream_pol on plain GEMMs, split-ring and joint-ring configs incl. K groups (bias +
+    residual epilogue): weight DMA nt, output stores nt or write-through — bit-identical to the
     default policy."""
     M, N, K = 384, 1024, 512
     x, w = _rand(M, K, seed=230), _rand(N, K, scale=0.05, seed=231)
     b, r = _rand(N, scale=0.1, seed=232), _rand(M, N, seed=233)
     e = ops.ext()
-    ys = [e.gemm(x, w, b, r, 0, 1.0, None, config, 1, stream_pol=p_) for p_ in (0, 1, 2, 3)]
+    ys = [e.gemm(x, w, b, r, 0, 1.0, None, config, 1, stream_pol=p_) for p_ in (0, 1, 2, 3, 4, 5)]
     torch.cuda.synchronize()
     for y in ys[1:]:
         assert torch.equal(ys[0], y)
     ref = ops.ref_linear(x.cpu(), w.cpu(), b.cpu()).float() + r.cpu().float()
     _close(ys[3].cpu(), ref, 2e-2)
+
+
+@pytest.mark.parametrize("config,splitk,act", [(0, 2, 0), (0, 4, 0), (14, 4, 0), (12, 1, 4), (33, 1, 4)])
+def test_gemm_write_through_splitk_swiglu(config, splitk, act):
+    """Write-through stores (stream_pol bit 4) on split-K partial slabs + their reduce kernel and
+    on the SwiGLU epilogue: bit-identical to the default stores."""
+    M, N, K = 256, 1024, 1024
+    x, w = _rand(M, K, seed=250), _rand(N, K, scale=0.05, seed=251)
+    if act == 4:
+        w = ops.interleave_gate_up(w)
+    e = ops.ext()
+    ys = [e.gemm(x, w, None, None, act, 1.0, None, config, splitk, stream_pol=p_) for p_ in (0, 4)]
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1])
+
+
+@pytest.mark.parametrize("S,n_head,n_kv,D", [(512, 12, 12, 64), (512, 32, 8, 128)])
+def test_attention_write_through_stores(S, n_head, n_kv, D):
+    """Attention with write-through (sc1) output stores writes exactly what the default
+    stores write."""
+    B = 1
+    q = _rand(B * S, n_head * D, seed=240)
+    k = _rand(B * S, n_kv * D, seed=241)
+    v = _rand(B * S, n_kv * D, seed=242)
+    e = ops.ext()
+    o0 = e.attention(q, k, v, B, S, n_head, n_kv, D, True, 1.0 / D ** 0.5, None, 0, 0, 0, 0)
+    o1 = e.attention(q, k, v, B, S, n_head, n_kv, D, True, 1.0 / D ** 0.5, None, 0, 0, 0, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(o0, o1)
 
 
 def test_mlp_fused_one_launch():
