@@ -9,6 +9,7 @@
 #   prof   MODEL [ARGS]   rocprofv3 kernel trace + per-dispatch breakdown of MODEL's step
 #   pmc    COUNTERS CMD   one rocprofv3 --pmc pass (<= the per-block counter limits) over CMD
 #   ab     VAR A B [ARGS] alternating bench runs under two values of an environment variable
+#   sweep  VAR "V1 V2 .." [ARGS]  bench runs under each value in turn, ROUNDS passes
 #   trees  ALT [ARGS]     alternating bench runs of another built source tree ALT against this one
 #   tables "T1 T2[@VAR=V]" [ARGS]  alternating bench runs under GEMM tuning tables (DLS_GEMM_TUNING)
 #   retune MODEL          exhaustive in-DAG GEMM refinement (benchmarks/refine_dag.py), then an A/B
@@ -72,6 +73,16 @@ case "$job" in
       for v in "$a" "$b"; do
         env "$var=$v" timeout -k 10 300 python bench.py --steps 200 --warmup 10 --no-extras "$@" > $O/ab.json 2> $O/ab.err || { tail -5 $O/ab.err; exit 3; }
         echo "$var=$v $(ms $O/ab.json)"
+      done
+    done
+    ;;
+  sweep)
+    var="$1"; vals="$2"; shift 2
+    for i in $(seq ${ROUNDS:-2}); do
+      for v in $vals; do
+        env "$var=$v" timeout -k 10 300 python bench.py --steps 200 --warmup 10 --no-extras "$@" > $O/sw.json 2> $O/sw.err || { tail -5 $O/sw.err; exit 3; }
+        echo "$var=$v $(ms $O/sw.json)" | tee -a $O/sweep.txt > /dev/null
+        echo "$var=$v $(ms $O/sw.json)"
       done
     done
     ;;

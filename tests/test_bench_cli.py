@@ -45,6 +45,9 @@ def test_bench_single_process():
     lines = _run([sys.executable, "bench.py", "--gpus", "1", *ARGS])
     assert len(lines) == 1
     _check(lines[0], 1)
+    # the cache policies the step's kernels ran with (defaults: LM head weight + logits nt,
+    # every other GEMM write-through)
+    assert lines[0]["cache_policy"] == {"lm_head": 3, "gemm": 4, "attention_write_through": False}
 
 
 @pytest.mark.timeout(300)

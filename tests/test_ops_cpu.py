@@ -73,3 +73,19 @@ def test_tuning_model_overrides(tmp_path, monkeypatch):
     doc = json.loads(path.read_text())
     assert doc["gemm"]["512x6144x4096"] == [38, 1]
     assert doc["model_overrides"]["mixtral-8x7b"]["512x6144x4096"] == [14, 4]
+
+
+def test_stream_policy_selection(monkeypatch):
+    """Cache policy per GEMM (ops._stream_pol): vocabulary-sized projections (the LM head) get
+    the LM-head policy, every other GEMM the activation policy, plus weight-nt above the size
+    threshold when one is set."""
+    from distributed_llm_scheduler_amd import ops
+    monkeypatch.setattr(ops, "LMHEAD_POL", 3)
+    monkeypatch.setattr(ops, "ACT_POL", 4)
+    monkeypatch.setattr(ops, "WEIGHT_NT_MB", 0.0)
+    assert ops._stream_pol(50257, 768) == 3
+    assert ops._stream_pol(128256, 4096) == 3
+    assert ops._stream_pol(2304, 768) == 4
+    monkeypatch.setattr(ops, "WEIGHT_NT_MB", 20.0)
+    assert ops._stream_pol(28672, 4096) == 5  # 235 MB gate/up weight: nt DMA + write-through
+    assert ops._stream_pol(2304, 768) == 4    # 3.5 MB: below the threshold
