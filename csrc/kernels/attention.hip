@@ -88,7 +88,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
                                                        const bf16* __restrict__ Kp, int ldk,
                                                        const bf16* __restrict__ Vp, int ldv, bf16* __restrict__ O,
                                                        int ldo, int S, int n_head, int n_kv_head, float scale_log2,
-                                                       int causal, int n_qtiles, int Sq, int q_off, int wt) {
+                                                       int causal, int n_qtiles, int Sq, int q_off, int flags) {
   using C = AttnCfg<D, NW, ST, KS>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave_id = tid >> 6;
@@ -96,8 +96,19 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
   // range is walked by KS independent online-softmax chains, merged through LDS at the end)
   const int wave = wave_id % NW, hg = wave_id / NW;
   const int g = lane >> 4, li = lane & 15;
-  const int qt = causal ? (n_qtiles - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heaviest first
-  const int h = blockIdx.y, b = blockIdx.z;
+  // flags bit 1: XCD-grouped blocks — the blocks of one (batch, head) run on one XCD (block
+  // b goes to XCD b % 8; xcd_remap hands each XCD a contiguous range of logical blocks, query
+  // tiles fastest), so the head's K/V rows come into ONE XCD's L2 from the MALL instead of all
+  // eight; the heaviest-first order then holds within each XCD's range
+  int bx = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  if (flags & 2) {
+    const int lin = bx + gridDim.x * (h + gridDim.y * b);
+    const int L = xcd_remap(lin, gridDim.x * gridDim.y * gridDim.z);
+    bx = L % gridDim.x;
+    h = (L / gridDim.x) % gridDim.y;
+    b = L / (gridDim.x * gridDim.y);
+  }
+  const int qt = causal ? (n_qtiles - 1 - bx) : bx;  // heaviest first
   const int kvh = h / (n_head / n_kv_head);
   const int q0 = qt * C::QB + wave * 16;  // this wave's 16 queries (local rows of the q chunk)
   const size_t tok0 = (size_t)b * S;       // first key row of this batch
@@ -282,7 +293,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
       bf16x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dn][i] * inv);
-      if (wt)
+      if (flags & 1)
         __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<const u32x2*>(&v), rs,
                                               (int)(((qtok0 + my_q) * ldo + h * D + 16 * dn + 4 * g) * 2), 0, 16);
       else

@@ -982,9 +982,20 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     return;
   }
   const int bid = xcd_remap(blockIdx.x, ntile * splitk);
-  const int ks = bid / ntile, tile = bid % ntile;
-  const int tm = tile % tiles_m, tn = tile / tiles_m;
+  int ks = bid / ntile, tile = bid % ntile;
+  int tm = tile % tiles_m, tn = tile / tiles_m;
   if constexpr (!RANGED) {
+    if (compact_rows > 0) {
+      // XCD-blocked tile order (launch: xcd_block; compact_rows is free on plain launches):
+      // XCD x = blockIdx.x % 8 owns an a x b block of output tiles, a = compact_rows M tiles,
+      // so its L2 fetches a rows of A panels and b columns of W panels from the MALL instead
+      // of all of A (splitk 1, tile counts divisible as the host checked)
+      const int a = compact_rows, b = (ntile >> 3) / a, gm = tiles_m / a;
+      const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+      tm = (xcd % gm) * a + idx % a;
+      tn = (xcd / gm) * b + idx / a;
+      ks = 0;
+    }
     glds_tile<C, LN, (POL & 1) ? kPolStream : 0, false, false, 0, false,
               ((POL & 2) ? kPolStream : 0) | ((POL & 4) ? kPolWT : 0)>(
         smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, M, M, N, K, act, alpha, ks, kslice, tm, tn, ln_colsum,
@@ -1003,6 +1014,35 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     glds_tile<C, 0>(smem, A, lda, W, ldw, Cp, ldc, bias, R, ldr, part, Mr, M, N, K, act, alpha, ks, kslice, t, tn,
                     ln_colsum, 0, ln_eps, ep);
   }
+}
+
+// XCD-blocked tile order for a plain launch: the M-tile count a of each XCD's a x b block of
+// output tiles (a x b = tiles / 8, the 8 blocks tiling the grid) that minimises the operand
+// panels one XCD's L2 fetches, a * (A panel bytes) + b * (W panel bytes), when that beats the
+// default order (32 consecutive tiles, M fastest) by 10 %; 0 = default order. DLS_XCD_BLOCK=0
+// turns it off.
+inline int xcd_block(int tiles_m, int tiles_n, size_t a_bytes, size_t w_bytes) {
+  static const bool on = [] {
+    const char* e = std::getenv("DLS_XCD_BLOCK");
+    return !(e && *e == '0');
+  }();
+  const int ntile = tiles_m * tiles_n;
+  if (!on || ntile % 8 || ntile < 64) return 0;
+  const int per = ntile / 8;
+  const size_t cur = (size_t)std::min(per, tiles_m) * a_bytes + (size_t)((per + tiles_m - 1) / tiles_m) * w_bytes;
+  size_t best = cur;
+  int best_a = 0;
+  for (int a = 1; a <= per; ++a) {
+    if (per % a || tiles_m % a) continue;
+    const int b = per / a;
+    if (tiles_n % b || (tiles_m / a) * (tiles_n / b) != 8) continue;
+    const size_t c = (size_t)a * a_bytes + (size_t)b * w_bytes;
+    if (c < best) {
+      best = c;
+      best_a = a;
+    }
+  }
+  return best * 10 < cur * 9 ? best_a : 0;
 }
 
 // resident blocks of a persistent launch: CUs x blocks per CU (occupancy query, cached)
@@ -1034,6 +1074,10 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
   // ep.w_stream carries the store policy to the split-K reduce kernels (grouped launches alone
   // read it as the weight policy)
   const Epi ep{a.rope, a.stats_out, a.ext_stats, fixup ? a.tile_sem : nullptr, nullptr, nullptr, a.stream_pol & 4};
+  const int crows = rows ? a.compact_rows
+                         : (!persist && splitk == 1 ? xcd_block((a.M + C::BM - 1) / C::BM, (a.N + C::BN - 1) / C::BN,
+                                                                (size_t)C::BM * a.K * 2, (size_t)C::BN * a.K * 2)
+                                                    : 0);
   static_assert(2 * C::BM * sizeof(float) <= C::LDS_UNITS * 16, "LN stats must fit the staging LDS");
   const int tiles_m = rows ? 1 : (a.M + C::BM - 1) / C::BM, tiles_n = (a.N + C::BN - 1) / C::BN;
   const int kslice = a.K / splitk;
@@ -1042,7 +1086,7 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
 #define DLS_K(LN_, RG_, ...)                                                                                      \
   hipLaunchKernelGGL((gemm_glds_kernel<C, LN_, RG_, ##__VA_ARGS__>), grid, block, 0, s, (const bf16*)a.A, a.lda, (const bf16*)a.W, \
                      a.ldw, (bf16*)a.C, a.ldc, (const bf16*)a.bias, (const bf16*)a.R, a.ldr, ws, a.M, a.N, a.K, a.act, \
-                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, a.compact_rows, ep)
+                     a.alpha, tiles_m, tiles_n, splitk, kslice, ln_colsum, ln_mode, ln_eps, rows, crows, ep)
   const bool ln_in = ln_mode != 0 && !a.ext_stats;
   if (rows) DLS_K(0, 1);
   else if (persist) {

@@ -42,7 +42,8 @@ WEIGHT_NT_MB = float(os.environ.get("DLS_WEIGHT_NT_MB", "0"))
 # back: GPT-2 0.620 vs 0.640 ms, Llama-3-8B 9.46 vs 9.49 ms (profiles/r4_ab/write_through.txt);
 # nt output stores cost GPT-2 5 %
 ACT_POL = int(os.environ.get("DLS_ACT_POL", "4"))
-# attention output stores write-through (A/B knob)
+# attention flags: bit 0 output stores write-through (no measurable difference), bit 1 the
+# blocks of one head grouped on one XCD (A/B knob)
 ATTN_WT = int(os.environ.get("DLS_ATTN_WT", "0"))
 # attention kernel variant (0: the launcher's choice by grid size; 1..13: attention.hip)
 ATTN_VARIANT = int(os.environ.get("DLS_ATTN_VARIANT", "0"))

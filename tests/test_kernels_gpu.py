@@ -684,17 +684,18 @@ def test_gemm_write_through_splitk_swiglu(config, splitk, act):
 
 @pytest.mark.parametrize("S,n_head,n_kv,D", [(512, 12, 12, 64), (512, 32, 8, 128)])
 def test_attention_write_through_stores(S, n_head, n_kv, D):
-    """Attention with write-through (sc1) output stores writes exactly what the default
-    stores write."""
-    B = 1
+    """Attention flags (bit 0 write-through output stores, bit 1 XCD-grouped blocks) compute
+    exactly what the default launch computes (batch 2: the grouping remaps batch and head)."""
+    B = 2
     q = _rand(B * S, n_head * D, seed=240)
     k = _rand(B * S, n_kv * D, seed=241)
     v = _rand(B * S, n_kv * D, seed=242)
     e = ops.ext()
     o0 = e.attention(q, k, v, B, S, n_head, n_kv, D, True, 1.0 / D ** 0.5, None, 0, 0, 0, 0)
-    o1 = e.attention(q, k, v, B, S, n_head, n_kv, D, True, 1.0 / D ** 0.5, None, 0, 0, 0, 1)
-    torch.cuda.synchronize()
-    assert torch.equal(o0, o1)
+    for flags in (1, 2, 3):
+        o1 = e.attention(q, k, v, B, S, n_head, n_kv, D, True, 1.0 / D ** 0.5, None, 0, 0, 0, flags)
+        torch.cuda.synchronize()
+        assert torch.equal(o0, o1), flags
 
 
 def test_mlp_fused_one_launch():
