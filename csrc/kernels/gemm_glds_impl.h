@@ -1019,12 +1019,13 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
 // XCD-blocked tile order for a plain launch: the M-tile count a of each XCD's a x b block of
 // output tiles (a x b = tiles / 8, the 8 blocks tiling the grid) that minimises the operand
 // panels one XCD's L2 fetches, a * (A panel bytes) + b * (W panel bytes), when that beats the
-// default order (32 consecutive tiles, M fastest) by 10 %; 0 = default order. DLS_XCD_BLOCK=0
-// turns it off.
+// default order (32 consecutive tiles, M fastest) by 10 %; 0 = default order. Off unless
+// DLS_XCD_BLOCK=1: on GPT-2's out-proj / fc2 (16 x 16 tiles, 8 x 4 blocks per XCD: 26 % fewer
+// panel bytes per L2) the step measured 0.3 % slower (profiles/r4_ab/xcd_grouping.txt).
 inline int xcd_block(int tiles_m, int tiles_n, size_t a_bytes, size_t w_bytes) {
   static const bool on = [] {
     const char* e = std::getenv("DLS_XCD_BLOCK");
-    return !(e && *e == '0');
+    return e && *e == '1';
   }();
   const int ntile = tiles_m * tiles_n;
   if (!on || ntile % 8 || ntile < 64) return 0;
