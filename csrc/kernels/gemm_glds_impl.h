@@ -314,7 +314,7 @@ __device__ __forceinline__ void mainloop_joint(bf16x8* smem, const bf16* __restr
 //  * q2 / q3: a barrier before the DMA issue — every wave has finished (lgkmcnt-waited,
 //    consumed by its MFMAs) the reads of the slots being re-filled (W after q1, A after q2).
 // Each wave's fragment reads of a quadrant are all issued before its 16 MFMAs.
-template <class C>
+template <class C, int WPOL = 0>
 __device__ __forceinline__ void mainloop_ring(bf16x8* smem, const bf16* __restrict__ A, int lda,
                                               const bf16* __restrict__ W, int ldw, int M, int N, int m0, int n0,
                                               int kbeg, int nk, int lane, int wave, int wm, int wn,
@@ -341,9 +341,14 @@ __device__ __forceinline__ void mainloop_ring(bf16x8* smem, const bf16* __restri
     const bf16* const* src = hk < 2 ? srcA[hk] : srcB[hk - 2];
     bf16x8* st = slot(t, hk);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + dst[j]), 16, 0, 0);
+    for (int j = 0; j < 2; ++j) {
+      if (hk < 2)  // (hk is a literal at every call: one immediate policy per DMA)
+        __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * C::BK),
+                                         (__attribute__((address_space(3))) void*)(st + dst[j]), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(src[j] + t * C::BK),
+                                         (__attribute__((address_space(3))) void*)(st + dst[j]), 16, 0, WPOL);
+    }
   };
   // prologue: K-tiles 0 and 1 (W halves first: issue order inside a K-tile does not matter
   // for the counted waits, which retire whole K-tiles)
@@ -554,7 +559,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 #pragma unroll
   for (int i = 0; i < C::FM; ++i) st_s[i] = st_q[i] = 0.f;
   if constexpr (C::RING && !SKIP && !GATHER)  // (grouped expert launches keep the joint ring)
-    mainloop_ring<C>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, acc);
+    mainloop_ring<C, WPOL>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, acc);
   else if constexpr (C::BXS > 0)
     mainloop_split<C, WPOL, SKIP, GATHER>(smem, A, lda, W, ldw, M, N, m0, n0, kbeg, nk, lane, wave, wm, wn, ln_acc, acc,
                                   st_s, st_q, min(C::FM, max(0, (M - m0 - wm * C::WTM + 15) / 16)), arows);
@@ -1104,7 +1109,7 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) DLS_K(1, 0);  // 256x256: no registers left for it
   } else {
     int pol = 0;
-    if constexpr (!C::RING) pol = a.stream_pol & 7;  // own kernel per policy (not the ring main loop)
+    pol = a.stream_pol & 7;  // an own kernel per policy
     switch (pol) {
       case 1: DLS_K(0, 0, 1); break;
       case 2: DLS_K(0, 0, 2); break;
