@@ -49,8 +49,16 @@ ATTN_WT = int(os.environ.get("DLS_ATTN_WT", "0"))
 ATTN_VARIANT = int(os.environ.get("DLS_ATTN_VARIANT", "0"))
 
 
+# the LM-head policy pays only while the model's layer weights can stay MALL-resident: a
+# vocabulary projection whose own weight is this large belongs to a model whose weights stream
+# from HBM every step anyway, and there nt weight DMA slows the LM head itself (Llama-3-8B's
+# 1 GB LM head: 683 vs 432 us per step, profiles/r4_ab/lmhead_stream_policy.txt)
+LMHEAD_POL_MAX_MB = 128
+
+
 def _stream_pol(N: int, K: int) -> int:
-    pol = LMHEAD_POL if N >= LMHEAD_MIN_N else ACT_POL
+    lm = N >= LMHEAD_MIN_N and N * K * 2 <= LMHEAD_POL_MAX_MB * 1e6
+    pol = LMHEAD_POL if lm else ACT_POL
     if WEIGHT_NT_MB > 0 and N * K * 2 >= WEIGHT_NT_MB * 1e6:
         pol |= 1
     return pol

@@ -83,8 +83,8 @@ def test_stream_policy_selection(monkeypatch):
     monkeypatch.setattr(ops, "LMHEAD_POL", 3)
     monkeypatch.setattr(ops, "ACT_POL", 4)
     monkeypatch.setattr(ops, "WEIGHT_NT_MB", 0.0)
-    assert ops._stream_pol(50257, 768) == 3
-    assert ops._stream_pol(128256, 4096) == 3
+    assert ops._stream_pol(50257, 768) == 3      # GPT-2's 77 MB LM head
+    assert ops._stream_pol(128256, 4096) == 4    # Llama-3's 1 GB LM head: an ordinary GEMM
     assert ops._stream_pol(2304, 768) == 4
     monkeypatch.setattr(ops, "WEIGHT_NT_MB", 20.0)
     assert ops._stream_pol(28672, 4096) == 5  # 235 MB gate/up weight: nt DMA + write-through
