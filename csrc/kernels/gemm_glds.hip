@@ -16,12 +16,11 @@ struct ReduceNorm {
   int K;
 };
 
-__device__ __forceinline__ void reduce_finalize(float (&x)[8], const float (&v)[8], int m, int c,
-                                                const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
-                                                int act, float alpha, const Epi& ep, const ReduceNorm& nm) {
-  bf16x8 bv = {}, rv = {};
-  if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
-  if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
+// (bv / rv: the bias and residual vectors, loaded by the caller — ahead of the partial slabs
+// where it can, so the whole row costs one memory round trip)
+__device__ __forceinline__ void reduce_finalize_pre(float (&x)[8], const float (&v)[8], int m, int c, bool has_bias,
+                                                    const bf16x8& bv, bool has_r, const bf16x8& rv, int act,
+                                                    float alpha, const Epi& ep, const ReduceNorm& nm) {
   float mu = 0.f, rs = 1.f;
   if (nm.mode != 0) {
     const float inv_k = 1.0f / (float)nm.K;
@@ -32,13 +31,22 @@ __device__ __forceinline__ void reduce_finalize(float (&x)[8], const float (&v)[
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float z = nm.mode != 0 ? rs * (v[e] - mu * nm.colsum[c + e]) : alpha * v[e];
-    x[e] = apply_act(z + (bias ? bf2f(bv[e]) : 0.f), act);
+    x[e] = apply_act(z + (has_bias ? bf2f(bv[e]) : 0.f), act);
   }
   if (ep.rope.cols) rope_pairs<8>(x, m, c, ep.rope);
-  if (R) {
+  if (has_r) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] += bf2f(rv[e]);
   }
+}
+
+__device__ __forceinline__ void reduce_finalize(float (&x)[8], const float (&v)[8], int m, int c,
+                                                const bf16* __restrict__ bias, const bf16* __restrict__ R, int ldr,
+                                                int act, float alpha, const Epi& ep, const ReduceNorm& nm) {
+  bf16x8 bv = {}, rv = {};
+  if (bias) bv = *reinterpret_cast<const bf16x8*>(bias + c);
+  if (R) rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + c);
+  reduce_finalize_pre(x, v, m, c, bias != nullptr, bv, R != nullptr, rv, act, alpha, ep, nm);
 }
 
 // out = act(alpha * sum_s P[s] + bias) + R, 8 columns per lane (N % 8 == 0). ACT_SWIGLU: P is in
@@ -183,6 +191,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_norm_kernel(const float* __
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t slab = (size_t)M * N;
   const int nsk = SK > 0 ? SK : splitk;
+  // every other operand of the row is requested first, so it lands with the slabs
+  bf16x8 rpre[VPT], bpre[VPT], wv[VPT], bv[VPT];
+#pragma unroll
+  for (int u = 0; u < VPT; ++u) {
+    const int cl = min((u * 256 + tid) * 8, N - 8);
+    rpre[u] = R ? *reinterpret_cast<const bf16x8*>(R + (size_t)m * ldr + cl) : bf16x8{};
+    bpre[u] = bias ? *reinterpret_cast<const bf16x8*>(bias + cl) : bf16x8{};
+    wv[u] = *reinterpret_cast<const bf16x8*>(nw + cl);
+    bv[u] = nb ? *reinterpret_cast<const bf16x8*>(nb + cl) : bf16x8{};
+  }
   float v[VPT][8];
 #pragma unroll
   for (int u = 0; u < VPT; ++u)
@@ -231,7 +249,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_norm_kernel(const float* __
     const int c = (u * 256 + tid) * 8;
     const int cl = min(c, N - 8);
     float x[8];
-    reduce_finalize(x, v[u], m, cl, bias, R, ldr, act, alpha, ep, nm);
+    reduce_finalize_pre(x, v[u], m, cl, bias != nullptr, bpre[u], R != nullptr, rpre[u], act, alpha, ep, nm);
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -243,13 +261,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_norm_kernel(const float* __
       if (ep.w_stream & 4) store16_pol<16>(C, ((size_t)m * ldc + c) * 2, *reinterpret_cast<const u32x4*>(&o));
       else store16_pol<0>(C, ((size_t)m * ldc + c) * 2, *reinterpret_cast<const u32x4*>(&o));
     }
-  }
-  bf16x8 wv[VPT], bv[VPT];  // the norm's weights, requested before the two reductions
-#pragma unroll
-  for (int u = 0; u < VPT; ++u) {
-    const int cl = min((u * 256 + tid) * 8, N - 8);
-    wv[u] = *reinterpret_cast<const bf16x8*>(nw + cl);
-    bv[u] = nb ? *reinterpret_cast<const bf16x8*>(nb + cl) : bf16x8{};
   }
   auto block_sum = [&](float t, int slot) {
     t = wave_sum(t);
