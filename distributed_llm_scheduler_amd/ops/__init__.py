@@ -340,10 +340,12 @@ def linear_norm(x, w_derived, colsum, bias_derived, mode, eps=1e-5, act=None, re
             out = torch.empty(shp, dtype=x.dtype, device=x.device)
         o2 = out.view(M, N)
         r2 = residual.reshape(M, N) if residual is not None else None
+        pol = _stream_pol(N, K)
         for n0, n1, c, k in split:
             ext().gemm(x, w_derived[n0:n1], bias_derived[n0:n1] if bias_derived is not None else None,
                        r2[:, n0:n1] if r2 is not None else None, a, 1.0, o2[:, n0:n1], int(c), int(k),
-                       colsum[n0:n1], m, float(eps), None, False, None, None, 1, 2, 0, None, ext_stats)
+                       colsum[n0:n1], m, float(eps), None, False, None, None, 1, 2, 0, None, ext_stats,
+                       stream_pol=pol)
         return out
     cfg, sk = tuning.lookup_fused(M, N, K, tuning.tag(a))
     if ext_stats is None:
