@@ -9,6 +9,8 @@ can name what bounds it (tools/pmc_summary.py).
     python benchmarks/pmc_probe.py moe           Mixtral-8x7B layer: the grouped gate/up (SwiGLU)
                                                  and down launches over 8 experts, 512 tokens top-2
     python benchmarks/pmc_probe.py gemm M N K    any plain GEMM shape with its tuned config
+    python benchmarks/pmc_probe.py attn          GPT-2 causal attention: S 512, 12 heads x 64, the
+                                                 launcher's variant
 """
 import os
 import sys
@@ -57,6 +59,16 @@ def moe():
     torch.cuda.synchronize()
 
 
+def attn():
+    S, Hh, D = 512, 12, 64
+    qkv = (torch.randn(S, 3 * Hh * D, device="cuda") * 0.5).bfloat16()
+    q, k, v = qkv[:, :Hh * D], qkv[:, Hh * D:2 * Hh * D], qkv[:, 2 * Hh * D:]
+    o = torch.empty(S, Hh * D, device="cuda", dtype=torch.bfloat16)
+    for _ in range(REPS):
+        ops.attention(q, k, v, 1, S, Hh, Hh, D, causal=True, out=o)
+    torch.cuda.synchronize()
+
+
 def gemm(M, N, K):
     x = (torch.randn(M, K, device="cuda")).bfloat16()
     ws = [(torch.randn(N, K, device="cuda") * 0.05).bfloat16() for _ in range(4)]
@@ -73,5 +85,7 @@ if __name__ == "__main__":
         lmhead()
     elif what == "moe":
         moe()
+    elif what == "attn":
+        attn()
     else:
         gemm(*(int(v) for v in sys.argv[2:5]))
