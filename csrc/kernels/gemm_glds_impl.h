@@ -1198,6 +1198,10 @@ using C41 = Cfg<192, 128, 4, 2, 3, 0, 2>;
 // (one round) instead of 138 more 256 x 256 tiles that leave 118 CUs idle (ops.linear_norm
 // column split, ops/gemm_tuning.json "col_splits"). 3 x 50 KiB joint stages.
 using C42 = Cfg<256, 144, 8, 1, 3>;
+// 256 x 192 tiles, 8 waves as 4 x 2 (wave 64 x 96), split rings 2 x 32 KiB A + 3 x 24 KiB W:
+// with split-K 4 a 512 x 6144 x 4096 projection (Llama-3 QKV) is 64 tiles x 4 slices = 256
+// blocks whose per-CU operand bytes are half those of the one-slice 128 x 96 tiles
+using C43 = Cfg<256, 192, 4, 2, 2, 0, 1>;
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,
