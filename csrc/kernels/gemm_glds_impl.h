@@ -1202,6 +1202,10 @@ using C42 = Cfg<256, 144, 8, 1, 3>;
 // with split-K 4 a 512 x 6144 x 4096 projection (Llama-3 QKV) is 64 tiles x 4 slices = 256
 // blocks whose per-CU operand bytes are half those of the one-slice 128 x 96 tiles
 using C43 = Cfg<256, 192, 4, 2, 2, 0, 1>;
+// MoE gate/up: 160 routed rows (an expert's whole row range at 512 tokens top-2 over 8 experts)
+// x 256 weight columns, wave 80 x 64, split rings 2 x 20 KiB A + 3 x 32 KiB W: 80 B of operand
+// intake per output instead of 102 for 192 x 128 (the gathered A rows are re-read per column tile)
+using C44 = Cfg<160, 256, 2, 4, 2, 0, 1>;
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,
