@@ -465,12 +465,21 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
   static_assert(D >= 1, "split rings: the W ring is deeper than the A ring");
   const bf16* srcA[C::PWA];
   const bf16* srcB[C::PWB];
+  // SKIP (grouped expert launches, whose row count is the expert's, known on the device only):
+  // the A rows come by buffer DMA, and a row past the expert's last one gets an offset past the
+  // buffer's end — the load returns zeros WITHOUT a memory request, so the CU's LDS-DMA intake
+  // carries only real rows (with clamped addresses every padding row re-read the last one).
+  // Every wave still issues the same instructions: the counted vmcnt waits stay exact.
+  uint32_t voffA[C::PWA];
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int j = 0; j < C::PWA; ++j) {
     const int row = 8 * (C::EVEN_A ? wave * C::PWA + j : min(wave * C::PWA + j, C::BM / 8 - 1)) + (lane >> 3);
     int gm = min(m0 + row, M - 1);
     if constexpr (GATHER) gm = arows[gm];  // gathered A rows (MoE: token of each expert-sorted row)
     srcA[j] = A + (size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8;
+    if constexpr (SKIP)
+      voffA[j] = m0 + row < M ? (uint32_t)(((size_t)gm * lda + kbeg + ((lane & 7) ^ (row & 7)) * 8) * 2) : 0x80000000u;
   }
 #pragma unroll
   for (int j = 0; j < C::PWB; ++j) {
@@ -483,10 +492,13 @@ __device__ __forceinline__ void mainloop_split(bf16x8* smem, const bf16* __restr
   auto issueA = [&](int kt) {
     bf16x8* st = ringA + (kt % C::SA) * C::A_STAGE;
 #pragma unroll
-    for (int j = 0; j < C::PWA; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * C::BK),
-                                       (__attribute__((address_space(3))) void*)(st + (C::EVEN_A ? wave * C::PWA + j : min(wave * C::PWA + j, C::BM / 8 - 1)) * 64), 16,
-                                       0, 0);
+    for (int j = 0; j < C::PWA; ++j) {
+      auto* dst = (__attribute__((address_space(3))) void*)(st + (C::EVEN_A ? wave * C::PWA + j : min(wave * C::PWA + j, C::BM / 8 - 1)) * 64);
+      if constexpr (SKIP)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, dst, 16, voffA[j] + kt * C::BK * 2, 0, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + kt * C::BK), dst, 16, 0, 0);
+    }
   };
   auto issueB = [&](int kt) {
     bf16x8* st = ringB + (kt % C::SB) * C::B_STAGE;
