@@ -91,9 +91,10 @@ def regime_cap_gb(model, regime, batch, seq, cost_model) -> float:
 
 def _cache_policy() -> dict:
     """The cache policies the step's kernels ran with (ops: DLS_LMHEAD_POL / DLS_ACT_POL /
-    DLS_ATTN_WT): stream_pol bits 1 weight DMA nt, 2 output stores nt, 4 write-through."""
+    DLS_ATTN_FLAGS): stream_pol bits 1 weight DMA nt, 2 output stores nt, 4 write-through;
+    attention flags bit 0 write-through stores, bit 1 XCD-grouped blocks."""
     from distributed_llm_scheduler_amd import ops
-    return {"lm_head": ops.LMHEAD_POL, "gemm": ops.ACT_POL, "attention_write_through": bool(ops.ATTN_WT)}
+    return {"lm_head": ops.LMHEAD_POL, "gemm": ops.ACT_POL, "attention_flags": ops.ATTN_FLAGS}
 
 
 def launch_ranks(n: int) -> int:

@@ -286,7 +286,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
     bf16* orow = O + (qtok0 + my_q) * ldo + h * D;
     // wt: write-through (sc1) stores — the tile leaves the XCD's L2 as it is written, so the
-    // kernel boundary has no dirty lines of it to write back (AttnArgs::store_wt)
+    // kernel boundary has no dirty lines of it to write back (AttnArgs::flags bit 0)
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(O, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
     for (int dn = 0; dn < C::ND; ++dn) {
@@ -313,7 +313,7 @@ static void launch_attn(const AttnArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((attn_fwd_kernel<D, NW, ST, KS>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
                      static_cast<const bf16*>(a.k), a.ldk, static_cast<const bf16*>(a.v), a.ldv,
                      static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq, Sq,
-                     a.Sq > 0 ? a.q_off : 0, a.store_wt);
+                     a.Sq > 0 ? a.q_off : 0, a.flags);
 }
 
 template <int D>

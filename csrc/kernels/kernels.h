@@ -114,7 +114,7 @@ struct AttnArgs {
   // 0 .. S-1). Sq = 0 means Sq = S, q_off = 0 (ordinary self-attention).
   int Sq = 0;
   int q_off = 0;
-  int store_wt = 0;  // bit 0: output stores write-through (sc1); bit 1: XCD-grouped blocks
+  int flags = 0;  // bit 0: output stores write-through (sc1); bit 1: XCD-grouped blocks
 };
 void launch_attention_fwd(const AttnArgs& a, hipStream_t s);
 

@@ -224,7 +224,7 @@ at::Tensor gemm(const at::Tensor& a_in, const at::Tensor& w, const c10::optional
 at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
                      int64_t n_head, int64_t n_kv_head, int64_t head_dim, bool causal, double scale,
                      const c10::optional<at::Tensor>& out, int64_t variant, int64_t Sq, int64_t q_off,
-                     int64_t store_wt) {
+                     int64_t flags) {
   if (Sq <= 0) Sq = S;
   TORCH_CHECK(q_off >= 0 && (!causal || q_off + Sq <= S), "query chunk must lie inside the key range");
   for (auto* p : {&q, &k, &v}) {
@@ -242,7 +242,7 @@ at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor&
   TORCH_CHECK(o.size(0) == B * Sq && o.size(1) >= n_head * head_dim, "out must be [B*Sq, >= n_head*head_dim]");
   AttnArgs a{q.data_ptr(), (int)q.stride(0), k.data_ptr(), (int)k.stride(0), v.data_ptr(), (int)v.stride(0),
              o.data_ptr(), (int)o.stride(0), (int)B, (int)S, (int)n_head, (int)n_kv_head, (int)head_dim,
-             (float)scale, causal ? 1 : 0, (int)variant, (int)Sq, (int)q_off, (int)store_wt};
+             (float)scale, causal ? 1 : 0, (int)variant, (int)Sq, (int)q_off, (int)flags};
   launch_attention_fwd(a, cur_stream());
   return o;
 }
@@ -715,7 +715,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention", &attention, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"),
         py::arg("n_head"), py::arg("n_kv_head"), py::arg("head_dim"), py::arg("causal") = true,
         py::arg("scale") = 0.125, py::arg("out") = py::none(), py::arg("variant") = 0, py::arg("Sq") = 0,
-        py::arg("q_off") = 0, py::arg("store_wt") = 0);
+        py::arg("q_off") = 0, py::arg("flags") = 0);
   m.def("norm", &norm, py::arg("x"), py::arg("w"), py::arg("b") = py::none(), py::arg("eps") = 1e-5,
         py::arg("residual") = py::none(), py::arg("rms") = false, py::arg("out") = py::none(),
         py::arg("sum_out") = py::none());

@@ -44,7 +44,7 @@ WEIGHT_NT_MB = float(os.environ.get("DLS_WEIGHT_NT_MB", "0"))
 ACT_POL = int(os.environ.get("DLS_ACT_POL", "4"))
 # attention flags: bit 0 output stores write-through (no measurable difference), bit 1 the
 # blocks of one head grouped on one XCD (A/B knob)
-ATTN_WT = int(os.environ.get("DLS_ATTN_WT", "0"))
+ATTN_FLAGS = int(os.environ.get("DLS_ATTN_FLAGS", "0"))
 # attention kernel variant (0: the launcher's choice by grid size; 1..13: attention.hip)
 ATTN_VARIANT = int(os.environ.get("DLS_ATTN_VARIANT", "0"))
 
@@ -427,7 +427,7 @@ def attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal=True, scale=Non
     scale = scale if scale is not None else 1.0 / math.sqrt(head_dim)
     if _gpu(q):
         return ext().attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, float(scale), out, ATTN_VARIANT,
-                               int(Sq or 0), int(q_off), int(ATTN_WT))
+                               int(Sq or 0), int(q_off), int(ATTN_FLAGS))
     y = ref_attention(q, k, v, B, S, n_head, n_kv_head, head_dim, causal, scale, Sq=Sq, q_off=q_off)
     if out is not None:
         out.copy_(y)

@@ -47,7 +47,7 @@ def test_bench_single_process():
     _check(lines[0], 1)
     # the cache policies the step's kernels ran with (defaults: LM head weight + logits nt,
     # every other GEMM write-through)
-    assert lines[0]["cache_policy"] == {"lm_head": 3, "gemm": 4, "attention_write_through": False}
+    assert lines[0]["cache_policy"] == {"lm_head": 3, "gemm": 4, "attention_flags": 0}
 
 
 @pytest.mark.timeout(300)
