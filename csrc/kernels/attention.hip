@@ -18,6 +18,15 @@
 #include "common.h"
 #include "kernels.h"
 
+// Phase stamps for a diagnostic build (benchmarks/attn_stamps.hip defines DLS_ASTAMP to read the
+// 100 MHz clock into a register; the block's wave 0 stores them once at the very end, so no
+// extra memory operation joins the counted vmcnt waits). Compiled out otherwise.
+#ifndef DLS_ASTAMP
+#define DLS_ASTAMP_DECL()
+#define DLS_ASTAMP(k)
+#define DLS_ASTAMP_STORE()
+#endif
+
 namespace {
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -56,7 +65,7 @@ struct AttnCfg {
   static constexpr int BUF_BYTES = 2 * TILE_BYTES;    // K + V
   static constexpr int NQK = D / 32;                  // k-steps of S^T
   static constexpr int ND = D / 16;                   // output d-subtiles
-  static constexpr int MERGE_BYTES = KS > 1 ? NW * 64 * (ND * 4 + 2) * 4 : 0;
+  static constexpr int MERGE_BYTES = KS > 1 ? (KS - 1) * NW * 64 * (ND * 4 + 2) * 4 : 0;
   static constexpr int SMEM = ST * BUF_BYTES > MERGE_BYTES ? ST * BUF_BYTES : MERGE_BYTES;
   static_assert(PW * (ST - 2) <= 63 && PW * NWT == 2 * INSTR, "DMA split");
   static_assert(SMEM <= 163840, "LDS budget");
@@ -109,6 +118,8 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
     b = L / (gridDim.x * gridDim.y);
   }
   const int qt = causal ? (n_qtiles - 1 - bx) : bx;  // heaviest first
+  DLS_ASTAMP_DECL()
+  DLS_ASTAMP(0)
   const int kvh = h / (n_head / n_kv_head);
   const int q0 = qt * C::QB + wave * 16;  // this wave's 16 queries (local rows of the q chunk)
   const size_t tok0 = (size_t)b * S;       // first key row of this batch
@@ -172,6 +183,9 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
     // tile t has landed once at most min(ST-2, tiles issued after t) tiles are in flight
     wait_tiles<C::PW, ST - 2>(min(ST - 2, ntiles - 1 - t));
     raw_barrier();
+    if (t == 0) {
+      DLS_ASTAMP(1)
+    }
     if (t + ST - 1 < ntiles) issue(t + ST - 1);  // into the buffer everyone finished in t-1
     const char* kb = smem + (t % ST) * C::BUF_BYTES + hg * C::KT * C::RB;
     const char* vb = kb + C::TILE_BYTES;
@@ -248,39 +262,54 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
       }
     }
   }
+  DLS_ASTAMP(2)
   if constexpr (KS > 1) {
-    // merge the key-half chains: group hg > 0 publishes (o, m, l), group 0 rescales and sums
+    // merge the key-group chains in ONE exchange: every group hg > 0 publishes (o, m, l) into
+    // its own LDS slab at once (field-major: a wave's 64 lanes store 64 consecutive floats, no
+    // bank conflicts), one barrier, and group 0 rescales and sums all of them in registers
     __syncthreads();  // all DMA landed and every wave is done with the K/V buffers
     float* mg = reinterpret_cast<float*>(smem);
-    constexpr int REC = C::ND * 4 + 2;
-    for (int h2 = 1; h2 < KS; ++h2) {
-      if (hg == h2) {
-        float* r = mg + (wave * 64 + lane) * REC;
+    constexpr int REC = C::ND * 4 + 2;  // floats per lane: o, m, l
+    constexpr int LN = C::NW * 64;      // lanes of one key group
+    const int me = wave * 64 + lane;
+    if (hg > 0) {
+      float* r = mg + (hg - 1) * REC * LN + me;
 #pragma unroll
-        for (int dn = 0; dn < C::ND; ++dn)
+      for (int dn = 0; dn < C::ND; ++dn)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) r[dn * 4 + i] = o[dn][i];
-        r[C::ND * 4] = m_run;
-        r[C::ND * 4 + 1] = l_run;
-      }
-      __syncthreads();
-      if (hg == 0) {
-        const float* r = mg + (wave * 64 + lane) * REC;
-        const float m1 = r[C::ND * 4], l1 = r[C::ND * 4 + 1];
-        const float mm = fmaxf(fmaxf(m_run, m1), -1e30f);
-        const float a0 = __builtin_amdgcn_exp2f((m_run - mm) * scale_log2);
-        const float a1 = __builtin_amdgcn_exp2f((m1 - mm) * scale_log2);
-        l_run = l_run * a0 + l1 * a1;
-        m_run = mm;
-#pragma unroll
-        for (int dn = 0; dn < C::ND; ++dn)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[dn][i] = o[dn][i] * a0 + r[dn * 4 + i] * a1;
-      }
-      if (h2 + 1 < KS) __syncthreads();
+        for (int i = 0; i < 4; ++i) r[(dn * 4 + i) * LN] = o[dn][i];
+      r[C::ND * 4 * LN] = m_run;
+      r[(C::ND * 4 + 1) * LN] = l_run;
     }
+    __syncthreads();
     if (hg != 0) return;
+    float mo[KS - 1], lo_[KS - 1];
+    float mm = m_run;
+#pragma unroll
+    for (int h2 = 0; h2 < KS - 1; ++h2) {
+      const float* r = mg + h2 * REC * LN + me;
+      mo[h2] = r[C::ND * 4 * LN];
+      lo_[h2] = r[(C::ND * 4 + 1) * LN];
+      mm = fmaxf(mm, mo[h2]);
+    }
+    mm = fmaxf(mm, -1e30f);
+    const float a0 = __builtin_amdgcn_exp2f((m_run - mm) * scale_log2);
+    l_run *= a0;
+#pragma unroll
+    for (int dn = 0; dn < C::ND; ++dn) o[dn] *= a0;
+#pragma unroll
+    for (int h2 = 0; h2 < KS - 1; ++h2) {
+      const float* r = mg + h2 * REC * LN + me;
+      const float a1 = __builtin_amdgcn_exp2f((mo[h2] - mm) * scale_log2);
+      l_run += lo_[h2] * a1;
+#pragma unroll
+      for (int dn = 0; dn < C::ND; ++dn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[dn][i] += r[(dn * 4 + i) * LN] * a1;
+    }
+    m_run = mm;
   }
+  DLS_ASTAMP(3)
   // ---- normalise and store O[q][d]: lane holds d = 16dn + 4g + i for query my_q
   if (my_q < Sq) {
     const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -300,6 +329,8 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
         *reinterpret_cast<bf16x4*>(orow + 16 * dn + 4 * g) = v;
     }
   }
+  DLS_ASTAMP(4)
+  DLS_ASTAMP_STORE()
 }
 
 }  // namespace
@@ -342,7 +373,9 @@ static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
       // keys over two wave groups (GPT-2 S=512: 96 blocks, 8.2 -> 6.2 us with 32-query blocks;
       // Llama-3-8B S=512: 256 blocks, 13.1 -> 11.9 us)
       const long blocks = (long)(((a.Sq > 0 ? a.Sq : a.S) + 63) / 64) * a.n_head * a.B;
-      if (blocks <= 128) launch_attn<D, 2, 2, 2>(a, s);
+      // (<= 128 blocks: four key groups per stage for D = 64 since the key-group merge is one
+      // LDS exchange — GPT-2 S=512: 0.623 vs 0.629 ms per step, profiles/r4_ab/attention_merge.txt)
+      if (blocks <= 128) launch_attn<D, 2, 2, (D == 64 ? 4 : 2)>(a, s);
       else if (blocks <= 320) launch_attn<D, 4, 2, 2>(a, s);
       else launch_attn<D, 4, 2>(a, s);
     }
