@@ -1089,9 +1089,13 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
     return (e && *e ? std::atoi(e) : 64) * 1024;
   }();
   const bool fixup = splitk > 1 && !rows && (splitk - 1) * C::BM * C::BN * 4 <= fixup_max;
+  // policy stores are buffer stores with 32-bit byte offsets from the output's base: outputs
+  // (or split-K slabs) of 2 GB and more keep the default stores
+  int spol = a.stream_pol & 7;
+  if ((size_t)a.M * a.ldc * 2 >= (1ull << 31) || (size_t)a.M * a.N * 4 * splitk >= (1ull << 31)) spol &= 1;
   // ep.w_stream carries the store policy to the split-K reduce kernels (grouped launches alone
   // read it as the weight policy)
-  const Epi ep{a.rope, a.stats_out, a.ext_stats, fixup ? a.tile_sem : nullptr, nullptr, nullptr, a.stream_pol & 4};
+  const Epi ep{a.rope, a.stats_out, a.ext_stats, fixup ? a.tile_sem : nullptr, nullptr, nullptr, spol & 4};
   const int crows = rows ? a.compact_rows
                          : (!persist && splitk == 1 ? xcd_block((a.M + C::BM - 1) / C::BM, (a.N + C::BN - 1) / C::BN,
                                                                 (size_t)C::BM * a.K * 2, (size_t)C::BN * a.K * 2)
@@ -1120,8 +1124,7 @@ bool launch(const GemmArgs& a, int splitk, float* ws, hipStream_t s, const float
   } else if (ln_in) {
     if constexpr (C::BM * C::BN <= 256 * 128 && C::KG == 1) DLS_K(1, 0);  // 256x256: no registers left for it
   } else {
-    int pol = 0;
-    pol = a.stream_pol & 7;  // an own kernel per policy
+    const int pol = spol;  // an own kernel per policy
     switch (pol) {
       case 1: DLS_K(0, 0, 1); break;
       case 2: DLS_K(0, 0, 2); break;
@@ -1228,7 +1231,10 @@ void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned
     const char* e = std::getenv("DLS_EXPERT_NT");
     return e && e[0] == '0' ? 0 : 1;
   }();
-  const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs, w_stream};
+  // (the nt path DMAs the A rows by buffer loads with 32-bit offsets: an A of 2 GB or more
+  // takes the default path)
+  const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs,
+               (size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0};
   const int tiles_n = (a.N + C::BN - 1) / C::BN;
   hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(n_groups * tiles_n), dim3(C::T), 0, s, (const bf16*)a.A,
                      a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0,

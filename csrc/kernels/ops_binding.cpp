@@ -242,7 +242,9 @@ at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor&
   TORCH_CHECK(o.size(0) == B * Sq && o.size(1) >= n_head * head_dim, "out must be [B*Sq, >= n_head*head_dim]");
   AttnArgs a{q.data_ptr(), (int)q.stride(0), k.data_ptr(), (int)k.stride(0), v.data_ptr(), (int)v.stride(0),
              o.data_ptr(), (int)o.stride(0), (int)B, (int)S, (int)n_head, (int)n_kv_head, (int)head_dim,
-             (float)scale, causal ? 1 : 0, (int)variant, (int)Sq, (int)q_off, (int)flags};
+             (float)scale, causal ? 1 : 0, (int)variant, (int)Sq, (int)q_off,
+             // write-through stores use 32-bit buffer offsets: not for outputs of 2 GB or more
+             (int)(o.numel() * 2 < (1ll << 31) ? flags : flags & ~1)};
   launch_attention_fwd(a, cur_stream());
   return o;
 }
