@@ -682,6 +682,20 @@ def test_gemm_write_through_splitk_swiglu(config, splitk, act):
     assert torch.equal(ys[0], ys[1])
 
 
+def test_gemm_write_through_large_output():
+    """A 2 GiB output keeps the default stores (policy stores address 32-bit buffer offsets):
+    its last rows, past 2^31 bytes, must be written correctly under the write-through default."""
+    M, N, K = 32768, 32768, 64
+    x, w = _rand(M, K, seed=260), _rand(N, K, scale=0.05, seed=261)
+    y = ops.ext().gemm(x, w, None, None, 0, 1.0, None, 0, 1, stream_pol=4)
+    torch.cuda.synchronize()
+    rows = torch.tensor([0, M // 2, M - 2, M - 1])
+    ref = ops.ref_linear(x[rows.to(DEV)].cpu(), w.cpu()).float()
+    _close(y[rows.to(DEV)].cpu(), ref, 2e-2)
+    del y
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("S,n_head,n_kv,D", [(512, 12, 12, 64), (512, 32, 8, 128)])
 def test_attention_write_through_stores(S, n_head, n_kv, D):
     """Attention flags (bit 0 write-through output stores, bit 1 XCD-grouped blocks) compute
