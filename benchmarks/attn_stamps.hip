@@ -5,7 +5,7 @@
 // end of the block. GPT-2 shape: S 512, 12 heads x 64, causal, batch 1.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -Icsrc/kernels benchmarks/attn_stamps.hip -o gpubin/attn_stamps
-//   gpubin/attn_stamps [variant] [S] [heads]
+//   gpubin/attn_stamps [variant] [S] [heads] [flags]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,6 +32,7 @@ __device__ unsigned long long g_astamps[4096 * 5];
 int main(int argc, char** argv) {
   const int variant = argc > 1 ? atoi(argv[1]) : 0;
   const int S = argc > 2 ? atoi(argv[2]) : 512, H = argc > 3 ? atoi(argv[3]) : 12, D = 64;
+  const int flags = argc > 4 ? atoi(argv[4]) : 0;
   std::vector<unsigned short> h((size_t)S * 3 * H * D);
   for (size_t i = 0; i < h.size(); ++i) h[i] = 0x3c00 + (unsigned short)(rand() & 0x3ff);
   void *qkv, *o;
@@ -40,7 +41,7 @@ int main(int argc, char** argv) {
   hipMemcpy(qkv, h.data(), h.size() * 2, hipMemcpyHostToDevice);
   const char* base = static_cast<const char*>(qkv);
   AttnArgs a{base, 3 * H * D, base + H * D * 2, 3 * H * D, base + 2 * H * D * 2, 3 * H * D, o, H * D,
-             1, S, H, H, D, 0.125f, 1, variant, 0, 0, 0};
+             1, S, H, H, D, 0.125f, 1, variant, 0, 0, flags};
   for (int i = 0; i < 5; ++i) launch_attention_fwd(a, 0);
   hipDeviceSynchronize();
   hipMemcpyToSymbol(HIP_SYMBOL(g_astamps), std::vector<unsigned long long>(4096 * 5, 0).data(), 4096 * 5 * 8);
@@ -63,6 +64,7 @@ int main(int argc, char** argv) {
       tend = std::max(tend, st[b * 5 + 4]);
       ++nb;
     }
+  printf("flags %d ", flags);
   printf("variant %d S %d heads %d: event %.2f us; blocks %d; first-start -> last-end %.2f us\n", variant, S, H,
          ms * 1e3, nb, (tend - t0) * 0.01);
   const char* names[] = {"start offset", "first K/V tile", "key loop", "merge", "normalise+store"};
