@@ -31,6 +31,11 @@ namespace {
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -157,15 +162,26 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
     doff[j] = op * C::TILE_BYTES + r0 * C::RB;
   }
   const bool tail_clamp = (S % C::KTS) != 0;
+  // running per-lane sources: issue() is called for t = 0, 1, 2, ... in order and moves each
+  // pointer one tile (KTS rows) on — no per-tile 64-bit address arithmetic (the ragged last
+  // tile clamps its rows explicitly)
+  const bf16* dptr[C::PW];
+  size_t dinc[C::PW];
+#pragma unroll
+  for (int j = 0; j < C::PW; ++j) {
+    dptr[j] = dsrc[j] + (size_t)drow[j] * dstep[j];
+    dinc[j] = (size_t)C::KTS * dstep[j];
+  }
   auto issue = [&](int t) {
     char* buf = smem + (t % ST) * C::BUF_BYTES;
     const bool clamp = tail_clamp && (t + 1) * C::KTS > S;
 #pragma unroll
     for (int j = 0; j < C::PW; ++j) {
-      int key = t * C::KTS + drow[j];
-      if (clamp) key = min(key, S - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(dsrc[j] + (size_t)key * dstep[j]),
-                                       (__attribute__((address_space(3))) void*)(buf + doff[j]), 16, 0, 0);
+      const bf16* src = dptr[j];
+      if (clamp) src = dsrc[j] + (size_t)min(t * C::KTS + drow[j], S - 1) * dstep[j];
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + doff[j]),
+                                       16, 0, 0);
+      dptr[j] += dinc[j];
     }
   };
 
@@ -176,21 +192,10 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
   const int my_q = q0 + li;         // local query row
   const int gq = q_off + my_q;       // its global position (causal mask)
 
-#pragma unroll
-  for (int p = 0; p < ST - 1; ++p)
-    if (p < ntiles) issue(p);
-  for (int t = 0; t < ntiles; ++t) {
-    // tile t has landed once at most min(ST-2, tiles issued after t) tiles are in flight
-    wait_tiles<C::PW, ST - 2>(min(ST - 2, ntiles - 1 - t));
-    raw_barrier();
-    if (t == 0) {
-      DLS_ASTAMP(1)
-    }
-    if (t + ST - 1 < ntiles) issue(t + ST - 1);  // into the buffer everyone finished in t-1
+  // one 64-key stage of this wave's chain: S^T = K Q^T, online softmax, O^T += V^T P^T
+  auto stage = [&](int t, int key0, auto mask_c) {
     const char* kb = smem + (t % ST) * C::BUF_BYTES + hg * C::KT * C::RB;
     const char* vb = kb + C::TILE_BYTES;
-    const int key0 = t * C::KTS + hg * C::KT;
-
     // ---- S^T = K Q^T : 4 key-subtiles x 16 queries
     f32x4 s[4];
 #pragma unroll
@@ -206,9 +211,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
     }
     // ---- online softmax for query my_q; scores s[n][i] <-> key key0 + 16n + 4g + i.
     // Raw scores are kept; the scale is folded into the exponent: p = 2^(s*c - m*c).
-    // Masks only on the wave's diagonal tile and the ragged last tile (wave-uniform branch).
-    const bool masked = (key0 + C::KT > S) || (causal && key0 + C::KT - 1 > q_off + q0);
-    if (masked) {
+    if constexpr (decltype(mask_c)::value) {
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -261,6 +264,26 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
         o[dn] = mfma16x16x32(vf, pf[ks], o[dn]);
       }
     }
+  };
+
+#pragma unroll
+  for (int p = 0; p < ST - 1; ++p)
+    if (p < ntiles) issue(p);
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t has landed once at most min(ST-2, tiles issued after t) tiles are in flight
+    wait_tiles<C::PW, ST - 2>(min(ST - 2, ntiles - 1 - t));
+    raw_barrier();
+    if (t == 0) {
+      DLS_ASTAMP(1)
+    }
+    if (t + ST - 1 < ntiles) issue(t + ST - 1);  // into the buffer everyone finished in t-1
+    const int key0 = t * C::KTS + hg * C::KT;
+    // Masks only on the wave's diagonal tile and the ragged last tile: a wave-uniform choice
+    // between two instantiations of the stage (a plain branch was if-converted, so every tile
+    // paid for the mask compares and selects)
+    const bool masked = (key0 + C::KT > S) || (causal && key0 + C::KT - 1 > q_off + q0);
+    if (masked) stage(t, key0, BoolC<true>{});
+    else stage(t, key0, BoolC<false>{});
   }
   DLS_ASTAMP(2)
   if constexpr (KS > 1) {
