@@ -41,7 +41,14 @@ int main(int argc, char** argv) {
   hipMemcpy(qkv, h.data(), h.size() * 2, hipMemcpyHostToDevice);
   const char* base = static_cast<const char*>(qkv);
   AttnArgs a{base, 3 * H * D, base + H * D * 2, 3 * H * D, base + 2 * H * D * 2, 3 * H * D, o, H * D,
-             1, S, H, H, D, 0.125f, 1, variant, 0, 0, flags};
+             1, S, H, H, D, 0.125f, 1, variant, 0, 0, flags, nullptr, nullptr};
+  if (variant == 14) {  // split variant: partials + zeroed tickets
+    size_t pf = 0, nc = 0;
+    attention_split_sizes(a, &pf, &nc);
+    hipMalloc(&a.part, pf * 4);
+    hipMalloc(&a.cnt, nc * 4);
+    hipMemset(a.cnt, 0, nc * 4);
+  }
   for (int i = 0; i < 5; ++i) launch_attention_fwd(a, 0);
   hipDeviceSynchronize();
   hipMemcpyToSymbol(HIP_SYMBOL(g_astamps), std::vector<unsigned long long>(4096 * 5, 0).data(), 4096 * 5 * 8);

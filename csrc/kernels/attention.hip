@@ -15,6 +15,8 @@
 // per-lane source address, rule 21), double-buffered: wait(tile t) -> ONE barrier ->
 // issue(tile t+1 into the buffer everyone finished in t-1) -> compute t.
 // Causal blocks stop at the diagonal tile and are launched heaviest-first.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -97,12 +99,18 @@ __device__ __forceinline__ float xlane(float x) {
   return MAX ? fmaxf(a, b) : a + b;
 }
 
-template <int D, int NW, int ST, int KS>
+// SPLIT: every block takes ONE key tile (KTS keys) of one query tile — a query tile's key range
+// is spread over as many blocks as it has tiles, so no CU streams a long causal row's whole K/V
+// (the per-CU LDS-DMA intake bounds a stage); the blocks of a query tile publish their
+// unnormalised (o, m, l) write-through into `part`, draw a ticket from cnt[query tile], and the
+// last arriver merges the others' partials and stores the output (it resets the ticket)
+template <int D, int NW, int ST, int KS, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __restrict__ Q, int ldq,
                                                        const bf16* __restrict__ Kp, int ldk,
                                                        const bf16* __restrict__ Vp, int ldv, bf16* __restrict__ O,
                                                        int ldo, int S, int n_head, int n_kv_head, float scale_log2,
-                                                       int causal, int n_qtiles, int Sq, int q_off, int flags) {
+                                                       int causal, int n_qtiles, int Sq, int q_off, int flags,
+                                                       float* __restrict__ part, int* __restrict__ cnt, int maxc) {
   using C = AttnCfg<D, NW, ST, KS>;
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave_id = tid >> 6;
@@ -122,7 +130,22 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
     h = (L / gridDim.x) % gridDim.y;
     b = L / (gridDim.x * gridDim.y);
   }
-  const int qt = causal ? (n_qtiles - 1 - bx) : bx;  // heaviest first
+  // key tiles [t0, t1) of query tile qt (SPLIT: one tile, chunk c of nch)
+  int qt, c = 0, nch = 1;
+  if constexpr (SPLIT) {
+    int rem = bx;
+    qt = n_qtiles - 1;
+    for (;;) {  // heaviest query tiles first; every block finds its item (bx < total items)
+      const int kvq = causal ? min(S, q_off + qt * C::QB + C::QB) : S;
+      nch = (kvq + C::KTS - 1) / C::KTS;
+      if (rem < nch || qt == 0) break;
+      rem -= nch;
+      --qt;
+    }
+    c = min(rem, nch - 1);
+  } else {
+    qt = causal ? (n_qtiles - 1 - bx) : bx;  // heaviest first
+  }
   DLS_ASTAMP_DECL()
   DLS_ASTAMP(0)
   const int kvh = h / (n_head / n_kv_head);
@@ -142,6 +165,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
   // LDS-DMA source pointers: instruction j of this wave -> operand (K or V) rows
   const int kv_end = causal ? min(S, q_off + qt * C::QB + C::QB) : S;
   const int ntiles = (kv_end + C::KTS - 1) / C::KTS;
+  const int t0 = SPLIT ? c : 0, t1 = SPLIT ? c + 1 : ntiles;
   // per-lane DMA sources, computed once: instruction j of this wave covers operand op's
   // rows r0..r0+ROWS_PER_INSTR-1 of every tile; a tile only moves the base by KT rows.
   // Rows past S (the last tile) are clamped to S-1 (their scores are masked to -inf).
@@ -169,7 +193,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
   size_t dinc[C::PW];
 #pragma unroll
   for (int j = 0; j < C::PW; ++j) {
-    dptr[j] = dsrc[j] + (size_t)drow[j] * dstep[j];
+    dptr[j] = dsrc[j] + (size_t)(drow[j] + t0 * C::KTS) * dstep[j];
     dinc[j] = (size_t)C::KTS * dstep[j];
   }
   auto issue = [&](int t) {
@@ -268,15 +292,15 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
 
 #pragma unroll
   for (int p = 0; p < ST - 1; ++p)
-    if (p < ntiles) issue(p);
-  for (int t = 0; t < ntiles; ++t) {
+    if (t0 + p < t1) issue(t0 + p);
+  for (int t = t0; t < t1; ++t) {
     // tile t has landed once at most min(ST-2, tiles issued after t) tiles are in flight
-    wait_tiles<C::PW, ST - 2>(min(ST - 2, ntiles - 1 - t));
+    wait_tiles<C::PW, ST - 2>(min(ST - 2, t1 - 1 - t));
     raw_barrier();
-    if (t == 0) {
+    if (t == t0) {
       DLS_ASTAMP(1)
     }
-    if (t + ST - 1 < ntiles) issue(t + ST - 1);  // into the buffer everyone finished in t-1
+    if (t + ST - 1 < t1) issue(t + ST - 1);  // into the buffer everyone finished in t-1
     const int key0 = t * C::KTS + hg * C::KT;
     // Masks only on the wave's diagonal tile and the ragged last tile: a wave-uniform choice
     // between two instantiations of the stage (a plain branch was if-converted, so every tile
@@ -305,7 +329,7 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
       r[(C::ND * 4 + 1) * LN] = l_run;
     }
     __syncthreads();
-    if (hg != 0) return;
+    if (hg == 0) {
     float mo[KS - 1], lo_[KS - 1];
     float mm = m_run;
 #pragma unroll
@@ -331,7 +355,62 @@ __global__ __launch_bounds__(64 * NW * KS) void attn_fwd_kernel(const bf16* __re
         for (int i = 0; i < 4; ++i) o[dn][i] += r[(dn * 4 + i) * LN] * a1;
     }
     m_run = mm;
+    }
   }
+  if constexpr (SPLIT) {
+    if (nch > 1) {
+      // publish this chunk's (o, m, l) per lane of key group 0: REC2 floats, o then (m, l)
+      constexpr int REC2 = C::ND * 4 + 4;
+      constexpr int LN = C::NW * 64;
+      const int me = wave * 64 + lane;
+      const size_t tile_id = ((size_t)b * n_head + h) * n_qtiles + qt;
+      float* pp = part + tile_id * (size_t)maxc * LN * REC2;
+      const auto rp = __builtin_amdgcn_make_buffer_rsrc(pp, 0, 0x7fffffff, 0x00020000);
+      if (hg == 0) {
+        const int base = ((c * LN + me) * REC2) * 4;
+#pragma unroll
+        for (int dn = 0; dn < C::ND; ++dn)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{__float_as_uint(o[dn][0]), __float_as_uint(o[dn][1]), __float_as_uint(o[dn][2]),
+                    __float_as_uint(o[dn][3])},
+              rp, base + dn * 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(m_run), __float_as_uint(l_run)}, rp,
+                                              base + C::ND * 16, 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores landed
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == nch - 1;
+        if (last) __hip_atomic_store(cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        flag[0] = last;
+      }
+      __syncthreads();
+      if (!flag[0] || hg != 0) return;  // block-uniform, then key group 0 only
+      // the last arriver merges every other chunk of its query tile (sc1 loads: no stale copy)
+      for (int c2 = 0; c2 < nch; ++c2) {
+        if (c2 == c) continue;
+        const int base = ((c2 * LN + me) * REC2) * 4;
+        f32x4 o2[C::ND];
+#pragma unroll
+        for (int dn = 0; dn < C::ND; ++dn) {
+          const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rp, base + dn * 16, 0, 16);
+          o2[dn] = f32x4{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3])};
+        }
+        const u32x2 ml = __builtin_amdgcn_raw_buffer_load_b64(rp, base + C::ND * 16, 0, 16);
+        const float m2 = __uint_as_float(ml[0]), l2 = __uint_as_float(ml[1]);
+        const float mm = fmaxf(fmaxf(m_run, m2), -1e30f);
+        const float a0 = __builtin_amdgcn_exp2f((m_run - mm) * scale_log2);
+        const float a1 = __builtin_amdgcn_exp2f((m2 - mm) * scale_log2);
+        l_run = l_run * a0 + l2 * a1;
+        m_run = mm;
+#pragma unroll
+        for (int dn = 0; dn < C::ND; ++dn) o[dn] = o[dn] * a0 + o2[dn] * a1;
+      }
+    }
+  }
+  if (hg != 0) return;
   DLS_ASTAMP(3)
   // ---- normalise and store O[q][d]: lane holds d = 16dn + 4g + i for query my_q
   if (my_q < Sq) {
@@ -367,7 +446,27 @@ static void launch_attn(const AttnArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((attn_fwd_kernel<D, NW, ST, KS>), grid, block, 0, s, static_cast<const bf16*>(a.q), a.ldq,
                      static_cast<const bf16*>(a.k), a.ldk, static_cast<const bf16*>(a.v), a.ldv,
                      static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq, Sq,
-                     a.Sq > 0 ? a.q_off : 0, a.flags);
+                     a.Sq > 0 ? a.q_off : 0, a.flags, nullptr, nullptr, 0);
+}
+
+// SPLIT launch: one block per (query tile, key tile) item; a.part / a.cnt from the caller
+// (attention_split_sizes)
+template <int D, int NW, int ST, int KS>
+static void launch_attn_split(const AttnArgs& a, hipStream_t s) {
+  using C = AttnCfg<D, NW, ST, KS>;
+  const int Sq = a.Sq > 0 ? a.Sq : a.S, q_off = a.Sq > 0 ? a.q_off : 0;
+  const int nq = (Sq + C::QB - 1) / C::QB;
+  int items = 0;
+  for (int qt = 0; qt < nq; ++qt) {
+    const int kvq = a.causal ? std::min(a.S, q_off + qt * C::QB + C::QB) : a.S;
+    items += (kvq + C::KTS - 1) / C::KTS;
+  }
+  dim3 grid(items, a.n_head, a.B), block(64 * NW * KS);
+  const float sl2 = a.scale * 1.4426950408889634f;
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NW, ST, KS, true>), grid, block, 0, s, static_cast<const bf16*>(a.q),
+                     a.ldq, static_cast<const bf16*>(a.k), a.ldk, static_cast<const bf16*>(a.v), a.ldv,
+                     static_cast<bf16*>(a.o), a.ldo, a.S, a.n_head, a.n_kv_head, sl2, a.causal, nq, Sq, q_off,
+                     a.flags & 1, static_cast<float*>(a.part), static_cast<int*>(a.cnt), (a.S + C::KTS - 1) / C::KTS);
 }
 
 template <int D>
@@ -390,6 +489,8 @@ static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
     // four key chains per query group (D = 128: two, the LDS holds no more)
     case 12: launch_attn<D, 1, 2, (D == 64 ? 4 : 2)>(a, s); break;
     case 13: launch_attn<D, 2, 2, (D == 64 ? 4 : 2)>(a, s); break;
+    // one key tile per block, query tiles merged by their last arriver (needs a.part / a.cnt)
+    case 14: launch_attn_split<D, 2, 2, 2>(a, s); break;
     default: {
       // 64-query blocks, 2 K/V stages fill the chip from ~320 blocks on (batch 8, S=2048);
       // below that the causal row's dependent chain is the kernel time, so split each stage's
@@ -403,6 +504,15 @@ static void launch_variant(const AttnArgs& a, int v, hipStream_t s) {
       else launch_attn<D, 4, 2>(a, s);
     }
   }
+}
+
+// workspace of the split variant (14): partial floats and ticket counters
+void attention_split_sizes(const AttnArgs& a, size_t* part_floats, size_t* counters) {
+  const int D = a.D, KTS = 128, QB = 32;  // launch_attn_split<D, 2, 2, 2>: 2 x 64 keys, 2 x 16 queries
+  const int Sq = a.Sq > 0 ? a.Sq : a.S;
+  const size_t nq = (Sq + QB - 1) / QB, maxc = (a.S + KTS - 1) / KTS;
+  *counters = (size_t)a.B * a.n_head * nq;
+  *part_floats = *counters * maxc * 128 * (D / 16 * 4 + 4);
 }
 
 void launch_attention_fwd(const AttnArgs& a, hipStream_t s) {

@@ -115,8 +115,11 @@ struct AttnArgs {
   int Sq = 0;
   int q_off = 0;
   int flags = 0;  // bit 0: output stores write-through (sc1); bit 1: XCD-grouped blocks
+  void* part = nullptr;  // variant 14: fp32 partials, attention_split_sizes() floats
+  void* cnt = nullptr;   // variant 14: int32 tickets, zero before the first launch (self-resetting)
 };
 void launch_attention_fwd(const AttnArgs& a, hipStream_t s);
+void attention_split_sizes(const AttnArgs& a, size_t* part_floats, size_t* counters);
 
 // y = LN(x [+ r]) * w + b ; if r != nullptr and sum_out != nullptr, sum_out = x + r
 void launch_layernorm(const void* x, const void* r, void* sum_out, const void* w, const void* b, void* y, int M,

@@ -245,6 +245,14 @@ at::Tensor attention(const at::Tensor& q, const at::Tensor& k, const at::Tensor&
              (float)scale, causal ? 1 : 0, (int)variant, (int)Sq, (int)q_off,
              // write-through stores use 32-bit buffer offsets: not for outputs of 2 GB or more
              (int)(o.numel() * 2 < (1ll << 31) ? flags : flags & ~1)};
+  at::Tensor part;
+  if (variant == 14) {  // one key tile per block: fp32 partials + self-resetting tickets
+    size_t pf = 0, nc = 0;
+    attention_split_sizes(a, &pf, &nc);
+    part = at::empty({(int64_t)pf}, q.options().dtype(at::kFloat));
+    a.part = part.data_ptr();
+    a.cnt = split_k_counters(q, (int64_t)nc);
+  }
   launch_attention_fwd(a, cur_stream());
   return o;
 }

@@ -87,7 +87,7 @@ def test_gemm_epilogue(act):
 @pytest.mark.parametrize("B,S,nh,nkv,D,causal", [(1, 512, 12, 12, 64, True), (2, 200, 4, 4, 64, True),
                                                   (1, 256, 8, 2, 128, True), (1, 130, 4, 4, 64, False),
                                                   (1, 64, 32, 8, 128, True)])
-@pytest.mark.parametrize("variant", list(range(14)))
+@pytest.mark.parametrize("variant", list(range(15)))
 def test_attention(B, S, nh, nkv, D, causal, variant):
     qkv = _rand(B * S, (nh + 2 * nkv) * D, seed=7)
     q, k, v = qkv[:, :nh * D], qkv[:, nh * D:(nh + nkv) * D], qkv[:, (nh + nkv) * D:]
