@@ -1221,6 +1221,9 @@ using C43 = Cfg<256, 192, 4, 2, 2, 0, 1>;
 // x 256 weight columns, wave 80 x 64, split rings 2 x 20 KiB A + 3 x 32 KiB W: 80 B of operand
 // intake per output instead of 102 for 192 x 128 (the gathered A rows are re-read per column tile)
 using C44 = Cfg<160, 256, 2, 4, 2, 0, 1>;
+// GPT-2's skinny N = 768 GEMMs: 32 x 48 tiles with FOUR K groups (8 waves issuing the LDS-DMA
+// of each 256-deep super-step instead of 4): more DMA issuers per CU for the intake-bound K loop
+using C45 = Cfg<32, 48, 2, 1, 3, 0, 0, 4>;
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,

@@ -52,7 +52,7 @@ def test_gemm_identity_asymmetric():
                                            (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2),
                                            (34, 1), (35, 1), (34, 2), (34, 3), (98, 1),
                                            (36, 1), (37, 1), (36, 2), (38, 1), (38, 2), (39, 1), (40, 1), (40, 3),
-                                           (41, 1), (41, 2), (12, 3), (31, 1), (42, 1), (43, 1), (43, 4), (44, 1), (44, 2)])
+                                           (41, 1), (41, 2), (12, 3), (31, 1), (42, 1), (43, 1), (43, 4), (44, 1), (44, 2), (45, 1)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
