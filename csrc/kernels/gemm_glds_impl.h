@@ -1224,6 +1224,8 @@ using C44 = Cfg<160, 256, 2, 4, 2, 0, 1>;
 // GPT-2's skinny N = 768 GEMMs: 32 x 48 tiles with FOUR K groups (8 waves issuing the LDS-DMA
 // of each 256-deep super-step instead of 4): more DMA issuers per CU for the intake-bound K loop
 using C45 = Cfg<32, 48, 2, 1, 3, 0, 0, 4>;
+// (measured and dropped: the same tile with 2 or 4 stages, with eight K groups, and fc1 as one
+// round of 64 x 96 tiles with four K groups — profiles/r4_ab/gpt2_n768_cfg45.txt)
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,
