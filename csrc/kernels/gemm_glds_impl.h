@@ -1226,6 +1226,8 @@ using C44 = Cfg<160, 256, 2, 4, 2, 0, 1>;
 using C45 = Cfg<32, 48, 2, 1, 3, 0, 0, 4>;
 // (measured and dropped: the same tile with 2 or 4 stages, with eight K groups, and fc1 as one
 // round of 64 x 96 tiles with four K groups — profiles/r4_ab/gpt2_n768_cfg45.txt)
+// (and the MoE experts' 192 x 128 tile with two K groups, 16 waves: Mixtral 28.7 / 42.6 ms
+// with it on down / gate-up against 24.3 — profiles/r4_ab/moe_gateup_cfg44.txt)
 
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,
