@@ -89,3 +89,20 @@ def test_stream_policy_selection(monkeypatch):
     monkeypatch.setattr(ops, "WEIGHT_NT_MB", 20.0)
     assert ops._stream_pol(28672, 4096) == 5  # 235 MB gate/up weight: nt DMA + write-through
     assert ops._stream_pol(2304, 768) == 4    # 3.5 MB: below the threshold
+
+
+def test_gemm_config_tables_agree():
+    """The Python tuner's view of the LDS-DMA GEMM configs (K step per config, SwiGLU-unsafe
+    configs) matches the kernel library's tables in csrc/kernels/gemm_glds.hip."""
+    import os
+    import re
+    from distributed_llm_scheduler_amd.ops import tuning
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "csrc", "kernels", "gemm_glds.hip")).read()
+    kstep = [int(v) for v in re.search(r"kKStep\[\] = \{([^}]*)\}", src).group(1).replace("\n", " ").split(",")]
+    ncfg = int(re.search(r"constexpr int kNumCfg = (\d+);", src).group(1))
+    assert len(kstep) == ncfg == len(tuning._KSTEP)
+    assert kstep == list(tuning._KSTEP)
+    bad = re.search(r"constexpr bool swiglu_bad\(int c\) \{ return ([^;]*); \}", src).group(1)
+    lib_bad = {c for c in range(ncfg) if eval(bad.replace("&&", " and ").replace("||", " or "), {"c": c})}
+    assert lib_bad == set(tuning.SWIGLU_BAD)
