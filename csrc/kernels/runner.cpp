@@ -247,6 +247,12 @@ int64_t graph_kernel_nodes(uint64_t graph) {
   return k;
 }
 
+int64_t graph_nodes(uint64_t graph) {
+  size_t n = 0;
+  C10_HIP_CHECK(hipGraphGetNodes(reinterpret_cast<hipGraph_t>(graph), nullptr, &n));
+  return (int64_t)n;
+}
+
 }  // namespace
 
 void register_loopback(py::module& m);  // loopback.cpp
@@ -254,6 +260,7 @@ void register_loopback(py::module& m);  // loopback.cpp
 void register_runner(py::module& m) {
   register_loopback(m);
   m.def("graph_kernel_nodes", &graph_kernel_nodes);
+  m.def("graph_nodes", &graph_nodes);
   py::class_<StepRunner>(m, "StepRunner")
       .def(py::init<>())
       .def("set_process_group", &StepRunner::set_process_group)

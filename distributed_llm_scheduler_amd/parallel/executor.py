@@ -1244,7 +1244,9 @@ class DAGExecutor:
                 for k in range(i, seg_end):  # everything the segment's runs wait for, before it
                     self._pre_run(self.prog.instrs[k], recv_work, events)
                 if i in segs:
-                    if self._rec is not None:
+                    if segs[i][1] is None:
+                        pass  # an empty segment (its runs were folded into other launches)
+                    elif self._rec is not None:
                         self._rec.r.add_graph(segs[i][1].raw_cuda_graph_exec())
                     else:
                         segs[i][1].replay()
@@ -1625,6 +1627,11 @@ class DAGExecutor:
             finally:
                 g.capture_end()
             self.launches = (self.launches or 0) + ops.ext().graph_kernel_nodes(g.raw_cuda_graph())
+            if ops.ext().graph_nodes(g.raw_cuda_graph()) == 0:
+                # every run of the segment was folded into another launch (a norm written by its
+                # producer, say): nothing to replay — no graph launch per step for it
+                cur.wait_stream(cs)
+                return None
             g.instantiate()
         cur.wait_stream(cs)
         return g
