@@ -132,13 +132,13 @@ def launch_ranks(n: int) -> int:
 
 def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas, batch, seq, cost_model,
         placement, tp=1, sp=1, fuse=True, use_graph=True, init="auto", refine=False, roctx=False,
-        profile=False, trace_out=None, tag="", node_speeds=None) -> dict:
+        profile=False, trace_out=None, tag="", node_speeds=None, merge_mb=1) -> dict:
     """Plan, build the rank's executor, warm up, time ``steps`` steps bracketed by a barrier +
     device synchronize on both sides; the step time is the MAX over ranks."""
     t0 = time.time()
     plan = runtime.plan(model, world=ctx.world, scheduler=scheduler, cap_gb=cap_gb, replicas=replicas, batch=batch,
                         seq=seq, cost_model=cost_model, fuse=fuse, placement=placement, tp=tp, sp=sp,
-                        node_speeds=node_speeds)
+                        node_speeds=node_speeds, merge_mb=merge_mb)
     log(f"[bench{tag}] rank {ctx.rank}: planned {plan.stats['tasks_completed']}/{plan.stats['tasks_total']} tasks in "
         f"{(time.time() - t0) * 1e3:.1f} ms; {plan.stats}")
     dev_init = init == "device" or (init == "auto" and ctx.gpu and runtime.device_init_ok(plan, ctx.rank))
@@ -243,6 +243,10 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="headline only (no capped / strong sub-results)")
     ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of each capped / strong sub-run")
     ap.add_argument("--strong-mb", type=int, default=8, help="micro-batches of the strong-scaling pipeline run")
+    ap.add_argument("--no-strong-merge", dest="strong_merge", action="store_false",
+                    help="run the strong sub-result's micro-batches as separate M = 512 chains (not merged)")
+    ap.add_argument("--merge-mb", type=int, default=1,
+                    help="headline: merge this many request replicas into one batched request (plan merge_mb)")
     ap.add_argument("--extras-timeout", type=float, default=180.0,
                     help="seconds the capped / strong sub-results may take before the headline is printed without them")
     ap.add_argument("--profile", action="store_true", help="also print a measured per-kernel timeline")
@@ -268,8 +272,9 @@ def main():
         torch.cuda.set_device(device)
     pg = None
     if world > 1:
-        dist.init_process_group("nccl" if gpu else "gloo", rank=rank, world_size=world,
-                                **({"device_id": device} if gpu else {}))
+        from distributed_llm_scheduler_amd.parallel.comm import init_world
+
+        init_world(rank, world, device if gpu else None)  # RCCL bound to this GPU + one barrier
         pg = dist.group.WORLD
     ctx = Ctx(world, rank, device, gpu, pg)
 
@@ -283,6 +288,7 @@ def main():
                   use_graph=not args.no_graph)
     head = run(ctx, args.steps, args.warmup, scheduler=args.scheduler, cap_gb=args.cap_gb, replicas=replicas,
                cost_model=args.cost_model, placement=args.placement, tp=args.tp, sp=args.sp, init=args.init,
+               merge_mb=args.merge_mb,
                refine=args.refine_tuning, roctx=args.roctx, profile=args.profile, trace_out=args.trace_out, **common)
 
     emitted = threading.Lock()  # ONE line per job: whichever of the main thread / watchdog gets it
@@ -409,14 +415,19 @@ def main():
                 cr[sched] = {k: r[k] for k in keys}
         # strong scaling with real cross-GPU edges: a fixed batch of micro-batches, pipeline
         # placement over the N GPUs (at N = 1: the same batch on one GPU)
+        # the micro-batches are merged into one batch before placement (plan merge_mb): every
+        # stage runs each op ONCE over all 8 x 512 rows, and consecutive steps overlap through
+        # the stages; stages are balanced by measured kernel time (runtime.pipeline_stages)
+        merge = args.strong_mb if args.strong_merge else 1
         strong = {"micro_batches": args.strong_mb, "placement": f"pipeline over {world} GPU(s)", "scaling": "strong",
-                  "tokens_per_step": args.strong_mb * args.batch * args.seq}
+                  "tokens_per_step": args.strong_mb * args.batch * args.seq, "micro_batches_merged": merge}
         extras["strong"] = strong
         try:
             r = run(ctx, args.extra_steps, ew, scheduler="EFT", cap_gb=288.0, replicas=args.strong_mb,
-                    cost_model="bytes", placement="pipeline", tag=":strong", **common)
+                    cost_model="bytes", placement="pipeline", tag=":strong", merge_mb=merge, **common)
             strong.update({k: r[k] for k in ("ms_per_step", "per_rank_ms", "tasks_completed", "tasks_total",
-                                             "cross_gpu_edges", "cross_gpu_bytes", "hip_graph")})
+                                             "cross_gpu_edges", "cross_gpu_bytes", "hip_graph",
+                                             "kernel_groups_per_rank", "launches_per_rank")})
         except Exception as e:  # noqa: BLE001
             log(f"[bench] strong sub-run failed: {e!r}")
             strong["error"] = repr(e)[:300]

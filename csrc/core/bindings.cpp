@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include "../runtime/arena.h"
+#include "partition.h"
 #include "scheduler.h"
 
 namespace py = pybind11;
@@ -27,7 +28,10 @@ PYBIND11_MODULE(_dlsched_core, m) {
       .def_readwrite("link_lat", &dls::Instance::link_lat)
       .def_readwrite("load_bw", &dls::Instance::load_bw)
       .def_readwrite("cyclic", &dls::Instance::cyclic)
-      .def_readwrite("param_refill", &dls::Instance::param_refill);
+      .def_readwrite("param_refill", &dls::Instance::param_refill)
+      .def_readwrite("real_time", &dls::Instance::real_time)
+      .def_readwrite("steady", &dls::Instance::steady)
+      .def_readwrite("p2p_host", &dls::Instance::p2p_host);
 
   py::class_<dls::NodeResult>(m, "NodeResult")
       .def_readonly("available_memory", &dls::NodeResult::available_memory)
@@ -48,6 +52,12 @@ PYBIND11_MODULE(_dlsched_core, m) {
       .def_readonly("time_step", &dls::Result::time_step)
       .def_readonly("start_time", &dls::Result::start_time)
       .def_readonly("finish_time", &dls::Result::finish_time)
+      .def_readonly("cold_period", &dls::Result::cold_period)
+      .def_readonly("steady_period", &dls::Result::steady_period)
+      .def_readonly("partitioned", &dls::Result::partitioned)
+      .def_readonly("stage_node", &dls::Result::stage_node)
+      .def_readonly("stage_busy", &dls::Result::stage_busy)
+      .def_readonly("stage_refill_gb", &dls::Result::stage_refill_gb)
       .def_property_readonly("events", [](const dls::Result& r) {
         py::list out;
         for (const auto& e : r.events) out.append(py::make_tuple(e.round, e.action, e.node, e.item));
@@ -69,6 +79,33 @@ PYBIND11_MODULE(_dlsched_core, m) {
         return py::make_tuple(s, f);
       },
       py::arg("instance"), py::arg("schedule"), py::arg("with_transfers") = true);
+  py::class_<dls::Partition>(m, "Partition")
+      .def_readonly("feasible", &dls::Partition::feasible)
+      .def_readonly("period", &dls::Partition::period)
+      .def_readonly("order", &dls::Partition::order)
+      .def_readonly("node_of_task", &dls::Partition::node_of_task)
+      .def_readonly("stage_node", &dls::Partition::stage_node)
+      .def_readonly("stage_begin", &dls::Partition::stage_begin)
+      .def_readonly("stage_busy", &dls::Partition::stage_busy)
+      .def_readonly("stage_compute", &dls::Partition::stage_compute)
+      .def_readonly("stage_refill_gb", &dls::Partition::stage_refill_gb)
+      .def_readonly("stage_comm", &dls::Partition::stage_comm);
+  m.def(
+      "steady_partition",
+      [](const dls::Instance& inst, int max_stages, int min_stages) {
+        py::gil_scoped_release nogil;
+        return dls::steady_partition(inst, max_stages, min_stages);
+      },
+      py::arg("instance"), py::arg("max_stages") = -1, py::arg("min_stages") = 1);
+  m.def(
+      "steady_node_cost",
+      [](const dls::Instance& inst, const std::vector<int>& node_of_task) {
+        std::vector<double> refill;
+        std::vector<double> busy = dls::steady_node_cost(inst, node_of_task, &refill);
+        return py::make_tuple(busy, refill);
+      },
+      py::arg("instance"), py::arg("node_of_task"));
+  m.def("steady_order", &dls::steady_order);
   m.def("depth_from_sources", &dls::depth_from_sources);
   m.def("bottom_level", &dls::bottom_level);
 

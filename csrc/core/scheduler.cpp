@@ -1,6 +1,8 @@
 // Native scheduling core — see scheduler.h for the behavioural contract.
 #include "scheduler.h"
 
+#include "partition.h"
+
 #include <algorithm>
 #include <cmath>
 #include <deque>
@@ -78,6 +80,7 @@ struct Sched {
   std::vector<int> last_step;
   int time_step = 0;
   std::vector<int> name_rank;  // lexicographic rank of each param name (tie-break)
+  std::vector<int> forced;     // EFT: node per task fixed by the steady partition (empty: free)
 
   explicit Sched(const Instance& inst)
       : I(inst),
@@ -425,6 +428,7 @@ struct Sched {
       double best_fin = std::numeric_limits<double>::infinity(), best_start = 0, best_fill = 0;
       std::vector<int> best_victims;
       for (int n = 0; n < N; ++n) {
+        if (!forced.empty() && forced[t] >= 0 && forced[t] != n) continue;
         std::vector<int> victims;
         double need = requirement(t, n);
         if (need > avail[n] + kEftTol) {
@@ -577,6 +581,7 @@ void validate(const Instance& I) {
   if (I.node_mem.size() != I.node_ids.size() || I.node_speed.size() != I.node_ids.size())
     throw std::invalid_argument("node arrays have inconsistent lengths");
   if (!I.out_size.empty() && I.out_size.size() != T) throw std::invalid_argument("out_size length mismatch");
+  if (!I.real_time.empty() && I.real_time.size() != T) throw std::invalid_argument("real_time length mismatch");
   const int P = static_cast<int>(I.param_names.size());
   for (size_t t = 0; t < T; ++t) {
     for (int d : I.deps[t])
@@ -628,13 +633,44 @@ std::vector<double> bottom_level(const Instance& I) {
   return bl;
 }
 
+// EFT: the cold earliest-finish-time pass, or — when the DAG repeats (cyclic), runs on
+// several GPUs and the cold pass leaves parameter groups to re-fill every step — the
+// steady-state partition (partition.h) if its modelled step period is >= 2 % shorter. The
+// partition only fixes each task's GPU; the list scheduler then re-runs with that
+// constraint, so loads, evictions and the timeline come from the same memory accounting.
+static Result run_eft_steady(const Instance& inst) {
+  Sched cold_s(inst);
+  cold_s.run_eft();
+  Result cold = cold_s.finish();
+  const int N = static_cast<int>(inst.node_ids.size());
+  if (!inst.cyclic || !inst.steady || N < 1) return cold;
+  std::vector<double> refill;
+  std::vector<double> busy = steady_node_cost(inst, cold.assigned_node, &refill);
+  cold.cold_period = cold.steady_period = *std::max_element(busy.begin(), busy.end());
+  if (N < 2 || std::accumulate(refill.begin(), refill.end(), 0.0) <= 0.0) return cold;
+  Partition part = steady_partition(inst);
+  if (!part.feasible || !(part.period < cold.cold_period * (1.0 - 0.02))) return cold;
+  Sched s(inst);
+  s.forced = part.node_of_task;
+  s.run_eft();
+  Result r = s.finish();
+  const auto done = [](const Result& x) { return std::accumulate(x.completed.begin(), x.completed.end(), 0); };
+  if (done(r) < done(cold)) return cold;
+  busy = steady_node_cost(inst, r.assigned_node, nullptr);
+  r.cold_period = cold.cold_period;
+  r.steady_period = *std::max_element(busy.begin(), busy.end());
+  r.partitioned = true;
+  r.stage_node = part.stage_node;
+  r.stage_busy = part.stage_busy;
+  r.stage_refill_gb = part.stage_refill_gb;
+  return r;
+}
+
 Result run_policy(const Instance& inst, Policy policy) {
   validate(inst);
+  if (policy == Policy::EFT) return run_eft_steady(inst);
   Sched s(inst);
-  if (policy == Policy::EFT)
-    s.run_eft();
-  else
-    s.run_reference(policy);
+  s.run_reference(policy);
   return s.finish();
 }
 

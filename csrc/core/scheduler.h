@@ -59,6 +59,16 @@ struct Instance {
   // Optional: bytes (GB) a refill of each parameter really moves, when the budget cost
   // model differs (the reference's flat 0.5 GB per parameter). Empty = param_cost.
   std::vector<double> param_refill;
+  // Optional: real seconds per task on a speed-1.0 node (roofline of its FLOPs and bytes)
+  // for the steady-state model, when `compute` is in other units (the reference's
+  // constants). Empty = compute.
+  std::vector<double> real_time;
+  // EFT with cyclic = true: also plan the steady state (partition.h) and keep whichever of
+  // the cold pass and the steady partition has the shorter modelled step period.
+  bool steady = true;
+  // Steady-state model only: host time per p2p transfer on each end (the step runner's
+  // segment boundary at a receive, ~10-16 us measured; README "native step runner").
+  double p2p_host = 10e-6;
 };
 
 struct NodeResult {
@@ -83,6 +93,13 @@ struct Result {
   int time_step = 0;
   // EFT timeline (seconds) when Policy::EFT
   std::vector<double> start_time, finish_time;
+  // EFT steady-state model (partition.h): modelled step period of the cold pass and of the
+  // returned placement (s), whether the steady partition replaced the cold pass, and its
+  // pipeline stages (node, busy s, re-filled GB per step).
+  double cold_period = 0.0, steady_period = 0.0;
+  bool partitioned = false;
+  std::vector<int> stage_node;
+  std::vector<double> stage_busy, stage_refill_gb;
 };
 
 Result run_policy(const Instance& inst, Policy policy);

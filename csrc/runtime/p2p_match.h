@@ -52,7 +52,16 @@ class P2PMatcher {
       Entry& o = ops_.at(oid);
       Entry& s = send ? e : o;
       Entry& r = send ? o : e;
-      on_match(s.op, r.op);  // may throw (size mismatch): nothing is marked matched then
+      try {
+        on_match(s.op, r.op);  // may throw (size mismatch)
+      } catch (const std::exception& ex) {
+        // both ends fail with the real error: the counterpart was already taken off its FIFO,
+        // so its wait() must not run into the timeout and report "never matched"
+        e.error = o.error = ex.what();
+        e.matched = o.matched = true;
+        cv_.notify_all();
+        throw;
+      }
       e.matched = o.matched = true;
       ++matched_pairs_;
       cv_.notify_all();
@@ -75,6 +84,11 @@ class P2PMatcher {
                           std::chrono::duration_cast<std::chrono::system_clock::duration>(
                               std::chrono::duration<double>(timeout_s));
     if (!cv_.wait_until(lk, deadline, [&] { return ops_.at(id).matched; })) return false;
+    if (!ops_.at(id).error.empty()) {
+      const std::string err = ops_.at(id).error;
+      ops_.erase(id);
+      throw std::runtime_error("p2p: " + err);
+    }
     if (out) *out = std::move(ops_.at(id).op);
     ops_.erase(id);
     return true;
@@ -106,6 +120,7 @@ class P2PMatcher {
     Op op{};
     bool send = false, matched = false;
     int self = 0, peer = 0;
+    std::string error;  // set on both ends when the match itself failed (on_match threw)
   };
   int world_;
   std::mutex mu_;

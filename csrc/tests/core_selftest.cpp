@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <random>
 #include <set>
@@ -23,6 +24,7 @@
 
 #include "../core/scheduler.h"
 #include "../runtime/arena.h"
+#include "../core/partition.h"
 #include "../runtime/p2p_match.h"
 
 namespace {
@@ -330,6 +332,59 @@ int main(int argc, char** argv) {
     int n = 0;
     for (int t = 0; t < T; ++t) n += r.completed[t] != 0;
     CHECK(n == T, "deep chain completed %d of %d", n, T);
+  }
+  // steady-state partition of a long capped chain over 3 nodes (csrc/core/partition.h)
+  {
+    dls::Instance in;
+    const int T = 300;
+    for (int t = 0; t < T; ++t) {
+      in.task_ids.push_back("s" + std::to_string(t));
+      in.mem.push_back(0.0);
+      in.compute.push_back(1e-5 * (1 + t % 7));
+      in.out_size.push_back(1e-3);
+      in.deps.push_back(t ? std::vector<int>{t - 1} : std::vector<int>{});
+      in.params.push_back({t});
+      in.param_names.push_back("p" + std::to_string(t));
+      in.param_cost.push_back(0.5);
+      in.param_refill.push_back(0.01 * (1 + t % 3));
+    }
+    in.node_ids = {"n0", "n1", "n2"};
+    in.node_mem = {20.0, 20.0, 20.0};
+    in.node_speed = {1.0, 1.0, 1.0};
+    auto part = dls::steady_partition(in);
+    CHECK(part.feasible && part.stage_node.size() == 3, "partition: feasible over 3 stages");
+    auto busy = dls::steady_node_cost(in, part.node_of_task);
+    double mx = 0;
+    for (double b : busy) mx = std::max(mx, b);
+    CHECK(std::fabs(mx - part.period) <= 1e-12 * std::max(1.0, mx), "partition: period matches node cost");
+    auto r = dls::run_policy(in, dls::Policy::EFT);
+    CHECK(r.partitioned && r.steady_period < r.cold_period, "EFT takes the steady partition");
+  }
+  // a p2p pair whose sizes disagree: both ends fail with the real error, not a timeout
+  {
+    dls::P2PMatcher<CpuOp> m(2);
+    std::vector<float> a(4), b(5);
+    CpuOp sop, rop;
+    sop.buf = &a;
+    rop.buf = &b;
+    auto copy = [](CpuOp& s, CpuOp& r) {
+      if (s.buf->size() != r.buf->size()) throw std::runtime_error("size mismatch");
+    };
+    const int64_t sid = m.post(true, 0, 1, sop, copy);
+    bool threw = false;
+    try {
+      m.post(false, 1, 0, rop, copy);
+    } catch (const std::runtime_error&) {
+      threw = true;
+    }
+    CHECK(threw, "mismatched post throws");
+    bool peer_threw = false;
+    try {
+      m.wait(sid, 5.0);
+    } catch (const std::runtime_error& e) {
+      peer_threw = std::string(e.what()).find("size mismatch") != std::string::npos;
+    }
+    CHECK(peer_threw, "the counterpart's wait reports the size mismatch");
   }
   // the step runner's action loop over the loopback pairing: 2 / 4 / 8 rank threads
   for (int world : {2, 4, 8}) p2p_pipeline(world, 4, 257, 20);

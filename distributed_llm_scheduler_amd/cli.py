@@ -87,8 +87,9 @@ def cmd_run(a) -> int:
     if world > 1:
         if "MASTER_ADDR" not in os.environ:
             raise SystemExit("world > 1 needs torchrun (or MASTER_ADDR/MASTER_PORT/RANK/WORLD_SIZE)")
-        dist.init_process_group("nccl" if gpu else "gloo", rank=rank, world_size=world,
-                                **({"device_id": dev} if gpu else {}))
+        from .parallel.comm import init_world
+
+        init_world(rank, world, dev if gpu else None)
         pg = dist.group.WORLD
     p = _plan(a, world, resume=a.resume)
     store = runtime.make_store(p, seed=a.seed, device_init=gpu and a.init == "device" and runtime.device_init_ok(p, rank))
@@ -150,10 +151,13 @@ def cmd_simulate(a) -> int:
 
         world = int(os.environ.get("WORLD_SIZE", "1"))
         gpu = torch.cuda.is_available()
+        dev = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}") if gpu else None
         if gpu:
-            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            torch.cuda.set_device(dev)
         if world > 1:
-            dist.init_process_group("nccl" if gpu else "gloo")
+            from .parallel.comm import init_world
+
+            init_world(int(os.environ.get("RANK", "0")), world, dev)
         try:
             execute.main(a.model, a.schedulers.split(",") if a.schedulers else None,
                          tuple(float(x) for x in a.regimes.split(",")), a.steps, a.warmup, a.seq,

@@ -515,6 +515,19 @@ class EFTScheduler(BaseScheduler):
     unit of budget freed goes first, so under a flat cost the big groups stay resident.
     ``cyclic=False``: least useful first (not needed by a ready task, then oldest use). Sets
     ``start_time`` / ``finish_time`` per task (the planned, dependency-respecting timeline).
+
+    Steady state (``steady=True``, default, with ``cyclic``): the executor replays the
+    placement every step, so on N > 1 GPUs the cold pass above — which never finds an empty
+    GPU better, every parameter being loaded once anyway — would leave one GPU re-filling the
+    model's overflow every step while the others idle. When the cold pass re-fills anything,
+    the native core also plans the repeating step (csrc/core/partition.h): a min-max pipeline
+    partition of the DAG's topological order over the GPUs, stage busy = kernels
+    (``real_time``: seconds per task, default ``compute_time``) + re-filled groups over the
+    GPU's own host link + p2p edges; consecutive steps pipeline through the stages, so the
+    step period is the busiest stage. The partition is kept when its modelled period is
+    >= 2 % shorter (``cold_period`` / ``steady_period`` / ``partitioned`` / ``stages``).
+    This is the reference's one-DAG-over-N-capped-nodes experiment
+    (/root/reference/simulation.py:161-192, 375-376) planned for execution.
     """
 
     native_policy = 4
@@ -522,10 +535,15 @@ class EFTScheduler(BaseScheduler):
 
     def __init__(self, nodes, *, link_bw_gbps: float = 153.0, link_latency_s: float = 5e-6,
                  load_bw_gbps: float = 50.0, cyclic: bool = True, refill_gb: Optional[Dict[str, float]] = None,
-                 **kw):
+                 real_time: Optional[Dict[str, float]] = None, steady: bool = True, **kw):
         super().__init__(nodes, **kw)
         self.cyclic = cyclic
+        self.steady = steady
         self.refill_gb = refill_gb
+        self.real_time = real_time
+        self.cold_period = self.steady_period = 0.0
+        self.partitioned = False
+        self.stages: List[Dict] = []
         self.link_bw_gbps = link_bw_gbps
         self.link_latency_s = link_latency_s
         self.load_bw_gbps = load_bw_gbps
@@ -537,12 +555,20 @@ class EFTScheduler(BaseScheduler):
         inst.link_lat = float(self.link_latency_s)
         inst.load_bw = float(self.load_bw_gbps)
         inst.cyclic = bool(self.cyclic)
+        inst.steady = bool(self.steady)
+        if self.real_time is not None:
+            inst.real_time = [float(self.real_time.get(t, self.tasks[t].compute_time)) for t in inst.task_ids]
         if self.refill_gb is not None:
             inst.param_refill = [float(self.refill_gb.get(p, self.param_size(p))) for p in inst.param_names]
 
     def _after_native(self, res, ids, pnames):
         self.start_time = {ids[i]: s for i, s in enumerate(res.start_time) if res.completed[i]}
         self.finish_time = {ids[i]: f for i, f in enumerate(res.finish_time) if res.completed[i]}
+        self.cold_period, self.steady_period = float(res.cold_period), float(res.steady_period)
+        self.partitioned = bool(res.partitioned)
+        nids = list(self.nodes)
+        self.stages = [{"node": nids[n], "busy_s": b, "refill_gb": g}
+                       for n, b, g in zip(res.stage_node, res.stage_busy, res.stage_refill_gb)]
 
     def _schedule_python(self):
         raise RuntimeError("EFTScheduler requires the native core (distributed_llm_scheduler_amd._dlsched_core): "

@@ -102,6 +102,21 @@ class LoopComm:
         return [self.isend(b, p) if s else self.irecv(b, p) for s, b, p in ops]
 
 
+def init_world(rank: int, world: int, device=None) -> None:
+    """``init_process_group`` for an executor job: ``nccl`` (= RCCL) bound to this rank's GPU
+    with ``device_id`` (the communicator is created eagerly), ``gloo`` on the CPU; then one
+    barrier on the whole group. Programs post each point's sends / receives as ONE
+    ``batch_isend_irecv`` group, which torch documents as undefined when it is the group's first
+    collective and not every rank takes part — the barrier makes sure it never is."""
+    import torch
+    import torch.distributed as dist
+
+    gpu = device is not None and torch.device(device).type == "cuda"
+    dist.init_process_group("nccl" if gpu else "gloo", rank=rank, world_size=world,
+                            **({"device_id": torch.device(device)} if gpu else {}))
+    dist.barrier()
+
+
 def make_comm(pg):
     """The transport for an executor's ``pg`` argument (None: single rank, no p2p)."""
     if pg is None:

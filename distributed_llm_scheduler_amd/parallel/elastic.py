@@ -43,7 +43,13 @@ def _worker(rank: int, world: int, port: int, plan_kw: Dict, steps: int, device:
     dev = torch.device(f"cuda:{phys}") if gpu else torch.device("cpu")
     if gpu:
         torch.cuda.set_device(dev)
-    dist.init_process_group("nccl" if gpu else "gloo", rank=rank, world_size=world)
+    # device_id binds the NCCL (RCCL) communicator to this GPU eagerly, and the barrier runs one
+    # collective on the whole group before any step: a rank whose first p2p point posts a
+    # batch_isend_irecv group may then never be the one that initialises the communicator
+    # (undefined for a batch that is the group's first collective and not every rank's)
+    from .comm import init_world
+
+    init_world(rank, world, dev if gpu else None)
     try:
         p = runtime.plan(world=world, **plan_kw)
         store = runtime.make_store(p)

@@ -162,7 +162,9 @@ MLP_FUSED = os.environ.get("DLS_MLP_FUSED", "0") == "1"
 class DAGExecutor:
     def __init__(self, tasks: Sequence[Task], program: Program, store: ParamStore, device: torch.device,
                  model_cfg=None, use_graph: bool = True, pg=None, seed: int = 1234, autotune: bool = True,
-                 trace: bool = False, debug: bool = False, model_name: Optional[str] = None):
+                 trace: bool = False, debug: bool = False, model_name: Optional[str] = None,
+                 input_parts: Optional[Dict[str, List[str]]] = None,
+                 requests: Optional[Dict[str, Tuple[str, int, int]]] = None):
         self.tasks = {t.id: t for t in tasks}
         # the model whose per-model GEMM choices (ops/gemm_tuning.json model_overrides) this
         # executor's launches use: set around each of its steps, captures and refinements, so
@@ -179,6 +181,10 @@ class DAGExecutor:
         # replay hipGraph SEGMENTS (runs of kernel groups) between their eager RCCL / copy steps
         self.use_graph = use_graph and self.gpu
         self.seed = seed
+        # merged micro-batches (runtime.plan merge_mb): an external input made of several
+        # requests' token ids, and request prefix -> (merged prefix, batch rows) for output()
+        self.input_parts = dict(input_parts or {})
+        self.requests = dict(requests or {})
         self.trace = trace  # roctx range per instruction (eager steps; a graph replay is one range)
         self.debug = debug  # canary guards after every arena + non-finite check of outputs, per step
         self._local_consumed = None
@@ -272,7 +278,12 @@ class DAGExecutor:
                         # a sequence chunk's embedding reads its slice of the whole request
                         M = op.attrs.get("tokens_total", math.prod(op.out_shape[:-1]))
                         vocab = self.cfg.vocab_size if self.cfg is not None else 50257
-                        self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
+                        parts = self.input_parts.get(name)
+                        if parts:  # merged micro-batches: the requests' own token ids, in row order
+                            self._inputs[name] = torch.cat([synthetic_tokens(q, M // len(parts), vocab, self.seed)
+                                                            for q in parts]).to(dev)
+                        else:
+                            self._inputs[name] = synthetic_tokens(name, M, vocab, self.seed).to(dev)
         if self.gpu and STATS_HANDOFF:
             self._plan_stats_handoff()
         self._zero_in_embedding = False
@@ -991,6 +1002,12 @@ class DAGExecutor:
             W, _, bias = self._prep(w_name, None, b_name, interleave=sw, rope_perm=rope_perm)
         else:
             W, bias = self._w(w_name), (self._w(b_name) if b_name else None)
+            if w_name in self._derived_named or (w_name, W.data_ptr()) in self._derived_cache:
+                # another reader folded a norm into / reordered this weight IN PLACE (_prep): the
+                # plain GEMM would compute with W' silently (the fold decision must be
+                # the same for every reader of a shared weight, e.g. DLS_HANDOFF_MAX_K > FOLD_MAX_K
+                # with a replica whose input came from a peer without row statistics)
+                raise RuntimeError(f"{w_name}: unfolded GEMM over a weight another reader transformed in place")
         return ops.linear(x, W, bias, act=act, residual=residual, out=out, rope=rope, stats_out=stats_out)
 
     def _scratch(self, tag: str, shape) -> torch.Tensor:
@@ -1821,7 +1838,23 @@ class DAGExecutor:
         return changes
 
     def output(self, tid: str) -> torch.Tensor:
-        return self._views[tid]
+        """The output of task ``tid``; for a request merged into a micro-batch group
+        (runtime.plan merge_mb), its batch rows of the merged task's output."""
+        if tid in self._views or "/" not in tid:
+            return self._views[tid]
+        rid, base = tid.split("/", 1)
+        merged, lo, hi = self.requests[rid + "/"]
+        return self._views[merged + base][lo:hi]
+
+    def owns_output(self, tid: str) -> bool:
+        """Does this rank hold ``tid``'s output (merged requests resolved)?"""
+        if tid in self._views:
+            return True
+        if "/" in tid:
+            rid, base = tid.split("/", 1)
+            m = self.requests.get(rid + "/")
+            return m is not None and (m[0] + base) in self._views
+        return False
 
     def memory_bytes(self) -> Dict[str, int]:
         return {"activations": self.act_slab.numel(), "params": self.param_slab.numel(),

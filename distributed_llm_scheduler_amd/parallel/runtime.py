@@ -36,6 +36,20 @@ class Plan:
     cap_gb: float
     stats: Dict = field(default_factory=dict)
     args: Dict = field(default_factory=dict)  # plan() arguments (checkpoint / replan)
+    # merged micro-batches (merge_mb > 1): request prefix "r{k}/" -> (merged prefix, batch
+    # rows lo, hi) and merged token input -> the requests' token inputs, in row order
+    requests: Dict = field(default_factory=dict)
+    input_parts: Dict = field(default_factory=dict)
+
+    def owner(self, tid: str) -> Optional[int]:
+        """Rank holding task ``tid``'s output (a merged request resolves to its group)."""
+        if tid in self.placement:
+            return self.placement[tid]
+        if "/" in tid and self.requests:
+            rid, base = tid.split("/", 1)
+            m = self.requests.get(rid + "/")
+            return self.placement.get(m[0] + base) if m else None
+        return None
 
     @property
     def completed(self) -> int:
@@ -50,7 +64,7 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
          batch: int = 1, seq: int = 512, cost_model: str = "bytes", fuse: bool = True,
          node_speeds: Optional[Sequence[float]] = None, link_bw_gbps: float = 153.0,
          placement: str = "scheduler", tp: int = 1, resume: Optional[str] = None, sp: int = 1,
-         residency: Optional[str] = None) -> Plan:
+         residency: Optional[str] = None, merge_mb: int = 1) -> Plan:
     """Build the DAG of ``replicas`` requests of ``model``, place it on ``world`` GPUs with
     ``scheduler`` under a per-GPU cap of ``cap_gb`` (one value, or one per GPU — the
     reference's heterogeneous node splits) and lower it to per-rank programs.
@@ -77,6 +91,13 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     whose memory model is the repeating step (EFT) the planned keep set
     (program.plan_keep_sets) and keeps whichever re-fills fewer bytes per step.
 
+    ``merge_mb`` = k > 1: the ``replicas`` requests are micro-batches of one batch, merged k at
+    a time into one request of batch k x ``batch`` BEFORE placement (a DAG transform: every
+    node of k co-located micro-batches becomes ONE node over k x the rows — one M = k x 512
+    GEMM instead of k M = 512 launches, one p2p edge of k x the bytes instead of k). Every
+    request keeps its own token ids and its own rows of the merged outputs
+    (``Plan.requests``, ``DAGExecutor.output("r{k}/...")``).
+
     ``resume``: path of a placement saved by :func:`save_plan` — the saved decision (task
     order per GPU and the LOAD/EVICT trace) is reused instead of re-running the policy; the
     DAG is rebuilt from the saved arguments, which must match this call's.
@@ -91,7 +112,20 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
                 link_bw_gbps=link_bw_gbps, placement=placement, tp=tp)
     if sp > 1:
         args["sp"] = sp
-    tasks, groups, cfg = registry.build(model, batch=batch, seq=seq, replicas=replicas, cost_model=cost_model, tp=tp,
+    requests, input_parts = {}, {}
+    n_req, mb_batch = replicas, batch
+    if merge_mb > 1:
+        if replicas % merge_mb:
+            raise ValueError(f"merge_mb={merge_mb} must divide replicas={replicas}")
+        args["merge_mb"] = merge_mb
+        n_req, mb_batch = replicas // merge_mb, batch * merge_mb
+        for g in range(n_req):
+            pre = f"r{g}/" if n_req > 1 else ""
+            members = list(range(g * merge_mb, (g + 1) * merge_mb))
+            input_parts[f"{pre}@tokens"] = [f"r{k}/@tokens" if replicas > 1 else "@tokens" for k in members]
+            for j, k in enumerate(members):
+                requests[f"r{k}/"] = (pre, j * batch, (j + 1) * batch)
+    tasks, groups, cfg = registry.build(model, batch=mb_batch, seq=seq, replicas=n_req, cost_model=cost_model, tp=tp,
                                         sp=sp)
     param_bytes = {pid: group_layout(g)[0] for pid, g in groups.items()}
     nodes = [Node(f"gpu{r}", caps_gb[r], (node_speeds[r] if node_speeds else 1.0), device=r) for r in range(world)]
@@ -103,6 +137,8 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     if cls.__name__ == "EFTScheduler":
         kw["link_bw_gbps"] = link_bw_gbps
         kw["refill_gb"] = {pid: b / 1e9 for pid, b in param_bytes.items()}  # what a refill really moves
+        if cost_model != "bytes":  # the steady-state model needs real seconds, not abstract constants
+            kw["real_time"] = {t.id: real_time_s(t, param_bytes) for t in tasks}
     sched = cls([n.fresh() for n in nodes], **kw)
     for t in tasks:
         sched.add_task(t.clone())
@@ -111,7 +147,11 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     elif placement == "scheduler":
         schedule = sched.schedule()
     elif placement in ("replica", "pipeline", "tensor", "sequence", "expert"):
-        schedule = _fixed_schedule(tasks, world, sched, placement, cfg)
+        stage_of = None
+        if placement == "pipeline" and world > 1 and os.environ.get("DLS_PIPELINE_STAGES", "balanced") != "layers":
+            stage_of = pipeline_stages(tasks, world, param_bytes, caps_gb, node_speeds, n_req,
+                                       task_times_key(cfg.name, seq, mb_batch))
+        schedule = _fixed_schedule(tasks, world, sched, placement, cfg, stage_of)
     else:
         raise ValueError(f"unknown placement {placement!r}")
     place = {tid: node_rank[sched.tasks[tid].assigned_node] for tid in sched.completed_tasks}
@@ -137,9 +177,18 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         plan_peer_fills(programs, tasks, param_bytes)  # refills from a peer's HBM over xGMI
     name = cls.name if placement == "scheduler" else placement
     p = Plan(model, tasks, groups, cfg, name, sched, schedule, place, order, node_rank, programs, param_bytes,
-             world, cap_gb, args=args)
+             world, cap_gb, args=args, requests=requests, input_parts=input_parts)
     p.stats = plan_stats(p)
     return p
+
+
+def real_time_s(t: Task, param_bytes: Dict[str, int]) -> float:
+    """Roofline seconds of one task on one MI355X (the ``bytes`` cost model's estimate:
+    models/gpt2._roofline), whatever cost model the task's ``compute_time`` is in."""
+    from ..models.gpt2 import _roofline
+
+    moved = float(getattr(t, "out_bytes", 0) or 0) + sum(float(param_bytes.get(p, 0)) for p in t.params_needed)
+    return _roofline(float(getattr(t, "flops", 0.0) or 0.0), moved)
 
 
 _PLAN_FORMAT = "dlsched-plan/1"
@@ -213,8 +262,90 @@ def _layer_of(tid: str, n_layer: int) -> int:
     return -1 if base in ("embedding",) else n_layer
 
 
-def _fixed_schedule(tasks: Sequence[Task], world: int, sched, mode: str, cfg) -> Dict[str, List[str]]:
-    """Place without the policy: by replica (DP) or by contiguous layer blocks (PP).
+def _base_id(tid: str) -> str:
+    return tid.split("/", 1)[1] if "/" in tid and tid[0] == "r" and tid.split("/", 1)[0][1:].isdigit() else tid
+
+
+def pipeline_stages(tasks: Sequence[Task], world: int, param_bytes: Dict[str, int], caps_gb: Sequence[float],
+                    node_speeds: Optional[Sequence[float]], replicas: int, model: str) -> Optional[Dict[str, int]]:
+    """Pipeline stages balanced by kernel time (the VERDICT r4 item: layer-count blocks left
+    half the stages idle half the time): a min-max partition of ONE request's DAG over the GPUs
+    (the native steady-state partition, csrc/core/partition.h), every micro-batch's task on
+    its base task's GPU. A stage's cost per step = its tasks' kernel time x the micro-batches +
+    the p2p edges it sends and receives; cut points are the DAG's clean boundaries (the residual
+    stream alone: attention / MLP half-layers), so no fused kernel pair is split. Kernel times:
+    the measured per-task table (``ops/task_times.json``, written by
+    ``benchmarks/measure_task_times.py`` on an MI355X) when it has the model, else the roofline
+    (:func:`real_time_s`). Returns base task id -> GPU, or None (no native core / infeasible:
+    the caller keeps layer-count blocks)."""
+    from ..core import native as _native
+
+    try:
+        core = _native.load()
+    except Exception:  # noqa: BLE001 — the layer-count split still works
+        return None
+    base = [t for t in tasks if _base_id(t.id) == t.id or t.id.startswith("r0/")]
+    ids = [_base_id(t.id) for t in base]
+    index = {tid: i for i, tid in enumerate(ids)}
+    measured = measured_task_times(model)
+    R = max(int(replicas), 1)
+    pn, pidx, prow = [], {}, []
+    for t in base:
+        row = []
+        for p in sorted(t.params_needed):
+            if p not in pidx:
+                pidx[p] = len(pn)
+                pn.append(p)
+            row.append(pidx[p])
+        prow.append(row)
+    inst = core.Instance()
+    inst.task_ids = ids
+    inst.mem = [float(t.out_bytes) * R / 1e9 for t in base]
+    times = [measured.get(i, real_time_s(t, param_bytes)) if measured else real_time_s(t, param_bytes)
+             for i, t in zip(ids, base)]
+    inst.compute = [v * R for v in times]
+    inst.real_time = list(inst.compute)
+    inst.deps = [[index.get(_base_id(d), -1) for d in t.dependencies] for t in base]
+    inst.params = prow
+    inst.param_names = pn
+    inst.param_cost = [param_bytes.get(p, 0) / 1e9 for p in pn]
+    inst.param_refill = list(inst.param_cost)
+    inst.node_ids = [f"gpu{r}" for r in range(world)]
+    inst.node_mem = [float(c) for c in caps_gb]
+    inst.node_speed = [float(v) for v in node_speeds] if node_speeds else [1.0] * world
+    inst.out_size = [float(t.out_bytes) * R / 1e9 for t in base]
+    part = core.steady_partition(inst, world, world)
+    if not part.feasible:
+        return None
+    return {ids[i]: int(n) for i, n in enumerate(part.node_of_task) if n >= 0}
+
+
+_TASK_TIMES: Dict[str, Dict[str, float]] = {}
+
+
+def task_times_key(model: str, seq: int, batch: int) -> str:
+    return f"{model}/s{seq}b{batch}"
+
+
+def measured_task_times(key: str) -> Dict[str, float]:
+    """Per-task kernel seconds measured on an MI355X (base task ids; a fused kernel group's
+    time split over its tasks) for ``key`` = :func:`task_times_key`, from
+    ``ops/task_times.json``; {} if absent."""
+    if not _TASK_TIMES:
+        path = os.environ.get("DLS_TASK_TIMES") or os.path.join(os.path.dirname(__file__), "..", "ops",
+                                                                  "task_times.json")
+        try:
+            with open(path) as f:
+                _TASK_TIMES.update(json.load(f))
+        except (OSError, ValueError):
+            _TASK_TIMES["__none__"] = {}
+    return dict(_TASK_TIMES.get(key, {}))
+
+
+def _fixed_schedule(tasks: Sequence[Task], world: int, sched, mode: str, cfg,
+                    stage_of: Optional[Dict[str, int]] = None) -> Dict[str, List[str]]:
+    """Place without the policy: by replica (DP) or by contiguous pipeline stages (PP:
+    ``stage_of`` base task -> GPU from :func:`pipeline_stages`, else layer-count blocks).
     Tasks are committed in DAG order; memory is still accounted per node."""
     out: Dict[str, List[str]] = {}
     nodes = list(sched.nodes.values())
@@ -229,6 +360,8 @@ def _fixed_schedule(tasks: Sequence[Task], world: int, sched, mode: str, cfg) ->
             tag = "tp" if mode == "tensor" else "sp"
             sfx = t.id.rsplit(".", 1)[-1] if "." in t.id.split("/")[-1] else ""
             r = int(sfx[2:]) % world if sfx.startswith(tag) and sfx[2:].isdigit() else 0
+        elif stage_of is not None and _base_id(t.id) in stage_of:
+            r = stage_of[_base_id(t.id)]
         else:
             layer = min(max(_layer_of(t.id, L), 0), L - 1)
             r = min(layer * world // L, world - 1)
@@ -266,7 +399,22 @@ def plan_stats(p: Plan) -> Dict:
         "peer_fill_gb_per_step_per_rank": [sum(int(p.param_bytes.get(i.param, 0)) for i in pr.instrs
                                                if i.op == "load" and i.peer >= 0) / 1e9 for pr in p.programs],
         "tasks_per_rank": [sum(1 for r in p.placement.values() if r == k) for k in range(p.world)],
+        # distinct (producer, consumer GPU) transfers: what the p2p edges really move
+        "cross_gpu_transfers": len({(d, r) for tid, r in p.placement.items() for d in tmap[tid].dependencies
+                                    if d in p.placement and p.placement[d] != r}),
+        **_steady_stats(p.scheduler),
     }
+
+
+def _steady_stats(s) -> Dict:
+    """EFT's steady-state model (csrc/core/partition.h): modelled step period of its cold pass
+    and of the placement it returned, and whether the pipeline partition replaced the cold pass."""
+    if not hasattr(s, "steady_period") or not getattr(s, "cold_period", 0.0):
+        return {}
+    return {"eft_partitioned": bool(s.partitioned), "modelled_period_ms": round(s.steady_period * 1e3, 4),
+            "modelled_cold_period_ms": round(s.cold_period * 1e3, 4),
+            "stages": [{"node": st["node"], "busy_ms": round(st["busy_s"] * 1e3, 4),
+                        "refill_gb": round(st["refill_gb"], 6)} for st in s.stages]}
 
 
 def make_store(p: Plan, seed: int = 0, device_init: bool = False) -> ParamStore:
@@ -295,4 +443,5 @@ def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None
             raise RuntimeError("invalid plan:\n  " + "\n  ".join(errs[:20]))
     # per-model GEMM choices by the canonical preset name (aliases such as "mixtral" resolve to it)
     return DAGExecutor(p.tasks, p.programs[rank], store or make_store(p), device, model_cfg=p.cfg,
-                       use_graph=use_graph, pg=pg, trace=trace, debug=debug, model_name=p.cfg.name, autotune=autotune)
+                       use_graph=use_graph, pg=pg, trace=trace, debug=debug, model_name=p.cfg.name, autotune=autotune,
+                       input_parts=p.input_parts, requests=p.requests)

@@ -60,10 +60,13 @@ def _execute_main(a):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     gpu = torch.cuda.is_available()
+    dev = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}") if gpu else None
     if gpu:
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl" if gpu else "gloo")
+        from distributed_llm_scheduler_amd.parallel.comm import init_world
+
+        init_world(int(os.environ.get("RANK", "0")), world, dev)
     try:
         return execute.main(a.model, a.schedulers.split(",") if a.schedulers else None,
                             tuple(float(x) for x in a.regimes.split(",")), a.steps, a.warmup, a.seq,

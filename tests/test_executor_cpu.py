@@ -136,11 +136,12 @@ def test_two_ranks_gloo(placement, scheduler):
         assert sum(r["sends"] for r in results) > 0 and sum(r["recvs"] for r in results) > 0
 
 
-def test_three_ranks_pipeline_reuses_sent_buffers():
+def test_three_ranks_pipeline_reuses_sent_buffers(monkeypatch):
     """GPT-2 on 3 ranks, pipeline placement, 3 micro-batches: rank 1 receives
     r1/layer_3_output into bytes of r0/layer_7_output that are still being sent to rank 2
     (the plan's recv carries a wait for that send); every request's logits must match the
     fp32 reference."""
+    monkeypatch.setenv("DLS_PIPELINE_STAGES", "layers")  # the layer-count split makes this buffer reuse
     world, replicas = 3, 3
     p = runtime.plan("gpt2", world=world, seq=64, batch=1, replicas=replicas, placement="pipeline")
     assert any(ins.op == "recv" and ins.wait_sends for pr in p.programs for ins in pr.instrs)

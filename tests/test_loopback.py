@@ -20,11 +20,16 @@ from distributed_llm_scheduler_amd.parallel.loopback import run_loopback
 # (model, plan kwargs, output task ids): every placement whose programs carry p2p edges
 CASES = {
     "pipeline": ("tiny-gpt2", dict(placement="pipeline", replicas=2), ["r0/output_projection", "r1/output_projection"]),
+    # the same micro-batches merged into ONE batch-2 request before placement (plan merge_mb)
+    "pipeline_merged": ("tiny-gpt2", dict(placement="pipeline", replicas=2, merge_mb=2),
+                        ["r0/output_projection", "r1/output_projection"]),
     "tensor": ("tiny-llama", dict(placement="tensor", tp=2), ["output_projection"]),
     "sequence": ("tiny-gpt2", dict(placement="sequence", sp=2), None),
     "expert": ("tiny-mixtral", dict(placement="expert", replicas=1), ["output_projection"]),
     # the reference's experiment: ONE DAG over the nodes under its 80 % regime (bench.py capped)
     "capped_one_dag": ("tiny-gpt2", dict(scheduler="MRU_spec", regime=0.8), ["output_projection"]),
+    # the same experiment placed by EFT's steady-state partition (a pipeline of capped stages)
+    "capped_eft": ("tiny-gpt2", dict(scheduler="EFT", regime=0.8), ["output_projection"]),
     # capped replicas: steady-state refills of a group a peer holds come from the peer's HBM
     # (program.plan_peer_fills, the xGMI path); the cap is a fraction of the model's parameters
     "peer_fill": ("tiny-gpt2", dict(replicas="world", cap_frac=0.7, cost_model="bytes"), "replicas"),
@@ -60,7 +65,7 @@ def _p2p_work(p):
 def _logits(p, run, ids):
     """{request prefix: [B, S, V] logits}, gathered from whichever rank produced them."""
     def out(tid):
-        return run.executors[p.placement[tid]].output(tid).float().cpu()
+        return run.executors[p.owner(tid)].output(tid).float().cpu()
     if ids is None:  # sequence chunks: the request's logits are the chunks' rows in order
         P = sum(1 for t in p.tasks if t.id.startswith("output_projection.sp"))
         return {"": torch.cat([out(f"output_projection.sp{c}") for c in range(P)], dim=1)}

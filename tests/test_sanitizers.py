@@ -11,7 +11,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRCS = ["csrc/tests/core_selftest.cpp", "csrc/core/scheduler.cpp", "csrc/runtime/arena.cpp"]
+SRCS = ["csrc/tests/core_selftest.cpp", "csrc/core/scheduler.cpp", "csrc/core/partition.cpp", "csrc/runtime/arena.cpp"]
 HDRS = ["csrc/core/scheduler.h", "csrc/runtime/arena.h", "csrc/runtime/p2p_match.h"]
 FLAGS = {
     "asan": ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],

@@ -102,9 +102,10 @@ def test_debug_executor_guards_and_validation():
         runtime.make_executor(bad, 0, "cpu", debug=True)
 
 
-def test_recv_into_inflight_send_buffer_waits():
+def test_recv_into_inflight_send_buffer_waits(monkeypatch):
     """The pipeline plan that reuses a sent buffer for a recv from another peer: the recv
     carries a planned wait for that send, and dropping the wait is flagged."""
+    monkeypatch.setenv("DLS_PIPELINE_STAGES", "layers")  # the layer-count split makes this buffer reuse
     p = runtime.plan("gpt2", world=3, placement="pipeline", replicas=3, seq=64)
     hits = [(pr.rank, i) for pr in p.programs for i, ins in enumerate(pr.instrs) if ins.op == "recv" and ins.wait_sends]
     assert hits, "expected a recv that reuses an in-flight send buffer"
