@@ -31,7 +31,8 @@ PYBIND11_MODULE(_dlsched_core, m) {
       .def_readwrite("param_refill", &dls::Instance::param_refill)
       .def_readwrite("real_time", &dls::Instance::real_time)
       .def_readwrite("steady", &dls::Instance::steady)
-      .def_readwrite("p2p_host", &dls::Instance::p2p_host);
+      .def_readwrite("p2p_host", &dls::Instance::p2p_host)
+      .def_readwrite("fuse_into", &dls::Instance::fuse_into);
 
   py::class_<dls::NodeResult>(m, "NodeResult")
       .def_readonly("available_memory", &dls::NodeResult::available_memory)

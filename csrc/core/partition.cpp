@@ -219,9 +219,23 @@ Partition steady_partition(const Instance& I, int max_stages, int min_stages) {
   for (int i = 1; i <= T; ++i) crossing[i] += crossing[i - 1];
   int min_cross = std::numeric_limits<int>::max();
   for (int i = 1; i < T; ++i) min_cross = std::min(min_cross, crossing[i]);
-  std::vector<char> clean(T + 1, 0);
+  // cuts that would split a fused kernel chain (Instance::fuse_into) are never taken
+  std::vector<int> splits(T + 2, 0);
+  if (I.fuse_into.size() == static_cast<size_t>(M.T))
+    for (int t = 0; t < M.T; ++t) {
+      const int c = I.fuse_into[t];
+      if (c < 0 || pos[t] < 0 || pos[c] < 0) continue;
+      const int lo = std::min(pos[t], pos[c]), hi = std::max(pos[t], pos[c]);
+      ++splits[lo + 1];
+      --splits[hi + 1];
+    }
+  for (int i = 1; i <= T; ++i) splits[i] += splits[i - 1];
+  std::vector<char> allowed(T + 1, 1), clean(T + 1, 0);
   clean[0] = 1;
-  for (int i = 1; i < T; ++i) clean[i] = crossing[i] <= min_cross;
+  for (int i = 1; i < T; ++i) {
+    allowed[i] = splits[i] == 0;
+    clean[i] = allowed[i] && crossing[i] <= min_cross;
+  }
 
   // cost[n][i*(T+1)+j]: busy time of stage [i, j) on node n (distinct nodes only)
   std::vector<int> rep(N);  // node -> representative node with the same cap and speed
@@ -304,10 +318,23 @@ Partition steady_partition(const Instance& I, int max_stages, int min_stages) {
   by([&](int a, int b) { return I.node_mem[a] < I.node_mem[b]; });
   by([&](int a, int b) { return M.speed(a) > M.speed(b); });
 
+  // Two passes: clean cuts only, then every cut that splits no fused chain; the second pass
+  // (multi-producer cuts: more transfers, already in the edge costs) is taken only for a >= 3 %
+  // shorter period, or when the clean cuts cannot make a feasible partition.
   double best = kInf;
   int best_k = 0;
   std::vector<int> best_cuts, best_nodes;
-  for (int only_clean = 1; only_clean >= 0 && best_k == 0; --only_clean)
+  double clean_best = kInf;
+  // (without fusion chains (Instance::fuse_into) any non-clean cut may split a fused kernel
+  // pair, so the finer pass only runs when the clean cuts are infeasible)
+  const bool know_fusion = I.fuse_into.size() == static_cast<size_t>(M.T);
+  for (int only_clean = 1; only_clean >= 0; --only_clean) {
+  if (!only_clean && !know_fusion && best_k > 0) break;
+  if (!only_clean) {
+    clean_best = best;
+    if (std::isfinite(best)) best *= 0.97;  // what the finer cuts must beat
+  }
+  const std::vector<char>& cut_ok = only_clean ? clean : allowed;
   for (const auto& o : orders) {
     // f[k][j]: min over cuts of the max stage busy covering positions [0, j) with k stages
     // (ties on the max: the smaller sum of squared stage times, i.e. the non-bottleneck
@@ -322,7 +349,7 @@ Partition steady_partition(const Instance& I, int max_stages, int min_stages) {
         double bv = kInf, bg = kInf;
         int bi = -1;
         for (int i = k - 1; i < j; ++i) {
-          if (std::isinf(f[k - 1][i]) || (only_clean && !clean[i])) continue;
+          if (std::isinf(f[k - 1][i]) || !cut_ok[i]) continue;
           const double cij = c[i * W + j];
           const double v = std::max(f[k - 1][i], cij);
           const double sq = g[k - 1][i] + cij * cij;
@@ -354,9 +381,10 @@ Partition steady_partition(const Instance& I, int max_stages, int min_stages) {
       best_nodes.assign(o.begin(), o.begin() + k);
     }
   }
+  }
   if (best_k == 0) return out;
+  (void)clean_best;
   out.feasible = true;
-  out.period = best;
   out.node_of_task.assign(M.T, -1);
   for (int s = 0; s < best_k; ++s) {
     const int a = best_cuts[s], b = best_cuts[s + 1], n = best_nodes[s];
@@ -369,6 +397,7 @@ Partition steady_partition(const Instance& I, int max_stages, int min_stages) {
     out.stage_refill_gb.push_back(refill_tab[rep[n]][ij]);
     out.stage_comm.push_back(comm_tab[ij]);
   }
+  out.period = *std::max_element(out.stage_busy.begin(), out.stage_busy.end());
   out.stage_begin.push_back(T);
   return out;
 }

@@ -69,6 +69,9 @@ struct Instance {
   // Steady-state model only: host time per p2p transfer on each end (the step runner's
   // segment boundary at a receive, ~10-16 us measured; README "native step runner").
   double p2p_host = 10e-6;
+  // Steady-state model only (optional): task -> the task whose fused kernel it runs in when
+  // co-located (program lowering's fusion chains), -1 = none. A pipeline cut never splits one.
+  std::vector<int> fuse_into;
 };
 
 struct NodeResult {

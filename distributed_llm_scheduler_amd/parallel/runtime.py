@@ -314,6 +314,13 @@ def pipeline_stages(tasks: Sequence[Task], world: int, param_bytes: Dict[str, in
     inst.node_mem = [float(c) for c in caps_gb]
     inst.node_speed = [float(v) for v in node_speeds] if node_speeds else [1.0] * world
     inst.out_size = [float(t.out_bytes) * R / 1e9 for t in base]
+    # fused kernel chains of the lowering (program._fusion): a stage cut never splits one
+    from .program import _consumers, _fusion
+    tmap = {t.id: t for t in base}
+    one = {t.id: 0 for t in base}
+    order = [t.id for t in base]
+    fused_into, _ = _fusion(tmap, one, order, _consumers(tmap, one, order), {t: i for i, t in enumerate(order)}, True)
+    inst.fuse_into = [index[_base_id(fused_into[t.id])] if t.id in fused_into else -1 for t in base]
     part = core.steady_partition(inst, world, world)
     if not part.feasible:
         return None
@@ -330,7 +337,8 @@ def task_times_key(model: str, seq: int, batch: int) -> str:
 def measured_task_times(key: str) -> Dict[str, float]:
     """Per-task kernel seconds measured on an MI355X (base task ids; a fused kernel group's
     time split over its tasks) for ``key`` = :func:`task_times_key`, from
-    ``ops/task_times.json``; {} if absent."""
+    ``ops/task_times.json``; a batch the table lacks is scaled from batch 1 (an upper bound:
+    bigger GEMMs run closer to peak); {} if absent."""
     if not _TASK_TIMES:
         path = os.environ.get("DLS_TASK_TIMES") or os.path.join(os.path.dirname(__file__), "..", "ops",
                                                                   "task_times.json")
@@ -339,7 +347,12 @@ def measured_task_times(key: str) -> Dict[str, float]:
                 _TASK_TIMES.update(json.load(f))
         except (OSError, ValueError):
             _TASK_TIMES["__none__"] = {}
-    return dict(_TASK_TIMES.get(key, {}))
+    if key in _TASK_TIMES:
+        return dict(_TASK_TIMES[key])
+    head, _, b = key.rpartition("b")
+    if b.isdigit() and int(b) > 1 and (head + "b1") in _TASK_TIMES:
+        return {t: v * int(b) for t, v in _TASK_TIMES[head + "b1"].items()}
+    return {}
 
 
 def _fixed_schedule(tasks: Sequence[Task], world: int, sched, mode: str, cfg,
