@@ -144,7 +144,8 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     dev_init = init == "device" or (init == "auto" and ctx.gpu and runtime.device_init_ok(plan, ctx.rank))
     store = runtime.make_store(plan, device_init=dev_init)
     t0 = time.time()
-    ex = runtime.make_executor(plan, ctx.rank, ctx.device, store, pg=ctx.pg, use_graph=use_graph, trace=roctx)
+    pg = runtime.p2p_group(plan, ctx.rank, ctx.device, ctx.pg) if ctx.gpu else ctx.pg  # DLS_P2P=device: kernels
+    ex = runtime.make_executor(plan, ctx.rank, ctx.device, store, pg=pg, use_graph=use_graph, trace=roctx)
     log(f"[bench{tag}] rank {ctx.rank}: executor ready in {(time.time() - t0):.1f} s (device_init={dev_init})")
     for _ in range(warmup):
         ex.step()
@@ -185,6 +186,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
         "hip_graph": bool(captured),
         # segment-replayed programs (p2p or copy-stream refills): native runner or Python loop
         "issue_mode": ex.issue_mode or ("graph" if captured else "python"),
+        "p2p": getattr(getattr(ex, "comm", None), "kind", None),
     }
     if profile or trace_out:
         s = ex.step(profile=True)

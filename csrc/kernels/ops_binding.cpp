@@ -698,10 +698,12 @@ at::Tensor alloc_device(int64_t nbytes, int64_t flags) {
 }
 
 void register_runner(py::module& m);  // runner.cpp
+void register_p2p(py::module& m);     // p2p_binding.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Hand-written HIP/CDNA4 (gfx950) kernels for distributed_llm_scheduler_amd";
   register_runner(m);
+  register_p2p(m);
   m.def("alloc_device", &alloc_device, py::arg("nbytes"), py::arg("flags") = 3);
   m.def("host_pull", &host_pull, py::arg("dst"), py::arg("src"), py::arg("blocks") = 256);
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),

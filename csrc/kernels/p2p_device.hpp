@@ -1,0 +1,27 @@
+// Device-initiated point-to-point transport (p2p_device.hip): DAG edges moved by kernels on the
+// ranks' own streams, so a step with cross-GPU edges captures into ONE hipGraph per rank.
+//
+// Protocol per edge (producer P -> consumer C, one slot per edge, values = the step number):
+//   P, in stream order after the producing kernel:   ready[slot]@C  = step      (notify)
+//   C, at the consumer:  wait ready[slot] >= step, copy P's region -> C's region (pull, over
+//                        xGMI when P is another GPU), then ack[slot]@P = step
+//   P, before overwriting the sent region again:     wait ack[slot] >= step    (wait)
+// Every rank bumps its own step counter at the start of a step (tick), so the same captured
+// graph replays with fresh sequence numbers. A wait that does not see its flag within the
+// timeout sets an error word and gives up (wrong data, never a hung GPU); the host checks it.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+void launch_p2p_tick(int64_t* step, hipStream_t s);
+void launch_p2p_notify(int64_t* remote_flag, const int64_t* step, hipStream_t s);
+// dst <- src (bytes % 16 == 0, both 16-B aligned) once *ready >= *step; then ack_remote = step.
+// `ticket` counts arriving workgroups (monotonic; its launches always use the same grid).
+void launch_p2p_pull(const void* src, void* dst, int64_t bytes, const int64_t* ready, int64_t* ack_remote,
+                     unsigned* ticket, const int64_t* step, int* err, int64_t timeout_ticks, int blocks,
+                     hipStream_t s);
+void launch_p2p_wait(const int64_t* flag, const int64_t* step, int* err, int64_t timeout_ticks, int code,
+                     hipStream_t s);
+int p2p_pull_blocks(int64_t bytes);

@@ -75,10 +75,14 @@ class DistComm:
 
 
 class LoopbackGroup:
-    """What a loopback rank's executor gets as ``pg``: the shared hub and this rank."""
+    """What a loopback rank's executor gets as ``pg``: the shared hub, this rank, and the
+    job-wide lock that makes a coalesced group's posts visible to the peers all at once."""
 
-    def __init__(self, hub, rank: int, world: int):
+    def __init__(self, hub, rank: int, world: int, group_lock=None):
+        import threading
+
         self.hub, self.rank, self.world = hub, rank, world
+        self.group_lock = group_lock or threading.Lock()
 
     def size(self) -> int:
         return self.world
@@ -99,7 +103,17 @@ class LoopComm:
         return _HubWork(self.hub, self.hub.post(False, buf, self.rank, peer), buf)
 
     def batch(self, ops: Sequence[Tuple[bool, torch.Tensor, int]]) -> List[object]:
-        return [self.isend(b, p) if s else self.irecv(b, p) for s, b, p in ops]
+        """ONE group, as ``ncclGroupStart/End``: every op of it is posted under the job-wide group
+        lock, so no peer matches against a partly posted group (a peer's post sees all of the
+        group's ops or none), and — as with RCCL's coalesced group — the group's single work
+        completes when every op has: waiting for any op waits for the whole group."""
+        if len(ops) == 1:
+            s, b, p = ops[0]
+            return [self.isend(b, p) if s else self.irecv(b, p)]
+        with self.g.group_lock:
+            works = [self.isend(b, p) if s else self.irecv(b, p) for s, b, p in ops]
+        g = _GroupWork(works)
+        return [g] * len(ops)
 
 
 def init_world(rank: int, world: int, device=None) -> None:
@@ -123,6 +137,10 @@ def make_comm(pg):
         return None
     if isinstance(pg, LoopbackGroup):
         return LoopComm(pg)
+    from .devp2p import DeviceComm, DeviceP2PGroup
+
+    if isinstance(pg, DeviceP2PGroup):
+        return DeviceComm(pg)
     return DistComm(pg)
 
 
@@ -130,5 +148,8 @@ def loopback_groups(world: int, delay_us: float = 20.0, poison: bool = True, tim
     """One :class:`LoopbackGroup` per rank of a ``world``-rank job living in this process."""
     from .. import ops
 
+    import threading
+
     hub = ops.ext().LoopbackHub(world, delay_us, poison, timeout_s)
-    return [LoopbackGroup(hub, r, world) for r in range(world)]
+    lock = threading.Lock()
+    return [LoopbackGroup(hub, r, world, lock) for r in range(world)]

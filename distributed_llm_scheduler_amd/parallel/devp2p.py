@@ -1,0 +1,257 @@
+"""Device-initiated p2p transport: DAG edges moved by KERNELS on the ranks' own streams.
+
+RCCL's send / recv are host-issued operations the executor cannot capture, so a multi-GPU step
+is cut into hipGraph segments at every receive and replayed by the native runner (≈10-16 µs of
+host time per segment). Here every edge is three small kernels instead (csrc/kernels/
+p2p_device.hpp):
+
+  producer P, after the producing kernel:  notify  — ready[slot] on the consumer := step
+  consumer C, before the first consumer:   pull    — wait ready[slot] >= step, copy P's region
+                                                     into C's (over xGMI when P is another GPU),
+                                                     then ack[slot] on P := step
+  P, before its region is written again:   wait    — ack[slot] >= step
+
+plus one ``tick`` per step that bumps the rank's step counter, so a rank's WHOLE step — kernels
+and edges — captures into ONE hipGraph and replays with fresh sequence numbers. Nothing pairs
+transfers on the host: a message's slot is a pure function of the plan (:func:`edge_slots`),
+the source address of a pull is the producer's arena base plus the offset its program gives
+the region, and the flags live in each rank's mailbox (uncached device memory).
+
+Ranks sharing a process (the single-GPU harness, parallel/loopback.py ``transport="device"``)
+address each other's arenas directly; separate processes exchange IPC handles of their arenas
+and mailboxes once (:meth:`DeviceP2PWorld.exchange`). A wait that does not see its flag within
+``DLS_P2P_TIMEOUT_S`` sets the rank's error word and gives up — wrong numbers, never a hung
+GPU; :meth:`DeviceComm.errors` reads it.
+
+Ordering matches RCCL's p2p contract (the programs validated for it need nothing new): a send
+never blocks (notify is a flag store), a receive completes before its first consumer, a sent
+region is written again only after its consumer pulled it.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+TIMEOUT_S = float(os.environ.get("DLS_P2P_TIMEOUT_S", "10"))
+_TICKS = int(TIMEOUT_S * 1e8)  # wall_clock64 runs at 100 MHz
+ERR_PULL, ERR_ACK = 1, 2
+
+
+def edge_slots(programs) -> Dict[Tuple[int, int, tuple], int]:
+    """Slot of every cross-rank message of a step, from the programs alone (the same on every
+    rank): key (src rank, dst rank, what), what = ("act", task) for a DAG edge or ("param",
+    group, gpos) for a parameter group filled from a peer (program.plan_peer_fills)."""
+    slots: Dict[Tuple[int, int, tuple], int] = {}
+    for pr in programs:
+        for ins in pr.instrs:
+            if ins.op == "send":
+                key = (pr.rank, ins.peer, ("act", ins.task))
+            elif ins.op == "psend":
+                key = (pr.rank, ins.peer, ("param", ins.param, ins.gpos))
+            else:
+                continue
+            if key in slots:
+                raise ValueError(f"device p2p: message {key} sent twice in one step")
+            slots[key] = len(slots)
+    return slots
+
+
+def source_regions(programs, param_bytes: Dict[str, int]) -> Dict[Tuple[int, int, tuple], Tuple[str, int, int]]:
+    """Where each message's bytes sit on its producer: key -> (arena "act" | "param", offset,
+    bytes) — the producer's program fixes every region, so a consumer computes its pull's
+    source address from the producer's arena base alone."""
+    out = {}
+    for pr in programs:
+        for ins in pr.instrs:
+            if ins.op == "send":
+                out[(pr.rank, ins.peer, ("act", ins.task))] = ("act", pr.act_offset[ins.task], pr.act_bytes[ins.task])
+            elif ins.op == "psend":
+                out[(pr.rank, ins.peer, ("param", ins.param, ins.gpos))] = (
+                    "param", ins.param_off, int(param_bytes.get(ins.param, 0)))
+    return out
+
+
+class Mailbox:
+    """One rank's flags: int64 [step, ready[S], ack[S]], int32 tickets[S] and an error word, in
+    uncached device memory (polled by one lane, written by peers)."""
+
+    def __init__(self, n_slots: int, device):
+        from .. import ops
+
+        self.S = n_slots
+        n64 = 1 + 2 * n_slots
+        n32 = n_slots + 1
+        nbytes = (n64 * 8 + n32 * 4 + 255) // 256 * 256
+        self.raw = ops.ext().alloc_device(nbytes, 3)  # hipDeviceMallocUncached
+        self.raw.zero_()
+        i64 = self.raw[:n64 * 8].view(torch.int64)
+        i32 = self.raw[n64 * 8:n64 * 8 + n32 * 4].view(torch.int32)
+        self.step = i64[0:1]
+        self.ready = i64[1:1 + n_slots]
+        self.ack = i64[1 + n_slots:1 + 2 * n_slots]
+        self.tickets = i32[:n_slots]
+        self.err = i32[n_slots:n_slots + 1]
+        self.base = self.raw.data_ptr()
+
+    def ready_addr(self, base: int, slot: int) -> int:
+        return base + 8 * (1 + slot)
+
+    def ack_addr(self, base: int, slot: int) -> int:
+        return base + 8 * (1 + self.S + slot)
+
+
+class DeviceP2PWorld:
+    """The transport state a job shares: message slots, source regions and every rank's
+    addresses (arena bases, mailbox). ``local_ranks``: the ranks living in this process (all of
+    them for the single-GPU harness, one for a process-per-GPU job)."""
+
+    def __init__(self, plan, device, local_ranks: Sequence[int], delay_us: float = 0.0, poison: bool = False):
+        self.world = plan.world
+        self.device = torch.device(device)
+        self.slots = edge_slots(plan.programs)
+        self.sources = source_regions(plan.programs, plan.param_bytes)
+        self.delay_us, self.poison = float(delay_us), bool(poison)
+        self.mail = {r: Mailbox(len(self.slots), self.device) for r in local_ranks}
+        self.bases: Dict[int, Dict[str, int]] = {}  # rank -> {"act", "param", "mail"} addresses here
+        self._opened: List[int] = []
+        self._exported: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    def attach(self, rank: int, act: torch.Tensor, param: torch.Tensor) -> None:
+        self.bases[rank] = {"act": act.data_ptr(), "param": param.data_ptr(), "mail": self.mail[rank].base}
+        self._exported[rank] = {"act": act, "param": param, "mail": self.mail[rank].raw}
+
+    def exchange(self, pg) -> None:
+        """Process-per-GPU job: publish this process's arenas and mailbox as IPC handles and open
+        every peer's (one collective, at executor construction)."""
+        import torch.distributed as dist
+
+        from .. import ops
+
+        e = ops.ext()
+        mine = {r: {k: e.ipc_handle(t) for k, t in d.items()} for r, d in self._exported.items()}
+        allh: List[Optional[dict]] = [None] * dist.get_world_size(pg)
+        dist.all_gather_object(allh, mine, group=pg)
+        for d in allh:
+            for r, hs in (d or {}).items():
+                if r in self.bases:
+                    continue
+                addr = {}
+                for k, (h, off) in hs.items():
+                    base = e.ipc_open(h)
+                    self._opened.append(base)
+                    addr[k] = base + off
+                self.bases[r] = addr
+
+    def close(self) -> None:
+        from .. import ops
+
+        for b in self._opened:
+            try:
+                ops.ext().ipc_close(b)
+            except RuntimeError:
+                pass
+        self._opened = []
+
+
+class DeviceP2PGroup:
+    """What a rank's executor gets as ``pg`` for the device transport."""
+
+    def __init__(self, world: DeviceP2PWorld, rank: int, pg=None):
+        self.world, self.rank, self.pg = world, rank, pg
+
+    def size(self) -> int:
+        return self.world.world
+
+
+class _SendWork:
+    __slots__ = ("comm", "slot", "done")
+
+    def __init__(self, comm, slot: int):
+        self.comm, self.slot, self.done = comm, slot, False
+
+    def wait(self):
+        if not self.done:
+            self.done = True
+            m = self.comm.mb
+            self.comm.e.p2p_wait(m.ack[self.slot:self.slot + 1], m.step, m.err, _TICKS, ERR_ACK)
+
+
+class _RecvWork:
+    __slots__ = ("comm", "slot", "buf", "src", "done")
+
+    def __init__(self, comm, slot: int, buf: torch.Tensor, src: Tuple[int, str, int]):
+        self.comm, self.slot, self.buf, self.src, self.done = comm, slot, buf, src, False
+
+    def wait(self):
+        if not self.done:
+            self.done = True
+            c = self.comm
+            peer, arena, off = self.src
+            pb = c.w.bases[peer]
+            m = c.mb
+            c.e.p2p_pull(pb[arena] + off, self.buf, m.ready[self.slot:self.slot + 1],
+                         m.ack_addr(pb["mail"], self.slot), m.tickets[self.slot:self.slot + 1], m.step, m.err,
+                         _TICKS)
+
+
+class DeviceComm:
+    kind = "device"
+
+    def __init__(self, group: DeviceP2PGroup):
+        from .. import ops
+
+        self.w = group.world
+        self.rank = group.rank
+        self.pg = group.pg
+        self.mb = self.w.mail[self.rank]
+        self.e = ops.ext()
+
+    def attach(self, ex) -> None:
+        """Register the executor's arenas (their base addresses are what peers pull from)."""
+        self.w.attach(self.rank, ex.act_slab, ex.param_slab)
+        if self.pg is not None:
+            self.w.exchange(self.pg)
+
+    def begin_step(self) -> None:
+        self.e.p2p_tick(self.mb.step)
+
+    def _slot(self, src: int, dst: int, key) -> int:
+        try:
+            return self.w.slots[(src, dst, key)]
+        except KeyError:
+            raise RuntimeError(f"device p2p: no message {key} from rank {src} to rank {dst} in the plan") from None
+
+    def isend(self, buf: torch.Tensor, peer: int, key=None):
+        slot = self._slot(self.rank, peer, key)
+        if self.w.delay_us > 0:  # single-GPU harness: the notify lands late (a missing wait shows)
+            self.e.p2p_delay(self.w.delay_us, self.mb.step)
+        self.e.p2p_notify(self.mb.ready_addr(self.w.bases[peer]["mail"], slot), self.mb.step)
+        return _SendWork(self, slot)
+
+    def irecv(self, buf: torch.Tensor, peer: int, key=None):
+        slot = self._slot(peer, self.rank, key)
+        arena, off, nbytes = self.w.sources[(peer, self.rank, key)]
+        # ``buf``: the receiver's whole region for the message (uint8, as its program sized it)
+        region = buf.view(torch.uint8) if buf.is_contiguous() and buf.dim() == 1 else None
+        if region is None or region.numel() != nbytes:
+            raise RuntimeError(f"device p2p: receive region of {key} does not match the producer's "
+                               f"({None if region is None else region.numel()} vs {nbytes} bytes)")
+        if self.w.poison:
+            region.fill_(0xFF)  # bf16 NaN until the pull lands
+        return _RecvWork(self, slot, region, (peer, arena, off))
+
+    def batch(self, ops_: Sequence[Tuple[bool, torch.Tensor, int, object]]) -> List[object]:
+        return [self.isend(b, p, k) if s else self.irecv(b, p, k) for s, b, p, k in ops_]
+
+    def reset_errors(self) -> None:
+        """Clear the error word (after warm-up: a first step's lazy code-object loading on one
+        rank can outlast a peer's wait; sequence numbers are monotonic, so the protocol itself
+        recovers on the next step)."""
+        self.mb.err.zero_()
+
+    def errors(self) -> int:
+        """The rank's error word (host read: synchronises): bit 0 a pull, bit 1 an ack wait
+        timed out."""
+        return int(self.mb.err.item())

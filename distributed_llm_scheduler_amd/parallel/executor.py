@@ -232,6 +232,8 @@ class DAGExecutor:
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._setup()
+        if self._device_p2p:
+            self.comm.attach(self)  # peers pull from this rank's arenas (IPC exchange across processes)
         if autotune and self.gpu:
             _tuning.set_model(self.model_name)
             _tuning.ensure_tuned(self.gemm_shapes(), self.device)
@@ -303,6 +305,7 @@ class DAGExecutor:
         self._rec: Optional[_Recorder] = None   # set while a step is recorded for the runner
         self._runner = None                     # native StepRunner replaying the recorded step
         self.issue_mode: Optional[str] = None  # "runner" / "python" for segment-replayed programs
+        self._graph_exec: Optional[int] = None  # the whole-step hipGraphExec (graph_launch)
         self._runner_stats: Optional[StepStats] = None
         self._stream_kind = 0                   # 0 compute / 1 copy stream (recording of fills)
         self._carry_at: Dict[int, List[int]] = {}  # instr -> next step's loads issued after it
@@ -723,27 +726,44 @@ class DAGExecutor:
         else:
             stream.wait_event(ev)
 
-    def _isend(self, buf, peer):
+    @property
+    def _device_p2p(self) -> bool:
+        """Edges moved by kernels (parallel/devp2p.py): the whole step is one hipGraph."""
+        return self.comm is not None and self.comm.kind == "device"
+
+    def _isend(self, buf, peer, key=None):
         if self._rec is not None:
             return _RWork(self._rec.r, self._rec.r.add_send(buf, peer))
+        if self._device_p2p:
+            return self.comm.isend(buf, peer, key)
         return self.comm.isend(buf, peer)
 
-    def _irecv(self, buf, peer):
+    def _irecv(self, buf, peer, key=None):
         if self._rec is not None:
             return _RWork(self._rec.r, self._rec.r.add_recv(buf, peer))
+        if self._device_p2p:
+            return self.comm.irecv(buf, peer, key)
         return self.comm.irecv(buf, peer)
 
     def _p2p_group(self, ops_):
-        """Post [(is_send, buffer, peer)] as ONE group (one ncclGroupStart/End); a work per op."""
+        """Post [(is_send, buffer, peer, key)] as ONE group (one ncclGroupStart/End); a work per
+        op. ``key`` names the message for the device transport (devp2p.edge_slots)."""
         if self._rec is not None:
             r = self._rec.r
             if len(ops_) > 1:
                 r.add_group_begin()
-            ws = [_RWork(r, r.add_send(b, p) if snd else r.add_recv(b, p)) for snd, b, p in ops_]
+            ws = [_RWork(r, r.add_send(b, p) if snd else r.add_recv(b, p)) for snd, b, p, _ in ops_]
             if len(ops_) > 1:
                 r.add_group_end()
             return ws
-        return self.comm.batch(ops_)
+        if self._device_p2p:
+            return self.comm.batch(ops_)
+        return self.comm.batch([(snd, b, p) for snd, b, p, _ in ops_])
+
+    def _act_region(self, tid: str) -> torch.Tensor:
+        """The bytes of task ``tid``'s activation region, as the program sized it."""
+        off = self.prog.act_offset[tid]
+        return self.act_slab[off:off + self.prog.act_bytes[tid]]
 
     def _fill(self, off, total, layout, views, pid, stats: StepStats, dma: bool = False) -> bool:
         """Copy the group into its arena region unless the region already holds it. ``dma``:
@@ -1220,6 +1240,8 @@ class DAGExecutor:
         tr = self.trace
         self._pending_sends = {}
         self._reset_step_state()
+        if self._device_p2p:
+            self.comm.begin_step()  # this rank's step counter: the sequence number of its flags
         if self._rec is not None and not self.gpu:  # replayed steps reset it too
             self._rec.r.add_pycall(self._reset_step_state)
         if self.prog.start_resident:  # warm-started program: its start groups are resident
@@ -1351,12 +1373,12 @@ class DAGExecutor:
             ins = self.prog.instrs[k]
             if ins.op == "recv":
                 self._wait_sends(ins)  # the recv buffer may still be read by a send to another peer
-            buf = self._views[ins.task]
-            ops_.append((ins.op == "send", buf, ins.peer))
+            buf = self._act_region(ins.task) if self._device_p2p else self._views[ins.task]
+            ops_.append((ins.op == "send", buf, ins.peer, ("act", ins.task)))
             idx.append(k)
         t0 = self._mark() if events is not None else None
         works = self._p2p_group(ops_)
-        for k, (snd, buf, peer), w in zip(idx, ops_, works):
+        for k, (snd, buf, peer, _), w in zip(idx, ops_, works):
             ins = self.prog.instrs[k]
             nbytes = buf.numel() * buf.element_size()
             if snd:
@@ -1433,7 +1455,7 @@ class DAGExecutor:
             pw.wait()  # this rank received the group itself: forward it once it arrived
         total = group_layout(self.store.groups[ins.param])[0]
         buf = self.param_slab[ins.param_off:ins.param_off + total]
-        self._pending_sends[i] = self._isend(buf, ins.peer)
+        self._pending_sends[i] = self._isend(buf, ins.peer, ("param", ins.param, ins.gpos))
         stats.sends += 1
         stats.bytes_sent += total
 
@@ -1447,7 +1469,8 @@ class DAGExecutor:
             if spec.name not in self._derived_named:
                 self._derived_cache.pop((spec.name, views[spec.name].data_ptr()), None)
                 self._derived_cache.pop(("side", spec.name, views[spec.name].data_ptr()), None)
-        self._param_recv[ins.param] = self._irecv(self.param_slab[off:off + total], ins.peer)
+        self._param_recv[ins.param] = self._irecv(self.param_slab[off:off + total], ins.peer,
+                                                  ("param", ins.param, ins.gpos))
         self._valid.append((off, total, ins.param))
         stats.recvs += 1
         stats.peer_fills += 1
@@ -1482,7 +1505,10 @@ class DAGExecutor:
         elif self._graph is not None and not profile:
             if self.trace:
                 Roctx.push(f"graph_step:rank{self.prog.rank}")
-            self._graph.replay()
+            if self._graph_exec is not None:
+                ops.ext().graph_launch(self._graph_exec, self.device.index or 0)  # GIL released
+            else:
+                self._graph.replay()
             if self.trace:
                 Roctx.pop()
             stats.kernels = self.prog.n_kernels
@@ -1498,10 +1524,21 @@ class DAGExecutor:
                     el = lambda a: (a - t_begin) * 1e3  # noqa: E731
                 stats.events = [(n, c, el(a), el(b)) for n, c, a, b in ev]
                 stats.timeline = [(n, a, b) for n, c, a, b in stats.events if c == "kernel"]
+        if self._mlp_fused:
+            self.check_mlp_fused()
         if self.debug:
             self.check_guards()
         self.last = stats
         return stats
+
+    def check_mlp_fused(self) -> None:
+        """The one-launch MLP block (DLS_MLP_FUSED=1, off by default) gives up a poll after its
+        spin limit and proceeds with wrong numbers rather than hang; its error word is read here
+        after every step (a host synchronisation: the price of the opt-in path) and a set word
+        fails the step loudly."""
+        if self._mlp_sync is not None and int(self._mlp_sync[-1].item()) != 0:
+            raise RuntimeError(f"rank {self.prog.rank}: fused MLP block gave up waiting for fc1 tiles "
+                               f"(error word {int(self._mlp_sync[-1].item())}); this step's outputs are wrong")
 
     def check_guards(self) -> None:
         """Debug mode: every arena's trailing canary is intact and the rank's outputs are
@@ -1539,7 +1576,9 @@ class DAGExecutor:
         if not self.use_graph:
             return False
         self._drop_runner()  # its hipGraphExec handles belong to the graphs a re-capture replaces
-        if self._copy_stream is not None or self.prog.has_comm:
+        if self._device_p2p and self._copy_stream is not None:
+            return False  # copy-stream refills beside device edges: the step stays eager
+        if self._copy_stream is not None or (self.prog.has_comm and not self._device_p2p):
             return self.capture_segments()
         self._sync()
         s = torch.cuda.Stream(self.device)
@@ -1566,6 +1605,7 @@ class DAGExecutor:
         g.instantiate()
         self._sync()
         self._graph = g
+        self._graph_exec = g.raw_cuda_graph_exec()
         return True
 
     def _sync(self) -> None:
@@ -1773,7 +1813,7 @@ class DAGExecutor:
             return {}  # whole-step graphs only
 
         def step_ms():
-            self._graph = None
+            self._graph = self._graph_exec = None
             self.capture()
             for _ in range(3):
                 self._graph.replay()
@@ -1833,7 +1873,7 @@ class DAGExecutor:
                 changes[f"{M}x{N}x{K}{tg}"] = (tuple(cur), tuple(best), round(best_ms, 4))
                 base = best_ms
         tuning.save()
-        self._graph = None
+        self._graph = self._graph_exec = None
         self.capture()
         return changes
 

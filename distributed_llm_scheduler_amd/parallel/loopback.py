@@ -19,6 +19,7 @@ device asynchrony (a gloo job cannot: its ``wait()`` blocks the host). CPU tenso
 """
 from __future__ import annotations
 
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
@@ -35,12 +36,15 @@ class LoopbackRun:
     hub: object
     issue_modes: List[Optional[str]] = field(default_factory=list)
     step_ms: List[float] = field(default_factory=list)
+    # host time per step.step() call (µs, mean over the timed steps): what issuing a step costs
+    host_us: List[float] = field(default_factory=list)
 
 
 def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = True, delay_us: float = 20.0,
                  poison: bool = True, store=None, timeout_s: float = 120.0,
                  before_steps: Optional[Callable] = None, cpu_runner: bool = False,
-                 sync_debug: bool = False, autotune: bool = False) -> LoopbackRun:
+                 sync_debug: bool = False, autotune: bool = False, transport: str = "hub",
+                 single_issue: bool = False) -> LoopbackRun:
     """Build one executor per rank of ``plan`` on ``device``, then drive every rank from its own
     thread: ``warmup`` eager steps, capture (segment hipGraphs + native runner for programs with
     p2p), ``steps`` timed steps. ``before_steps(executors)`` may patch the executors first
@@ -48,14 +52,36 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     step runner (kernel groups as callbacks) instead of the Python issue loop. ``sync_debug``:
     the timed steps run under torch's sync debug mode "error" (any device->host synchronising
     call inside a step raises). ``autotune``: tune GEMM shapes missing from the table first (off:
-    the kernel's heuristic config — the harness checks ordering and numerics, not speed)."""
+    the kernel's heuristic config — the harness checks ordering and numerics, not speed).
+    ``transport="device"`` (GPU): the edges are moved by kernels (parallel/devp2p.py) — notify,
+    pull and ack flags, no host pairing — and each rank's whole step captures into ONE hipGraph;
+    ``delay_us`` then delays every notify and ``poison`` fills each receive region with NaN
+    when the receive is posted. ``single_issue`` (captured whole-step graphs only): after
+    warm-up, ONE host thread issues every rank's timed steps round-robin (graph launches are
+    asynchronous), so ``host_us`` is the issue cost of a step without GIL contention between
+    rank threads."""
     from . import executor as exm
     from . import runtime
 
     device = torch.device(device)
     gpu = device.type == "cuda"
     world = plan.world
-    groups = loopback_groups(world, delay_us=delay_us if gpu else 0.0, poison=poison, timeout_s=timeout_s)
+    if transport == "device":
+        if not gpu:
+            raise ValueError("the device p2p transport needs a GPU")
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        if world + 1 > queues:
+            # a pull / ack wait spins on its rank's stream; a peer stream on the same hardware
+            # queue would be queued behind it (the waits time out: wrong numbers, not a hang)
+            raise ValueError(f"device transport with {world} ranks in one process needs GPU_MAX_HW_QUEUES >= "
+                             f"{world + 1} (set before the first CUDA call; it is {queues})")
+        from .devp2p import DeviceP2PGroup, DeviceP2PWorld
+        dw = DeviceP2PWorld(plan, device, range(world), delay_us=delay_us, poison=poison)
+        groups = [DeviceP2PGroup(dw, r) for r in range(world)]
+    elif transport == "hub":
+        groups = loopback_groups(world, delay_us=delay_us if gpu else 0.0, poison=poison, timeout_s=timeout_s)
+    else:
+        raise ValueError(f"unknown transport {transport!r}")
     store = store or runtime.make_store(plan)
     # executors are built on this thread (autotuning and weight transforms are not thread-safe)
     streams = [torch.cuda.Stream(device) for _ in range(world)] if gpu else [None] * world
@@ -73,6 +99,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
         before_steps(exs)
     stats = [None] * world
     ms = [0.0] * world
+    host_us = [0.0] * world
     errors = []
     start = threading.Barrier(world)
 
@@ -89,15 +116,25 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
                     ex.step()
                 if capture and gpu:
                     ex.capture()
+                if transport == "device":
+                    streams[r].synchronize()
+                    start.wait()  # every rank past its warm-up before any error word is cleared
+                    ex.comm.reset_errors()
                 elif cpu_runner and not gpu and not ex.build_runner():
                     raise RuntimeError("CPU step runner refused the program")
                 start.wait()
                 if sync_debug and gpu and r == 0:
                     torch.cuda.set_sync_debug_mode("error")
                 start.wait()
+                if single_issue:
+                    return  # the timed steps are issued by the calling thread (below)
                 t0 = time.perf_counter()
+                issue = 0.0
                 for _ in range(steps):
+                    a = time.perf_counter()
                     stats[r] = ex.step()
+                    issue += time.perf_counter() - a
+                host_us[r] = issue / max(steps, 1) * 1e6
                 start.wait()
                 if sync_debug and gpu and r == 0:
                     torch.cuda.set_sync_debug_mode(0)
@@ -122,13 +159,31 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
         exm.RUNNER_CPU = saved
     if any(t.is_alive() for t in threads):
         raise RuntimeError("loopback harness: a rank thread did not finish (hung transfer?)")
+    if single_issue and not errors:
+        import time
+
+        if not all(ex._graph_exec is not None for ex in exs):
+            raise RuntimeError("single_issue needs every rank's step captured as one hipGraph")
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            for r, ex in enumerate(exs):
+                with torch.cuda.stream(streams[r]):
+                    stats[r] = ex.step()
+        issue = time.perf_counter() - t0
+        for r in range(world):
+            streams[r].synchronize()
+        wall = time.perf_counter() - t0
+        host_us = [issue / max(steps * world, 1) * 1e6] * world
+        ms = [wall / max(steps, 1) * 1e3] * world
     if gpu:
         torch.cuda.synchronize(device)
     real = [(r, e) for r, e in errors if not isinstance(e, threading.BrokenBarrierError)]
     if real or errors:
         r, e = (real or errors)[0]
         raise RuntimeError(f"loopback harness: rank {r} failed: {e!r}") from e
-    return LoopbackRun(exs, stats, groups[0].hub, [ex.issue_mode for ex in exs], ms)
+    hub = getattr(groups[0], "hub", None)
+    issue = [ex.issue_mode or ("graph" if ex._graph is not None else None) for ex in exs]
+    return LoopbackRun(exs, stats, hub, issue, ms, host_us=host_us)
 
 
 class _Null:

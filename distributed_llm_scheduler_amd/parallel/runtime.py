@@ -441,6 +441,25 @@ def device_init_ok(p: Plan, rank: int) -> bool:
     return steady_fill_bytes(p.programs[rank], p.param_bytes) == 0
 
 
+P2P = os.environ.get("DLS_P2P", "rccl")  # cross-GPU DAG edges: "rccl" (c10d p2p) or "device" (devp2p.py)
+
+
+def p2p_group(p: Plan, rank: int, device, pg, transport: Optional[str] = None):
+    """The ``pg`` to hand :func:`make_executor` for a process-per-GPU job: the process group
+    itself (RCCL p2p, the default), or — ``transport="device"`` / ``DLS_P2P=device`` — the
+    device-initiated transport (parallel/devp2p.py: edges moved by kernels, each rank's whole
+    step one hipGraph), whose arenas and mailboxes the ranks exchange as IPC handles over ``pg``
+    once, when the executors are built."""
+    transport = transport or P2P
+    if pg is None or p.world == 1 or transport == "rccl":
+        return pg
+    if transport != "device":
+        raise ValueError(f"unknown p2p transport {transport!r}")
+    from .devp2p import DeviceP2PGroup, DeviceP2PWorld
+
+    return DeviceP2PGroup(DeviceP2PWorld(p, device, [rank]), rank, pg=pg)
+
+
 def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None, pg=None, use_graph: bool = True,
                   trace: bool = False, debug: bool = False, autotune: bool = True):
     """``debug=True``: validate every rank's program first (parallel/validate.py) and run the

@@ -7,6 +7,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# Hardware queues per process (HIP's default is 4). The single-GPU multi-rank harness with the
+# device p2p transport runs up to 4 ranks' streams in this ONE process, each of which may hold
+# a kernel spinning on a peer's flag: a rank stream that shares a hardware queue with another
+# rank's queues that rank's kernels behind the spin (parallel/loopback.py). Set before HIP
+# initialises (the first CUDA call), well under the pool's limit of 32.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")

@@ -94,3 +94,25 @@ def test_loopback_poison_marks_receive_buffers():
     LoopComm(g[0]).isend(torch.arange(4.0), 1).wait()
     w.wait()
     assert torch.equal(buf, torch.arange(4.0))
+
+
+def test_loopback_group_semantics():
+    """A coalesced group (``LoopComm.batch``, as ncclGroupStart/End): ONE work for all its ops
+    (waiting for the receive waits for the group), and its posts go out under the job-wide group
+    lock, so a peer never matches against a partly posted group."""
+    g = loopback_groups(2, poison=False, timeout_s=5.0)
+    c0, c1 = LoopComm(g[0]), LoopComm(g[1])
+    assert g[0].group_lock is g[1].group_lock
+    a, b = torch.zeros(4), torch.zeros(4)
+    ws = c0.batch([(True, torch.ones(4), 1), (False, a, 1)])
+    assert ws[0] is ws[1]
+    with g[0].group_lock:  # another group's posts wait while one is being posted
+        t = threading.Thread(target=lambda: [w.wait() for w in c1.batch([(False, b, 0),
+                                                                         (True, torch.full((4,), 3.0), 0)])])
+        t.start()
+        t.join(0.3)
+        assert t.is_alive() and g[0].hub.transfers == 0
+    ws[1].wait()
+    t.join(5)
+    assert not t.is_alive()
+    assert torch.equal(a, torch.full((4,), 3.0)) and torch.equal(b, torch.ones(4))

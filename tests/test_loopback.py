@@ -190,3 +190,61 @@ def test_loopback_gpu_mixed_issue_modes():
     assert run.issue_modes[0] == "runner" and run.issue_modes[1] != "runner", run.issue_modes
     assert run.hub.outstanding() == 0
     _check(p, run, store, ids, 0.03)
+
+
+# ------------------------------------------------------------------ device transport (GPU)
+# every placement's edges moved by kernels (parallel/devp2p.py): notify / pull / ack flags with
+# no host pairing, each rank's WHOLE step captured into one hipGraph
+DEVICE_CASES = ["pipeline", "pipeline_merged", "capped_eft", "capped_one_dag", "tensor", "sequence", "expert",
+                "peer_fill"]
+
+
+@gpu
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("case", DEVICE_CASES)
+@pytest.mark.parametrize("world", [2, 4])
+def test_loopback_gpu_device_transport(case, world, monkeypatch):
+    """Each rank replays ONE hipGraph per step — kernels, notifies, pulls and acks — with 50 us
+    of delay in front of every notify and NaN-poisoned receive regions; no wait timed out, the
+    logits match fp32, and issuing a step costs the host one graph launch whatever the edge
+    count (<= 30 us per step, round-4 runner: 10-16 us per segment)."""
+    from distributed_llm_scheduler_amd.parallel import devp2p
+    monkeypatch.setattr(devp2p, "_TICKS", int(2e8))  # 2 s: a broken protocol fails fast
+    p, ids = _gpu_plan(case, world)
+    assert _p2p_work(p) > 0
+    store = runtime.make_store(p)
+    run = run_loopback(p, "cuda:0", steps=20, warmup=2, store=store, delay_us=50.0, transport="device",
+                       single_issue=True)
+    assert run.issue_modes == ["graph"] * world, run.issue_modes
+    assert [ex.comm.errors() for ex in run.executors] == [0] * world
+    assert max(run.host_us) <= 30.0, run.host_us
+    _check(p, run, store, ids, 0.03)
+
+
+@gpu
+@pytest.mark.timeout(240)
+def test_loopback_gpu_device_transport_catches_missing_pull(monkeypatch):
+    """Negative control: rank 1 never pulls its received regions (the consumer's wait dropped):
+    its consumers read the NaN poison and the check fails."""
+    from distributed_llm_scheduler_amd.parallel import devp2p
+    monkeypatch.setattr(devp2p, "_TICKS", int(2e8))
+    p, ids = _gpu_plan("pipeline", 2)
+    store = runtime.make_store(p)
+
+    class _NoPull:
+        def wait(self):
+            pass
+
+    def drop_pulls(exs):
+        comm = exs[1].comm
+        orig = comm.irecv
+
+        def irecv(buf, peer, key=None):
+            orig(buf, peer, key)  # poisons the region
+            return _NoPull()
+        comm.irecv = irecv
+
+    run = run_loopback(p, "cuda:0", steps=1, warmup=1, capture=False, store=store, delay_us=200.0,
+                       before_steps=drop_pulls, transport="device")
+    with pytest.raises(AssertionError):
+        _check(p, run, store, ids, 0.03)
