@@ -23,7 +23,8 @@ The same JSON line also carries (unless ``--no-extras``):
     python bench.py --gpus N --steps K --warmup W      # N > 1: starts its own N rank processes
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
     python bench.py --model gpt2-medium --gpus 2 --cap-gb 8 --replicas 1          # one DAG across 2 GPUs
-    python bench.py --model mixtral-8x7b --gpus 8 --placement expert --replicas 1  # experts over 8 GPUs
+    python bench.py --model mixtral-8x7b --gpus 8 --placement expert               # DP attention + experts over 8 GPUs
+    DLS_P2P=device python bench.py --gpus N ...   # cross-GPU edges moved by kernels (parallel/devp2p.py)
 """
 from __future__ import annotations
 
@@ -132,7 +133,7 @@ def launch_ranks(n: int) -> int:
 
 def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas, batch, seq, cost_model,
         placement, tp=1, sp=1, fuse=True, use_graph=True, init="auto", refine=False, roctx=False,
-        profile=False, trace_out=None, tag="", node_speeds=None, merge_mb=1) -> dict:
+        profile=False, trace_out=None, tag="", node_speeds=None, merge_mb=1, transport=None) -> dict:
     """Plan, build the rank's executor, warm up, time ``steps`` steps bracketed by a barrier +
     device synchronize on both sides; the step time is the MAX over ranks."""
     t0 = time.time()
@@ -144,7 +145,8 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     dev_init = init == "device" or (init == "auto" and ctx.gpu and runtime.device_init_ok(plan, ctx.rank))
     store = runtime.make_store(plan, device_init=dev_init)
     t0 = time.time()
-    pg = runtime.p2p_group(plan, ctx.rank, ctx.device, ctx.pg) if ctx.gpu else ctx.pg  # DLS_P2P=device: kernels
+    # DLS_P2P=device (or transport="device"): cross-GPU edges moved by kernels, IPC-mapped peers
+    pg = runtime.p2p_group(plan, ctx.rank, ctx.device, ctx.pg, transport) if ctx.gpu else ctx.pg
     ex = runtime.make_executor(plan, ctx.rank, ctx.device, store, pg=pg, use_graph=use_graph, trace=roctx)
     log(f"[bench{tag}] rank {ctx.rank}: executor ready in {(time.time() - t0):.1f} s (device_init={dev_init})")
     for _ in range(warmup):
@@ -167,6 +169,8 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     mine = elapsed / steps * 1e3
     ms, per_rank = ctx.gather(mine)
     launches = ctx.gather_list(ex.launches if ex.launches is not None else -1)
+    dev_p2p = getattr(getattr(ex, "comm", None), "kind", None) == "device"
+    p2p_err = ctx.gather_list(ex.comm.errors() if dev_p2p else 0)  # a timed-out device wait: numbers invalid
     st = plan.stats
     res = {
         "ms_per_step": round(ms, 5),
@@ -176,6 +180,10 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
         "scheduler": plan.scheduler_name,
         "cross_gpu_edges": st["cross_gpu_edges"],
         "cross_gpu_bytes": st["cross_gpu_bytes"],
+        "cross_gpu_bytes_routed": st.get("cross_gpu_bytes_routed", st["cross_gpu_bytes"]),
+        "cross_gpu_transfers": st.get("cross_gpu_transfers"),
+        "modelled_period_ms": st.get("modelled_period_ms"),
+        "tasks_per_rank": st.get("tasks_per_rank"),
         "kernel_groups_per_rank": st["kernels_per_rank"],
         # kernel launches of one step on this rank (counted in the captured hipGraphs; None if eager)
         "launches_per_rank": [None if v < 0 else int(v) for v in launches],
@@ -187,6 +195,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
         # segment-replayed programs (p2p or copy-stream refills): native runner or Python loop
         "issue_mode": ex.issue_mode or ("graph" if captured else "python"),
         "p2p": getattr(getattr(ex, "comm", None), "kind", None),
+        "p2p_errors": [int(v) for v in p2p_err],
     }
     if profile or trace_out:
         s = ex.step(profile=True)
@@ -247,6 +256,8 @@ def main():
     ap.add_argument("--strong-mb", type=int, default=8, help="micro-batches of the strong-scaling pipeline run")
     ap.add_argument("--no-strong-merge", dest="strong_merge", action="store_false",
                     help="run the strong sub-result's micro-batches as separate M = 512 chains (not merged)")
+    ap.add_argument("--no-device-p2p-extra", dest="device_p2p_extra", action="store_false",
+                    help="N > 1: skip the strong sub-result repeated over the device p2p transport")
     ap.add_argument("--merge-mb", type=int, default=1,
                     help="headline: merge this many request replicas into one batched request (plan merge_mb)")
     ap.add_argument("--extras-timeout", type=float, default=180.0,
@@ -342,6 +353,8 @@ def main():
             "launches_per_rank": head["launches_per_rank"],
             "cross_gpu_edges": head["cross_gpu_edges"],
             "cross_gpu_bytes": head["cross_gpu_bytes"],
+            "cross_gpu_bytes_routed": head["cross_gpu_bytes_routed"],
+            "p2p_transport": head["p2p"] or "none",
             "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
             "per_rank_ms": head["per_rank_ms"],
             "hip_graph": head["hip_graph"],
@@ -390,7 +403,8 @@ def main():
                   "mem_cap_gb_per_gpu": [round(m, 6) for m, _ in nodes], "node_speeds": [round(v, 4) for _, v in nodes]}
         extras["capped"] = capped
         keys = ("tasks_completed", "tasks_total", "ms_per_step", "refill_gb_per_step", "peer_fill_gb_per_step",
-                "param_loads_per_step", "param_evictions_per_step", "cross_gpu_edges", "cross_gpu_bytes", "issue_mode")
+                "param_loads_per_step", "param_evictions_per_step", "cross_gpu_edges", "cross_gpu_bytes",
+                "cross_gpu_transfers", "tasks_per_rank", "modelled_period_ms", "issue_mode")
         for sched in ("MRU_spec", "EFT", "DFS"):
             try:
                 r = run(ctx, args.extra_steps, ew, scheduler=sched, cap_gb=[m for m, _ in nodes], replicas=1,
@@ -433,6 +447,21 @@ def main():
         except Exception as e:  # noqa: BLE001
             log(f"[bench] strong sub-run failed: {e!r}")
             strong["error"] = repr(e)[:300]
+        if world > 1 and gpu and args.device_p2p_extra:
+            # the same strong pipeline with its edges moved by kernels (parallel/devp2p.py): each
+            # rank's whole step ONE hipGraph; peers' arenas mapped over xGMI through IPC handles
+            sd = {"transport": "device", "micro_batches": args.strong_mb, "micro_batches_merged": merge}
+            extras["strong_device_p2p"] = sd
+            try:
+                r = run(ctx, args.extra_steps, ew, scheduler="EFT", cap_gb=288.0, replicas=args.strong_mb,
+                        cost_model="bytes", placement="pipeline", tag=":strong-devp2p", merge_mb=merge,
+                        transport="device", **common)
+                sd.update({k: r[k] for k in ("ms_per_step", "per_rank_ms", "hip_graph", "launches_per_rank",
+                                             "p2p_errors", "cross_gpu_bytes")})
+                sd["valid"] = not any(r["p2p_errors"])
+            except Exception as e:  # noqa: BLE001
+                log(f"[bench] strong device-p2p sub-run failed: {e!r}")
+                sd["error"] = repr(e)[:300]
 
     if world > 1:
         dist.barrier()

@@ -5,7 +5,7 @@ any slot whose two snapshots differ is printed (case, world from argv)."""
 import os
 import sys
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -17,7 +17,7 @@ from distributed_llm_scheduler_amd.parallel import devp2p, runtime  # noqa: E402
 from distributed_llm_scheduler_amd.parallel.loopback import run_loopback  # noqa: E402
 import test_loopback as T  # noqa: E402
 
-devp2p._TICKS = int(2e8)
+devp2p._TICKS = int(2e9)
 case, world = sys.argv[1], int(sys.argv[2])
 delay = float(sys.argv[3]) if len(sys.argv) > 3 else 50.0
 capture = len(sys.argv) > 4 and sys.argv[4] == "graph"
@@ -73,7 +73,12 @@ for (k, n), dst in sorted(got.items(), key=lambda kv: (kv[0][1], str(kv[0][0])))
     if not torch.equal(src, dst):
         bad += 1
         diff = (src != dst).nonzero()
-        print(f"BAD step {n} {k}: {diff.numel()} bytes differ, first at {int(diff[0])} of {src.numel()}")
+        ff = float((dst == 0xFF).float().mean())
+        same = [f"{kk[2]}@{nn}" for (kk, nn), v in sent.items() if v.numel() == dst.numel() and torch.equal(v, dst)]
+        later = sent.get((k, n + 1))
+        print(f"BAD step {n} {k}: {diff.numel()} bytes differ, first at {int(diff[0])} of {src.numel()}; "
+              f"dst 0xFF frac {ff:.3f}; dst equals snapshots {same[:4]}; "
+              f"src(step {n}) == src(step {n + 1}): {None if later is None else torch.equal(later, src)}")
 print(f"{case} x{world}: {len(got)} pulls checked, {bad} bad; errors {[ex.comm.errors() for ex in run.executors]}")
 try:
     print("worst", T._check(p, run, store, ids, 0.03))

@@ -23,6 +23,8 @@ import time
 
 import torch
 
+os.environ["GPU_MAX_HW_QUEUES"] = "32"  # 8 ranks' streams in this process (parallel/loopback.py)
+TRANSPORT = "hub"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_llm_scheduler_amd.parallel import runtime  # noqa: E402
 from distributed_llm_scheduler_amd.parallel.loopback import run_loopback  # noqa: E402
@@ -30,13 +32,19 @@ from distributed_llm_scheduler_amd.parallel.loopback import run_loopback  # noqa
 CONFIGS = {
     "gpt2m_cap": dict(model="gpt2-medium", world=2, scheduler="MRU_spec", cap_gb=8.0, replicas=1,
                       cost_model="reference"),
+    # the same cap placed by EFT's steady-state partition (one pipeline stage per GPU)
+    "gpt2m_cap_eft": dict(model="gpt2-medium", world=2, scheduler="EFT", cap_gb=8.0, replicas=1,
+                          cost_model="reference"),
     "llama_pipeline": dict(model="llama3-8b", world=8, placement="pipeline", replicas=8),
-    "mixtral_expert": dict(model="mixtral-8x7b", world=8, placement="expert", replicas=1),
+    # one request per GPU (data-parallel attention) with the experts spread over the 8 GPUs
+    "mixtral_expert": dict(model="mixtral-8x7b", world=8, placement="expert", replicas=8),
 }
 # full-width one-layer variants whose fp32 reference forward fits a CPU check
 # (a one-layer model has no pipeline stages to split: its check runs the layer tensor-parallel)
 CHECK = {"llama_pipeline": dict(model="llama3-8b-1l", world=2, placement="tensor", tp=2),
          "mixtral_expert": dict(model="mixtral-8x7b-1l", world=8, placement="expert", replicas=1),
+         "gpt2m_cap_eft": dict(model="gpt2-medium", world=2, scheduler="EFT", cap_gb=8.0, replicas=1,
+                               cost_model="reference"),
          "gpt2m_cap": dict(model="gpt2-medium", world=2, scheduler="MRU_spec", cap_gb=8.0, replicas=1,
                            cost_model="reference")}
 
@@ -47,10 +55,16 @@ def run(name, kw, steps, check):
     t0 = time.time()
     p = runtime.plan(model, world=world, seq=512, batch=1, **kw)
     store = runtime.make_store(p, device_init=not check and all(runtime.device_init_ok(p, r) for r in range(world)))
-    res = run_loopback(p, "cuda:0", steps=steps, warmup=2, store=store, delay_us=0.0, poison=False, autotune=True)
+    res = run_loopback(p, "cuda:0", steps=steps, warmup=2, store=store, delay_us=0.0, poison=False, autotune=True,
+                       transport=TRANSPORT)
     out = {"config": name, "model": model, "world": world, "tasks_completed": p.completed, "tasks_total": p.total,
            "cross_gpu_edges": p.stats["cross_gpu_edges"], "cross_gpu_mb": round(p.stats["cross_gpu_bytes"] / 1e6, 2),
-           "issue_modes": res.issue_modes, "transfers_total": res.hub.transfers,
+           "cross_gpu_mb_routed": round(p.stats["cross_gpu_bytes_routed"] / 1e6, 2), "transport": TRANSPORT,
+           "issue_modes": res.issue_modes,
+           "transfers_total": res.hub.transfers if res.hub is not None else None,
+           "pulled_mb_last_steps": (round(sum(ex.comm.bytes_pulled() for ex in res.executors) / 1e6, 2)
+                                    if TRANSPORT == "device" else None),
+           "host_us_per_step": [round(h, 1) for h in res.host_us],
            "ms_per_step_all_ranks_on_one_gpu": round(max(res.step_ms), 3), "wall_s": round(time.time() - t0, 1)}
     if check:
         from distributed_llm_scheduler_amd.models import reference
@@ -76,7 +90,12 @@ def main():
     ap.add_argument("--configs", default="gpt2m_cap,llama_pipeline,mixtral_expert")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--check", action="store_true", help="full-width one-layer variants, compared with fp32")
+    ap.add_argument("--transport", default="hub", choices=["hub", "device"],
+                    help="hub: RCCL semantics through the loopback hub; device: edges moved by kernels "
+                         "(parallel/devp2p.py), each rank's step one hipGraph")
     a = ap.parse_args()
+    global TRANSPORT
+    TRANSPORT = a.transport
     for name in a.configs.split(","):
         run(name, (CHECK if a.check else CONFIGS)[name], a.steps, a.check)
         torch.cuda.empty_cache()

@@ -30,8 +30,14 @@ void p2p_notify(int64_t remote_flag, at::Tensor step) {
   launch_p2p_notify(reinterpret_cast<int64_t*>(remote_flag), step.data_ptr<int64_t>(), cur(step));
 }
 
+unsigned long long* moved_ptr(const c10::optional<at::Tensor>& moved) {
+  if (!moved || !moved->defined()) return nullptr;
+  TORCH_CHECK(moved->is_cuda() && moved->scalar_type() == at::kLong, "p2p: int64 byte counter");
+  return reinterpret_cast<unsigned long long*>(moved->data_ptr<int64_t>());
+}
+
 void p2p_pull(int64_t src, at::Tensor dst, at::Tensor ready, int64_t ack_remote, at::Tensor ticket, at::Tensor step,
-              at::Tensor err, int64_t timeout_ticks) {
+              at::Tensor err, int64_t timeout_ticks, c10::optional<at::Tensor> moved) {
   TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "p2p_pull: dst must be a contiguous CUDA region");
   const int64_t bytes = dst.nbytes();
   TORCH_CHECK(bytes % 16 == 0 && src % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
@@ -44,7 +50,31 @@ void p2p_pull(int64_t src, at::Tensor dst, at::Tensor ready, int64_t ack_remote,
   if (bytes == 0) return;
   launch_p2p_pull(reinterpret_cast<const void*>(src), dst.data_ptr(), bytes, ready.data_ptr<int64_t>(),
                   reinterpret_cast<int64_t*>(ack_remote), reinterpret_cast<unsigned*>(ticket.data_ptr<int>()),
-                  step.data_ptr<int64_t>(), err.data_ptr<int>(), timeout_ticks, p2p_pull_blocks(bytes), cur(dst));
+                  step.data_ptr<int64_t>(), err.data_ptr<int>(), timeout_ticks, p2p_pull_blocks(bytes), moved_ptr(moved),
+                  cur(dst));
+}
+
+// rows of the listed experts' ranges in `off` (int32 [E+1], device): gathered through `idx`
+// (int32, expert-sorted order -> source row) when given, else copied as compact rows
+void p2p_pull_rows(int64_t src, at::Tensor dst, int64_t row_bytes, c10::optional<at::Tensor> idx, at::Tensor off,
+                   at::Tensor experts, int64_t max_rows, at::Tensor ready, int64_t ack_remote, at::Tensor ticket,
+                   at::Tensor step, at::Tensor err, int64_t timeout_ticks, c10::optional<at::Tensor> moved) {
+  TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "p2p_pull_rows: contiguous CUDA destination");
+  TORCH_CHECK(row_bytes > 0 && row_bytes % 16 == 0 && src % 16 == 0, "p2p_pull_rows: 16-B rows");
+  TORCH_CHECK(off.is_cuda() && off.scalar_type() == at::kInt, "p2p_pull_rows: int32 offsets");
+  TORCH_CHECK(experts.is_cuda() && experts.scalar_type() == at::kInt, "p2p_pull_rows: int32 expert list");
+  TORCH_CHECK(dst.nbytes() >= max_rows * row_bytes, "p2p_pull_rows: destination smaller than max_rows rows");
+  const int32_t* ip = nullptr;
+  if (idx && idx->defined()) {
+    TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == at::kInt, "p2p_pull_rows: int32 row index");
+    ip = idx->data_ptr<int32_t>();
+  }
+  check_i64(ready, "p2p_pull_rows ready");
+  check_i64(step, "p2p_pull_rows step");
+  launch_p2p_pull_rows(reinterpret_cast<const void*>(src), dst.data_ptr(), row_bytes, ip, off.data_ptr<int32_t>(),
+                       experts.data_ptr<int32_t>(), (int)experts.numel(), max_rows, ready.data_ptr<int64_t>(),
+                       reinterpret_cast<int64_t*>(ack_remote), reinterpret_cast<unsigned*>(ticket.data_ptr<int>()),
+                       step.data_ptr<int64_t>(), err.data_ptr<int>(), timeout_ticks, moved_ptr(moved), cur(dst));
 }
 
 void p2p_delay(double us, at::Tensor like) { launch_delay(us, cur(like)); }
@@ -81,13 +111,12 @@ int64_t ipc_open(py::bytes handle) {
 
 void ipc_close(int64_t p) { C10_HIP_CHECK(hipIpcCloseMemHandle(reinterpret_cast<void*>(p))); }
 
-// Launch an instantiated hipGraph on the device's current stream with the GIL released: a
+// Launch an instantiated hipGraph on `stream` (a raw hipStream_t) with the GIL released: a
 // captured step's whole host cost (torch's CUDAGraph.replay also updates RNG offsets the
 // executor's graphs never use, under the GIL — which ranks sharing a process contend for).
-void graph_launch(int64_t exec, int64_t device) {
-  hipStream_t s = c10::hip::getCurrentHIPStream(static_cast<c10::DeviceIndex>(device)).stream();
+void graph_launch(int64_t exec, int64_t stream) {
   py::gil_scoped_release nogil;
-  C10_HIP_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), s));
+  C10_HIP_CHECK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), reinterpret_cast<hipStream_t>(stream)));
 }
 
 }  // namespace
@@ -95,7 +124,11 @@ void graph_launch(int64_t exec, int64_t device) {
 void register_p2p(py::module& m) {
   m.def("p2p_tick", &p2p_tick);
   m.def("p2p_notify", &p2p_notify);
-  m.def("p2p_pull", &p2p_pull);
+  m.def("p2p_pull", &p2p_pull, py::arg("src"), py::arg("dst"), py::arg("ready"), py::arg("ack_remote"),
+        py::arg("ticket"), py::arg("step"), py::arg("err"), py::arg("timeout_ticks"), py::arg("moved") = py::none());
+  m.def("p2p_pull_rows", &p2p_pull_rows, py::arg("src"), py::arg("dst"), py::arg("row_bytes"), py::arg("idx"),
+        py::arg("off"), py::arg("experts"), py::arg("max_rows"), py::arg("ready"), py::arg("ack_remote"),
+        py::arg("ticket"), py::arg("step"), py::arg("err"), py::arg("timeout_ticks"), py::arg("moved") = py::none());
   m.def("p2p_wait", &p2p_wait);
   m.def("p2p_delay", &p2p_delay);
   m.def("p2p_pull_blocks", &p2p_pull_blocks);

@@ -19,9 +19,17 @@ void launch_p2p_tick(int64_t* step, hipStream_t s);
 void launch_p2p_notify(int64_t* remote_flag, const int64_t* step, hipStream_t s);
 // dst <- src (bytes % 16 == 0, both 16-B aligned) once *ready >= *step; then ack_remote = step.
 // `ticket` counts arriving workgroups (monotonic; its launches always use the same grid).
+// `moved` (optional): a device byte counter of what the rank pulled (reports, tests)
 void launch_p2p_pull(const void* src, void* dst, int64_t bytes, const int64_t* ready, int64_t* ack_remote,
                      unsigned* ticket, const int64_t* step, int* err, int64_t timeout_ticks, int blocks,
-                     hipStream_t s);
+                     unsigned long long* moved, hipStream_t s);
+// Routed-row pull (expert parallelism): rows [off[e], off[e+1]) of each listed expert, gathered
+// through idx (hidden state -> expert GPU) or as compact rows (expert output -> combine); see
+// p2p_device.hip. max_rows sizes the grid (the device-side counts decide what moves).
+void launch_p2p_pull_rows(const void* src, void* dst, int64_t row_bytes, const int32_t* idx, const int32_t* off,
+                          const int32_t* experts, int n_exp, int64_t max_rows, const int64_t* ready,
+                          int64_t* ack_remote, unsigned* ticket, const int64_t* step, int* err, int64_t timeout_ticks,
+                          unsigned long long* moved, hipStream_t s);
 void launch_p2p_wait(const int64_t* flag, const int64_t* step, int* err, int64_t timeout_ticks, int code,
                      hipStream_t s);
 int p2p_pull_blocks(int64_t bytes);

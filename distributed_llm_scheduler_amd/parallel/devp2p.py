@@ -24,8 +24,12 @@ and mailboxes once (:meth:`DeviceP2PWorld.exchange`). A wait that does not see i
 GPU; :meth:`DeviceComm.errors` reads it.
 
 Ordering matches RCCL's p2p contract (the programs validated for it need nothing new): a send
-never blocks (notify is a flag store), a receive completes before its first consumer, a sent
-region is written again only after its consumer pulled it.
+never blocks (notify is a flag store); a receive is pulled where it is posted — at the
+producer's position in the consumer's program, as an RCCL receive completes once both ends have
+posted (pulling later, at the consumer, can deadlock: the producer may wait to reuse the region
+for something the consumer needs first); a sent region is written again only after its
+consumer pulled it. Routed expert-parallel rows are the exception: they are pulled by the
+consumer's MoE code once the routing is known on the device, right after the receive.
 """
 from __future__ import annotations
 
@@ -74,14 +78,14 @@ def source_regions(programs, param_bytes: Dict[str, int]) -> Dict[Tuple[int, int
 
 
 class Mailbox:
-    """One rank's flags: int64 [step, ready[S], ack[S]], int32 tickets[S] and an error word, in
-    uncached device memory (polled by one lane, written by peers)."""
+    """One rank's flags: int64 [step, bytes pulled, ready[S], ack[S]], int32 tickets[S] and an
+    error word, in uncached device memory (polled by one lane, written by peers)."""
 
     def __init__(self, n_slots: int, device):
         from .. import ops
 
         self.S = n_slots
-        n64 = 1 + 2 * n_slots
+        n64 = 2 + 2 * n_slots
         n32 = n_slots + 1
         nbytes = (n64 * 8 + n32 * 4 + 255) // 256 * 256
         self.raw = ops.ext().alloc_device(nbytes, 3)  # hipDeviceMallocUncached
@@ -89,17 +93,18 @@ class Mailbox:
         i64 = self.raw[:n64 * 8].view(torch.int64)
         i32 = self.raw[n64 * 8:n64 * 8 + n32 * 4].view(torch.int32)
         self.step = i64[0:1]
-        self.ready = i64[1:1 + n_slots]
-        self.ack = i64[1 + n_slots:1 + 2 * n_slots]
+        self.moved = i64[1:2]
+        self.ready = i64[2:2 + n_slots]
+        self.ack = i64[2 + n_slots:2 + 2 * n_slots]
         self.tickets = i32[:n_slots]
         self.err = i32[n_slots:n_slots + 1]
         self.base = self.raw.data_ptr()
 
     def ready_addr(self, base: int, slot: int) -> int:
-        return base + 8 * (1 + slot)
+        return base + 8 * (2 + slot)
 
     def ack_addr(self, base: int, slot: int) -> int:
-        return base + 8 * (1 + self.S + slot)
+        return base + 8 * (2 + self.S + slot)
 
 
 class DeviceP2PWorld:
@@ -184,16 +189,35 @@ class _RecvWork:
     def __init__(self, comm, slot: int, buf: torch.Tensor, src: Tuple[int, str, int]):
         self.comm, self.slot, self.buf, self.src, self.done = comm, slot, buf, src, False
 
+    def _args(self):
+        c = self.comm
+        peer, arena, off = self.src
+        pb = c.w.bases[peer]
+        m = c.mb
+        return (pb[arena] + off, m.ready[self.slot:self.slot + 1], m.ack_addr(pb["mail"], self.slot),
+                m.tickets[self.slot:self.slot + 1])
+
     def wait(self):
+        """Pull the whole region (the receiving rank's stream; later kernels see it)."""
         if not self.done:
             self.done = True
-            c = self.comm
-            peer, arena, off = self.src
-            pb = c.w.bases[peer]
-            m = c.mb
-            c.e.p2p_pull(pb[arena] + off, self.buf, m.ready[self.slot:self.slot + 1],
-                         m.ack_addr(pb["mail"], self.slot), m.tickets[self.slot:self.slot + 1], m.step, m.err,
-                         _TICKS)
+            src, ready, ack, ticket = self._args()
+            m = self.comm.mb
+            self.comm.e.p2p_pull(src, self.buf, ready, ack, ticket, m.step, m.err, _TICKS, m.moved)
+
+    def pull_rows(self, dst: torch.Tensor, row_bytes: int, idx: Optional[torch.Tensor], off: torch.Tensor,
+                  experts: torch.Tensor, max_rows: int) -> None:
+        """Pull only routed rows instead (expert parallelism, the device-side routing ``off`` /
+        ``idx`` decides which): for each expert in ``experts``, rows [off[e], off[e+1]) of the
+        expert-sorted order — gathered from source rows ``idx[j]`` into dst row j, or (``idx``
+        None) compact rows 0.. of the source into the same rows of ``dst``."""
+        if self.done:
+            return
+        self.done = True
+        src, ready, ack, ticket = self._args()
+        m = self.comm.mb
+        self.comm.e.p2p_pull_rows(src, dst, int(row_bytes), idx, off, experts, int(max_rows), ready, ack, ticket,
+                                  m.step, m.err, _TICKS, m.moved)
 
 
 class DeviceComm:
@@ -250,6 +274,10 @@ class DeviceComm:
         rank can outlast a peer's wait; sequence numbers are monotonic, so the protocol itself
         recovers on the next step)."""
         self.mb.err.zero_()
+
+    def bytes_pulled(self) -> int:
+        """Bytes this rank pulled from its peers since the mailbox was made (host read)."""
+        return int(self.mb.moved.item())
 
     def errors(self) -> int:
         """The rank's error word (host read: synchronises): bit 0 a pull, bit 1 an ack wait

@@ -119,6 +119,8 @@ def synthetic_tokens(name: str, n: int, vocab: int, seed: int = 1234) -> torch.T
     return torch.randint(0, vocab, (n,), generator=g, dtype=torch.int32)
 
 
+# device p2p transport: expert-parallel edges move only the routed rows (DAGExecutor._plan_routed_edges)
+EP_ROUTED = os.environ.get("DLS_EP_ROUTED", "1") == "1"
 FOLD_MAX_K = 1024  # fold a preceding norm into the GEMM only up to this K (see DAGExecutor._gemm)
 # widest norm input whose statistics a producer GEMM hands over (beyond it: a norm kernel)
 HANDOFF_MAX_K = int(os.environ.get("DLS_HANDOFF_MAX_K", str(FOLD_MAX_K)))
@@ -232,8 +234,14 @@ class DAGExecutor:
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._setup()
+        self._exp_ids: Dict[str, torch.Tensor] = {}
+        self._routed_in: Dict[str, torch.Tensor] = {}  # received hidden state -> local experts (int32)
+        self._routed_out: set = set()                   # received expert outputs (compact rows)
+        self._deferred: Dict[str, object] = {}          # their receives, pulled by the MoE code
         if self._device_p2p:
             self.comm.attach(self)  # peers pull from this rank's arenas (IPC exchange across processes)
+            if EP_ROUTED:
+                self._plan_routed_edges()
         if autotune and self.gpu:
             _tuning.set_model(self.model_name)
             _tuning.ensure_tuned(self.gemm_shapes(), self.device)
@@ -306,13 +314,16 @@ class DAGExecutor:
         self._runner = None                     # native StepRunner replaying the recorded step
         self.issue_mode: Optional[str] = None  # "runner" / "python" for segment-replayed programs
         self._graph_exec: Optional[int] = None  # the whole-step hipGraphExec (graph_launch)
+        self._fast = None  # (launch, exec, device, stats) of a captured whole step
         self._runner_stats: Optional[StepStats] = None
         self._stream_kind = 0                   # 0 compute / 1 copy stream (recording of fills)
         self._carry_at: Dict[int, List[int]] = {}  # instr -> next step's loads issued after it
         self._carry: Dict[int, object] = {}  # next step's loads already issued -> their events
         self._copy_stream = None
+        # (device p2p transport: refills stay in order on the compute stream, so the whole step —
+        # refills, kernels and edges — is ONE hipGraph)
         if self.gpu and (PREFETCH == "1" or (PREFETCH == "auto" and p.prefetch)) \
-                and any(i.op == "load" for i in p.instrs):
+                and any(i.op == "load" for i in p.instrs) and not self._device_p2p:
             self._plan_prefetch()
             self._copy_stream = torch.cuda.Stream(self.device)
         self._post_norm: Dict[int, Task] = {}  # producer run -> the next norm it also writes
@@ -1060,8 +1071,16 @@ class DAGExecutor:
         key = ("perm", h_name, r_name)
         xp = self._moe_memo.get(key)
         if xp is None:
-            src = self._moe_route(r_name, E, top_k)[2]
-            xp = ops.moe_permute(self._flat(self._x(h_name)), src)
+            route = self._moe_route(r_name, E, top_k)
+            src = route[2]
+            rw = self._deferred.pop(h_name, None)
+            if rw is not None:  # device transport: pull the local experts' routed rows only
+                H = self.tasks[h_name].op.out_shape[-1]
+                xp = self._scratch("moe_xp", (src.numel(), H))
+                rw.pull_rows(xp.view(-1).view(torch.uint8), H * xp.element_size(), src.to(torch.int32), route[4],
+                             self._routed_in[h_name], src.numel())
+            else:
+                xp = ops.moe_permute(self._flat(self._x(h_name)), src)
             self._moe_memo[key] = xp
         return xp
 
@@ -1089,6 +1108,12 @@ class DAGExecutor:
         ins_ = t.op.inputs
         experts, r_name, res_name = ins_[:-2], ins_[-2], ins_[-1]
         idx, gate, _, slot, off = self._moe_route(r_name, a["n_experts"], a["top_k"])
+        for x in experts:
+            rw = self._deferred.pop(x, None)
+            if rw is not None:  # device transport: only the expert's count of compact rows crosses
+                v = self._views[x]
+                M, H = math.prod(v.shape[:-1]), v.shape[-1]
+                rw.pull_rows(self._act_region(x), H * v.element_size(), None, off, self._exp_ids[x], M)
         bufs = [self._x(x) for x in experts]
         key = ("ptrs", t.id)
         ptrs = self._moe_ptrs.get(key)
@@ -1358,6 +1383,9 @@ class DAGExecutor:
             self._await_fill(pid)
         for w, _ in recv_work.values():
             w.wait()
+        for w in self._deferred.values():  # (a routed receive no MoE node took: the whole region)
+            w.wait()
+        self._deferred = {}
         for w in self._pending_sends.values():
             w.wait()
         self._pending_sends = {}
@@ -1388,6 +1416,11 @@ class DAGExecutor:
                 stats.sends += 1
                 stats.bytes_sent += nbytes
             else:
+                if self._device_p2p and ins.task not in self._routed_in and ins.task not in self._routed_out:
+                    # pulled HERE, at the producer's position, as an RCCL receive completes once both
+                    # ends posted: a pull deferred to the consumer could wait for a peer that is itself
+                    # waiting for this rank to release the source (routed EP rows wait for routing)
+                    w.wait()
                 recv_work[ins.task] = (w, t0)
                 stats.recvs += 1
                 stats.bytes_recv += nbytes
@@ -1400,6 +1433,33 @@ class DAGExecutor:
     def _reset_step_state(self) -> None:
         self._moe_memo = {}
         self._pn_done = None
+        self._deferred = {}
+
+    def _plan_routed_edges(self) -> None:
+        """Expert-parallel edges that move ROUTED ROWS only (device transport): a hidden state
+        received here whose every local consumer is an expert node reading it as its tokens, and
+        an expert's output received here whose consumer is the layer's combine. Their receives
+        are left to the MoE code, which pulls — after routing on the device — only the rows the
+        local experts were routed (gathered into the expert-sorted order) and only an expert's
+        count of compact output rows: bytes = routed rows, no capacity, no host sync."""
+        received = {i.task for i in self.prog.instrs if i.op == "recv"}
+        users: Dict[str, List[Task]] = {}
+        for ins in self.prog.instrs:
+            if ins.op == "run":
+                for tid in ins.group:
+                    for d in self.tasks[tid].dependencies:
+                        users.setdefault(d, []).append(self.tasks[tid])
+        for x in received:
+            us = users.get(x, [])
+            if us and all(u.op is not None and u.op.kind == "moe_expert" and u.op.inputs[0] == x
+                          and u.id not in self._moe_batched_ids for u in us):
+                ex = sorted({u.op.attrs["expert"] for u in us})
+                self._routed_in[x] = torch.tensor(ex, dtype=torch.int32, device=self.device)
+            elif us and all(u.op is not None and u.op.kind == "moe_combine" for u in us) \
+                    and self.tasks[x].op is not None and self.tasks[x].op.kind == "moe_expert":
+                self._routed_out.add(x)
+                self._exp_ids[x] = torch.tensor([self.tasks[x].op.attrs["expert"]], dtype=torch.int32,
+                                                device=self.device)
 
     def _pre_run(self, ins, recv_work, events) -> None:
         """What a run must wait for: copy-stream fills and peer receives of its parameter
@@ -1413,6 +1473,9 @@ class DAGExecutor:
             for d in self.tasks[tid].dependencies:
                 rw = recv_work.pop(d, None)
                 if rw is not None:
+                    if d in self._routed_in or d in self._routed_out:
+                        self._deferred[d] = rw[0]  # routed rows, pulled by the MoE code
+                        continue
                     rw[0].wait()
                     if events is not None:
                         events.append((d, "recv", rw[1], self._mark()))
@@ -1471,6 +1534,8 @@ class DAGExecutor:
                 self._derived_cache.pop(("side", spec.name, views[spec.name].data_ptr()), None)
         self._param_recv[ins.param] = self._irecv(self.param_slab[off:off + total], ins.peer,
                                                   ("param", ins.param, ins.gpos))
+        if self._device_p2p:
+            self._param_recv[ins.param].wait()  # pulled at the message's position (see _post_p2p)
         self._valid.append((off, total, ins.param))
         stats.recvs += 1
         stats.peer_fills += 1
@@ -1489,6 +1554,12 @@ class DAGExecutor:
         it eagerly with a timestamp pair around every instruction and fills
         ``stats.timeline`` (kernel groups) and ``stats.events`` (kernels, parameter fills,
         p2p sends/recvs), in ms from the step start."""
+        if self._fast is not None and not profile:  # a captured whole step: one graph launch
+            self._fast[0](self._fast[1], self._fast[2])
+            if self._mlp_fused:
+                self.check_mlp_fused()
+            self.last = self._fast[3]
+            return self._fast[3]
         stats = StepStats()
         if self._runner is not None and profile:
             self._leave_runner()
@@ -1505,8 +1576,8 @@ class DAGExecutor:
         elif self._graph is not None and not profile:
             if self.trace:
                 Roctx.push(f"graph_step:rank{self.prog.rank}")
-            if self._graph_exec is not None:
-                ops.ext().graph_launch(self._graph_exec, self.device.index or 0)  # GIL released
+            if self._graph_exec is not None:  # GIL released
+                ops.ext().graph_launch(self._graph_exec, torch.cuda.current_stream(self.device).cuda_stream)
             else:
                 self._graph.replay()
             if self.trace:
@@ -1576,6 +1647,7 @@ class DAGExecutor:
         if not self.use_graph:
             return False
         self._drop_runner()  # its hipGraphExec handles belong to the graphs a re-capture replaces
+        self._fast = None
         if self._device_p2p and self._copy_stream is not None:
             return False  # copy-stream refills beside device edges: the step stays eager
         if self._copy_stream is not None or (self.prog.has_comm and not self._device_p2p):
@@ -1606,6 +1678,11 @@ class DAGExecutor:
         self._sync()
         self._graph = g
         self._graph_exec = g.raw_cuda_graph_exec()
+        if not (self.trace or self.debug):
+            # step()'s fast path: the launch function, its arguments, the (static) stats
+            # (the stream current at capture: the rank's own, where every later step is issued)
+            self._fast = (ops.ext().graph_launch, self._graph_exec, cur.cuda_stream,
+                          StepStats(kernels=self.prog.n_kernels))
         return True
 
     def _sync(self) -> None:
@@ -1813,7 +1890,7 @@ class DAGExecutor:
             return {}  # whole-step graphs only
 
         def step_ms():
-            self._graph = self._graph_exec = None
+            self._graph = self._graph_exec = self._fast = None
             self.capture()
             for _ in range(3):
                 self._graph.replay()
@@ -1873,7 +1950,7 @@ class DAGExecutor:
                 changes[f"{M}x{N}x{K}{tg}"] = (tuple(cur), tuple(best), round(best_ms, 4))
                 base = best_ms
         tuning.save()
-        self._graph = self._graph_exec = None
+        self._graph = self._graph_exec = self._fast = None
         self.capture()
         return changes
 

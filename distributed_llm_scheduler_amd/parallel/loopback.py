@@ -38,6 +38,8 @@ class LoopbackRun:
     step_ms: List[float] = field(default_factory=list)
     # host time per step.step() call (µs, mean over the timed steps): what issuing a step costs
     host_us: List[float] = field(default_factory=list)
+    # device transport: each rank's error word after the warm-up steps (then cleared)
+    warmup_errors: List[int] = field(default_factory=list)
 
 
 def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = True, delay_us: float = 20.0,
@@ -70,11 +72,12 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
         if not gpu:
             raise ValueError("the device p2p transport needs a GPU")
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-        if world + 1 > queues:
-            # a pull / ack wait spins on its rank's stream; a peer stream on the same hardware
-            # queue would be queued behind it (the waits time out: wrong numbers, not a hang)
+        if 4 * world > queues:
+            # a pull / ack wait spins on its rank's stream; a peer's stream (compute, refill copy
+            # or capture: up to 3 per rank, + the default) on the same hardware queue would be
+            # queued behind it — every wait then times out (wrong numbers, never a hang)
             raise ValueError(f"device transport with {world} ranks in one process needs GPU_MAX_HW_QUEUES >= "
-                             f"{world + 1} (set before the first CUDA call; it is {queues})")
+                             f"{4 * world} (set before the first CUDA call; it is {queues})")
         from .devp2p import DeviceP2PGroup, DeviceP2PWorld
         dw = DeviceP2PWorld(plan, device, range(world), delay_us=delay_us, poison=poison)
         groups = [DeviceP2PGroup(dw, r) for r in range(world)]
@@ -100,6 +103,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     stats = [None] * world
     ms = [0.0] * world
     host_us = [0.0] * world
+    warm_err = [0] * world
     errors = []
     start = threading.Barrier(world)
 
@@ -119,6 +123,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
                 if transport == "device":
                     streams[r].synchronize()
                     start.wait()  # every rank past its warm-up before any error word is cleared
+                    warm_err[r] = ex.comm.errors()
                     ex.comm.reset_errors()
                 elif cpu_runner and not gpu and not ex.build_runner():
                     raise RuntimeError("CPU step runner refused the program")
@@ -166,9 +171,8 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
             raise RuntimeError("single_issue needs every rank's step captured as one hipGraph")
         t0 = time.perf_counter()
         for _ in range(steps):
-            for r, ex in enumerate(exs):
-                with torch.cuda.stream(streams[r]):
-                    stats[r] = ex.step()
+            for r, ex in enumerate(exs):  # (a captured step launches on its rank's own stream)
+                stats[r] = ex.step()
         issue = time.perf_counter() - t0
         for r in range(world):
             streams[r].synchronize()
@@ -183,7 +187,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
         raise RuntimeError(f"loopback harness: rank {r} failed: {e!r}") from e
     hub = getattr(groups[0], "hub", None)
     issue = [ex.issue_mode or ("graph" if ex._graph is not None else None) for ex in exs]
-    return LoopbackRun(exs, stats, hub, issue, ms, host_us=host_us)
+    return LoopbackRun(exs, stats, hub, issue, ms, host_us=host_us, warmup_errors=warm_err)
 
 
 class _Null:

@@ -9,7 +9,7 @@ from __future__ import annotations
 import json
 import os
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from ..core import Node, get_scheduler
 from ..core.task import Task
@@ -415,8 +415,34 @@ def plan_stats(p: Plan) -> Dict:
         # distinct (producer, consumer GPU) transfers: what the p2p edges really move
         "cross_gpu_transfers": len({(d, r) for tid, r in p.placement.items() for d in tmap[tid].dependencies
                                     if d in p.placement and p.placement[d] != r}),
+        # what the same transfers move when expert-parallel edges carry routed rows only (the
+        # device transport, DAGExecutor._plan_routed_edges): expected M*k/E rows per expert
+        "cross_gpu_bytes_routed": _routed_cross_bytes(p, tmap),
         **_steady_stats(p.scheduler),
     }
+
+
+def _routed_cross_bytes(p: Plan, tmap) -> int:
+    """Cross-GPU bytes per step with routed-row expert edges: a hidden state sent to a GPU whose
+    consumers there are experts moves the rows routed to those experts (expected M*k/E per
+    expert), an expert's output its routed rows; every other transfer its whole buffer."""
+    total = 0
+    users_at: Dict[Tuple[str, int], List[Task]] = {}
+    for tid, r in p.placement.items():
+        for d in tmap[tid].dependencies:
+            if d in p.placement and p.placement[d] != r:
+                users_at.setdefault((d, r), []).append(tmap[tid])
+    for (d, r), users in users_at.items():
+        t = tmap[d]
+        exp_users = [u for u in users if u.op is not None and u.op.kind == "moe_expert" and u.op.inputs[0] == d]
+        if users and len(exp_users) == len(users):
+            a = exp_users[0].op.attrs
+            total += int(t.xfer_bytes * a["top_k"] * len(exp_users) / a["n_experts"])
+        elif t.op is not None and t.op.kind == "moe_expert":
+            total += int(t.xfer_bytes * t.op.attrs["top_k"] / t.op.attrs["n_experts"])
+        else:
+            total += t.xfer_bytes
+    return total
 
 
 def _steady_stats(s) -> Dict:

@@ -8,11 +8,12 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 # Hardware queues per process (HIP's default is 4). The single-GPU multi-rank harness with the
-# device p2p transport runs up to 4 ranks' streams in this ONE process, each of which may hold
-# a kernel spinning on a peer's flag: a rank stream that shares a hardware queue with another
-# rank's queues that rank's kernels behind the spin (parallel/loopback.py). Set before HIP
-# initialises (the first CUDA call), well under the pool's limit of 32.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# device p2p transport runs up to 4 ranks in this ONE process — compute, copy and capture
+# streams each — and a rank's compute stream may hold a kernel spinning on a peer's flag: a
+# stream sharing that hardware queue would be queued behind the spin (parallel/loopback.py).
+# Set before HIP initialises (the first CUDA call), under the pool's limit of 32.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 
 def pytest_configure(config):
