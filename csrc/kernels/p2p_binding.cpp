@@ -121,7 +121,17 @@ void graph_launch(int64_t exec, int64_t stream) {
 
 }  // namespace
 
+// A stream of its own (hipStreamCreateWithFlags, non-blocking), outside torch's stream pool:
+// the pool hands out 32 streams round-robin over the device's hardware queues, so two pool
+// streams can share a queue; HIP gives consecutively created streams consecutive queues.
+int64_t stream_create() {
+  hipStream_t s = nullptr;
+  C10_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return reinterpret_cast<int64_t>(s);
+}
+
 void register_p2p(py::module& m) {
+  m.def("stream_create", &stream_create);
   m.def("p2p_tick", &p2p_tick);
   m.def("p2p_notify", &p2p_notify);
   m.def("p2p_pull", &p2p_pull, py::arg("src"), py::arg("dst"), py::arg("ready"), py::arg("ack_remote"),

@@ -220,6 +220,14 @@ class _RecvWork:
                                   m.step, m.err, _TICKS, m.moved)
 
 
+class _NoWork:
+    def wait(self):
+        pass
+
+    def pull_rows(self, *a, **k):
+        pass
+
+
 class DeviceComm:
     kind = "device"
 
@@ -231,6 +239,11 @@ class DeviceComm:
         self.pg = group.pg
         self.mb = self.w.mail[self.rank]
         self.e = ops.ext()
+        # a DRY step posts nothing and waits for nothing (no tick either, on every rank alike):
+        # the single-GPU harness runs one per rank, one rank at a time, before the real steps, so
+        # a rank's first-step allocations — which may synchronise the whole device — never wait
+        # behind a peer rank's spinning pull in the same process
+        self.dry = False
 
     def attach(self, ex) -> None:
         """Register the executor's arenas (their base addresses are what peers pull from)."""
@@ -239,7 +252,8 @@ class DeviceComm:
             self.w.exchange(self.pg)
 
     def begin_step(self) -> None:
-        self.e.p2p_tick(self.mb.step)
+        if not self.dry:
+            self.e.p2p_tick(self.mb.step)
 
     def _slot(self, src: int, dst: int, key) -> int:
         try:
@@ -249,6 +263,8 @@ class DeviceComm:
 
     def isend(self, buf: torch.Tensor, peer: int, key=None):
         slot = self._slot(self.rank, peer, key)
+        if self.dry:
+            return _NoWork()
         if self.w.delay_us > 0:  # single-GPU harness: the notify lands late (a missing wait shows)
             self.e.p2p_delay(self.w.delay_us, self.mb.step)
         self.e.p2p_notify(self.mb.ready_addr(self.w.bases[peer]["mail"], slot), self.mb.step)
@@ -262,6 +278,8 @@ class DeviceComm:
         if region is None or region.numel() != nbytes:
             raise RuntimeError(f"device p2p: receive region of {key} does not match the producer's "
                                f"({None if region is None else region.numel()} vs {nbytes} bytes)")
+        if self.dry:
+            return _NoWork()
         if self.w.poison:
             region.fill_(0xFF)  # bf16 NaN until the pull lands
         return _RecvWork(self, slot, region, (peer, arena, off))

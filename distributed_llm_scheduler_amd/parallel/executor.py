@@ -1653,11 +1653,16 @@ class DAGExecutor:
         if self._copy_stream is not None or (self.prog.has_comm and not self._device_p2p):
             return self.capture_segments()
         self._sync()
-        s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            self._step_body(StepStats())  # warm the residency state on the capture stream
-        torch.cuda.current_stream(self.device).wait_stream(s)
+        if self._device_p2p:
+            # (on this rank's own stream: a warm step spinning on a peer's flag from a pooled side
+            # stream could share a hardware queue with that peer's stream — parallel/loopback.py)
+            self._step_body(StepStats())
+        else:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._step_body(StepStats())  # warm the residency state on the capture stream
+            torch.cuda.current_stream(self.device).wait_stream(s)
         self._sync()
         # captured on a side stream without torch.cuda.graph's device-wide synchronize (ranks
         # sharing one GPU may be capturing their own graphs meanwhile)

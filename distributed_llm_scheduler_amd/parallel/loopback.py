@@ -87,7 +87,10 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
         raise ValueError(f"unknown transport {transport!r}")
     store = store or runtime.make_store(plan)
     # executors are built on this thread (autotuning and weight transforms are not thread-safe)
-    streams = [torch.cuda.Stream(device) for _ in range(world)] if gpu else [None] * world
+    if gpu and transport == "device":
+        streams = _rank_streams(device, world)
+    else:
+        streams = [torch.cuda.Stream(device) for _ in range(world)] if gpu else [None] * world
     exs = []
     for r in range(world):
         if gpu:
@@ -98,6 +101,17 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
             exs.append(runtime.make_executor(plan, r, device, store, pg=groups[r], use_graph=False))
     if gpu:
         torch.cuda.synchronize(device)
+    if transport == "device":
+        # one DRY step per rank, one rank at a time (no p2p, garbage numbers): first-step
+        # allocations and weight transforms — some synchronise the whole device — happen before
+        # any rank's kernels spin on a peer's flag in this shared process (a multi-process job
+        # needs none: there a device-wide wait waits for that process's own streams only)
+        for r, ex in enumerate(exs):
+            ex.comm.dry = True
+            with torch.cuda.stream(streams[r]):
+                ex.step()
+            ex.comm.dry = False
+            streams[r].synchronize()
     if before_steps is not None:
         before_steps(exs)
     stats = [None] * world
@@ -188,6 +202,23 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     hub = getattr(groups[0], "hub", None)
     issue = [ex.issue_mode or ("graph" if ex._graph is not None else None) for ex in exs]
     return LoopbackRun(exs, stats, hub, issue, ms, host_us=host_us, warmup_errors=warm_err)
+
+
+_RAW_STREAMS: dict = {}
+
+
+def _rank_streams(device, world: int):
+    """Streams for the device transport's ranks: created once per process with hipStreamCreate,
+    consecutively — so each sits on a hardware queue of its own (GPU_MAX_HW_QUEUES of them),
+    unlike torch's pooled streams, which share queues round-robin (measured:
+    benchmarks/hwq_probe.py) — and reused by every later run. A rank's spinning wait must never
+    queue another rank's kernels behind it."""
+    from .. import ops
+
+    have = _RAW_STREAMS.setdefault(str(device), [])
+    while len(have) < world:
+        have.append(torch.cuda.ExternalStream(ops.ext().stream_create(), device=device))
+    return have[:world]
 
 
 class _Null:
