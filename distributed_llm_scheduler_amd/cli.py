@@ -93,6 +93,8 @@ def cmd_run(a) -> int:
         pg = dist.group.WORLD
     p = _plan(a, world, resume=a.resume)
     store = runtime.make_store(p, seed=a.seed, device_init=gpu and a.init == "device" and runtime.device_init_ok(p, rank))
+    if gpu and pg is not None:  # DLS_P2P=device: cross-GPU edges moved by kernels (parallel/devp2p.py)
+        pg = runtime.p2p_group(p, rank, dev, pg)
     ex = runtime.make_executor(p, rank, dev, store, pg=pg, use_graph=gpu and not a.no_graph, trace=a.roctx)
 
     def sync():
