@@ -16,7 +16,7 @@ from distributed_llm_scheduler_amd.parallel import devp2p, runtime  # noqa: E402
 from distributed_llm_scheduler_amd.parallel.loopback import run_loopback  # noqa: E402
 import test_loopback as T  # noqa: E402
 
-devp2p._TICKS = int(2e9)
+devp2p._TICKS = int(float(os.environ.get("TICKS", "2e9")))  # 100 MHz wall-clock ticks per wait
 cases = sys.argv[1].split(",") if len(sys.argv) > 1 else T.DEVICE_CASES
 worlds = [int(w) for w in sys.argv[2].split(",")] if len(sys.argv) > 2 else [2, 4]
 single = os.environ.get("SINGLE", "1") == "1"

@@ -151,6 +151,20 @@ bool launch_moe_gate_route(const void* x, int ldx, const void* wg, int M, int H,
                            int* ticket, int32_t* topk_idx, float* topk_w, int32_t* src_rows, int32_t* slot_of,
                            int32_t* offsets, hipStream_t s);
 void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int rows, int H, hipStream_t s);
+// cross-request expert batch: per group g = (request req[g], expert expert[g]) the device-side
+// row range of that request's routing (off[req]: int32 [E+1]) placed at base[req] — writes the
+// groups' offsets [G+1] and the token row of every sorted row (a_rows) for one grouped launch
+constexpr int kXbatchMaxReq = 16, kXbatchMaxGroups = 64;
+struct XbatchIndexArgs {
+  const int32_t* off[kXbatchMaxReq];
+  int32_t base[kXbatchMaxReq];
+  int32_t req[kXbatchMaxGroups];
+  int32_t expert[kXbatchMaxGroups];
+  int G;
+  int32_t* offsets;
+  int32_t* a_rows;
+};
+void launch_moe_xbatch_index(const XbatchIndexArgs& a, hipStream_t s);
 void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
                         int topk, int H, const int32_t* range, hipStream_t s);
 // X [rows][K] sorted by expert, offsets [E+1], W [E][N][K] -> Y [rows][N]

@@ -522,6 +522,38 @@ void launch_moe_permute(const void* x, const int32_t* src_rows, void* out, int r
                      rows, H);
 }
 
+// Cross-request expert batch (executor._run_moe_xbatch): group g is one (request, expert) pair
+// placed on this GPU; its rows are rows [off_q[e], off_q[e+1]) of request q's expert-sorted block,
+// which starts at row base[q] of the batch's token matrix. One workgroup writes the groups'
+// offsets (prefix sums of their device-side counts) and every sorted row's token row, so ONE
+// grouped launch pair runs all of them with each weight panel streamed once (no host sync).
+__global__ __launch_bounds__(256) void xbatch_index_kernel(XbatchIndexArgs a) {
+  __shared__ int lo[kXbatchMaxGroups];
+  __shared__ int start[kXbatchMaxGroups + 1];
+  const int t = threadIdx.x;
+  if (t < a.G) {
+    const int32_t* off = a.off[a.req[t]];
+    const int e = a.expert[t];
+    lo[t] = a.base[a.req[t]] + off[e];
+    start[t + 1] = off[e + 1] - off[e];
+  }
+  __syncthreads();
+  if (t == 0) {
+    start[0] = 0;
+    for (int g = 0; g < a.G; ++g) start[g + 1] += start[g];
+  }
+  __syncthreads();
+  if (t <= a.G) a.offsets[t] = start[t];
+  for (int g = 0; g < a.G; ++g) {
+    const int n = start[g + 1] - start[g];
+    for (int r = t; r < n; r += 256) a.a_rows[start[g] + r] = lo[g] + r;
+  }
+}
+
+void launch_moe_xbatch_index(const XbatchIndexArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(xbatch_index_kernel, dim3(1), dim3(256), 0, s, a);
+}
+
 void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
                         int topk, int H, const int32_t* range, hipStream_t s) {
   hipLaunchKernelGGL(combine_kernel, dim3((M + 3) / 4), dim3(256), 0, s, (const bf16*)expert_out, slot_of, weights,

@@ -500,14 +500,55 @@ std::vector<at::Tensor> moe_gate_route(const at::Tensor& x, const at::Tensor& wg
   return {idx, w, src, slot, off};
 }
 
-at::Tensor moe_permute(const at::Tensor& x, const at::Tensor& src_rows) {
+at::Tensor moe_permute(const at::Tensor& x, const at::Tensor& src_rows, const c10::optional<at::Tensor>& out_) {
   check_bf16(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "x must be contiguous [M][H]");
   TORCH_CHECK(src_rows.scalar_type() == at::kInt && src_rows.is_contiguous(), "src_rows must be int32");
-  auto out = at::empty({src_rows.numel(), x.size(1)}, x.options());
+  at::Tensor out;
+  if (out_.has_value()) {
+    out = *out_;
+    check_bf16(out, "out");
+    TORCH_CHECK(out.is_contiguous() && out.dim() == 2 && out.size(0) == src_rows.numel() && out.size(1) == x.size(1),
+                "out must be contiguous [rows][H]");
+  } else {
+    out = at::empty({src_rows.numel(), x.size(1)}, x.options());
+  }
   launch_moe_permute(x.data_ptr(), src_rows.data_ptr<int32_t>(), out.data_ptr(), (int)src_rows.numel(),
                      (int)x.size(1), cur_stream());
   return out;
+}
+
+// offs: each request's routing offsets (int32 [E+1], on the GPU); groups g: (reqs[g], experts[g]);
+// bases[q]: row of request q's expert-sorted block in the batch's token matrix
+void moe_xbatch_index(const std::vector<at::Tensor>& offs, const std::vector<int64_t>& reqs,
+                      const std::vector<int64_t>& experts, const std::vector<int64_t>& bases, at::Tensor& offsets,
+                      at::Tensor& a_rows) {
+  const int Q = (int)offs.size(), G = (int)reqs.size();
+  TORCH_CHECK(Q >= 1 && Q <= kXbatchMaxReq && (int)bases.size() == Q, "1..", kXbatchMaxReq, " requests, one base each");
+  TORCH_CHECK(G >= 1 && G <= kXbatchMaxGroups && (int)experts.size() == G, "1..", kXbatchMaxGroups, " groups");
+  TORCH_CHECK(offsets.is_cuda() && offsets.scalar_type() == at::kInt && offsets.numel() == G + 1, "offsets int32 [G+1]");
+  TORCH_CHECK(a_rows.is_cuda() && a_rows.scalar_type() == at::kInt && a_rows.is_contiguous(), "a_rows int32");
+  XbatchIndexArgs a{};
+  int64_t E = -1;
+  for (int q = 0; q < Q; ++q) {
+    TORCH_CHECK(offs[q].is_cuda() && offs[q].scalar_type() == at::kInt && offs[q].is_contiguous(),
+                "routing offsets: int32 on the GPU");
+    TORCH_CHECK(E < 0 || offs[q].numel() == E + 1, "every request routes over the same experts");
+    E = offs[q].numel() - 1;
+    a.off[q] = offs[q].data_ptr<int32_t>();
+    a.base[q] = (int32_t)bases[q];
+  }
+  for (int g = 0; g < G; ++g) {
+    TORCH_CHECK(reqs[g] >= 0 && reqs[g] < Q && experts[g] >= 0 && experts[g] < E, "group (request, expert) range");
+    a.req[g] = (int32_t)reqs[g];
+    a.expert[g] = (int32_t)experts[g];
+  }
+  // a_rows holds every group's rows: the caller sizes it to the requests' blocks (the device
+  // counts of distinct (request, expert) pairs never exceed their requests' sorted orders)
+  a.G = G;
+  a.offsets = offsets.data_ptr<int32_t>();
+  a.a_rows = a_rows.data_ptr<int32_t>();
+  launch_moe_xbatch_index(a, cur_stream());
 }
 
 at::Tensor moe_combine(const at::Tensor& eo, const at::Tensor& slot_of, const at::Tensor& w,
@@ -747,7 +788,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_align", &moe_align);
   m.def("moe_route", &moe_route);
   m.def("moe_gate_route", &moe_gate_route);
-  m.def("moe_permute", &moe_permute);
+  m.def("moe_permute", &moe_permute, py::arg("x"), py::arg("src_rows"), py::arg("out") = py::none());
+  m.def("moe_xbatch_index", &moe_xbatch_index);
   m.def("moe_combine", &moe_combine, py::arg("expert_out"), py::arg("slot_of"), py::arg("weights"),
         py::arg("range") = py::none(), py::arg("out") = py::none());
   m.def("grouped_gemm", &grouped_gemm, py::arg("X"), py::arg("offsets"), py::arg("W"), py::arg("act") = 0);

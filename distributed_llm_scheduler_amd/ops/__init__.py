@@ -532,10 +532,35 @@ def moe_gate_route(x, w_gate, topk, logits):
     return moe_route(logits.view(x.shape[0], -1), topk, w_gate.shape[0])
 
 
-def moe_permute(x, src_rows):
+def moe_permute(x, src_rows, out=None):
     if _gpu(x):
-        return ext().moe_permute(x.contiguous(), src_rows)
-    return x[src_rows.long()]
+        return ext().moe_permute(x.contiguous(), src_rows, out)
+    y = x[src_rows.long()]
+    return out.copy_(y) if out is not None else y
+
+
+XBATCH_MAX_REQ, XBATCH_MAX_GROUPS = 16, 64  # kXbatchMaxReq / kXbatchMaxGroups (kernels.h)
+
+
+def moe_xbatch_index(offs, reqs, experts, bases, offsets, a_rows):
+    """Row map of a cross-request expert batch (one grouped launch for several requests'
+    experts): group g = (request ``reqs[g]``, expert ``experts[g]``) takes rows
+    [offs[q][e], offs[q][e+1]) of request q's expert-sorted block, which starts at row
+    ``bases[q]`` of the batch's token matrix. Writes ``offsets`` (int32 [G+1], prefix sums of
+    the groups' device-side counts) and ``a_rows`` (the token row of each sorted row) — one
+    workgroup on the GPU, no host sync."""
+    if _gpu(offsets):
+        ext().moe_xbatch_index(list(offs), list(reqs), list(experts), list(bases), offsets, a_rows)
+        return offsets, a_rows
+    a_rows.zero_()
+    o = 0
+    offsets[0] = 0
+    for g, (q, e) in enumerate(zip(reqs, experts)):
+        lo, hi = int(offs[q][e]), int(offs[q][e + 1])
+        a_rows[o:o + hi - lo] = torch.arange(bases[q] + lo, bases[q] + hi, dtype=a_rows.dtype)
+        o += hi - lo
+        offsets[g + 1] = o
+    return offsets, a_rows
 
 
 def moe_combine(expert_out, slot_of, weights, slot_range=None, out=None):

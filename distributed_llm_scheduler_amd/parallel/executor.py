@@ -140,6 +140,9 @@ EMBED_STATS = os.environ.get("DLS_EMBED_STATS", "1") != "0"
 PREFETCH = os.environ.get("DLS_PREFETCH", "auto")
 # one grouped launch pair per MoE layer for the experts co-located on this rank (GPU)
 MOE_BATCH = os.environ.get("DLS_MOE_BATCH", "1") != "0"
+# one grouped launch pair per co-run span (program.plan_coruns): a layer's experts on this rank
+# over every request (expert parallelism with data-parallel attention)
+MOE_XBATCH = os.environ.get("DLS_MOE_XBATCH", "1") != "0"
 # MoE routing in one launch (router + align, ops.moe_route) and the grouped gate/up GEMM
 # gathering its token rows itself (no permute kernel); 0 restores the separate launches
 MOE_FUSED_ROUTE = os.environ.get("DLS_MOE_FUSED_ROUTE", "1") != "0"
@@ -238,6 +241,7 @@ class DAGExecutor:
         self._routed_in: Dict[str, torch.Tensor] = {}  # received hidden state -> local experts (int32)
         self._routed_out: set = set()                   # received expert outputs (compact rows)
         self._deferred: Dict[str, object] = {}          # their receives, pulled by the MoE code
+        self._pull_at: Dict[int, List[str]] = {}        # instruction -> hidden states pulled after it
         if self._device_p2p:
             self.comm.attach(self)  # peers pull from this rank's arenas (IPC exchange across processes)
             if EP_ROUTED:
@@ -304,6 +308,7 @@ class DAGExecutor:
             self._zero_in_embedding = first is not None and first.op.kind == "embedding"
             self._zero_run = runs[0] if self._zero_in_embedding else None
         self._plan_moe_batches()
+        self._plan_moe_xbatch()
         self._hoist: Dict[int, List[int]] = {}
         self._await: Dict[str, object] = {}  # group -> copy-stream event its first reader waits on
         self._segments: Dict[int, Tuple[int, object]] = {}  # segment start -> (end, hipGraph)
@@ -435,6 +440,91 @@ class DAGExecutor:
                 if MOE_FUSED_ROUTE:  # the layer's router node computes its logits AND the routing
                     self._gate_route[t0.op.inputs[1]] = (E, t0.op.attrs["top_k"])
             i = j
+
+    def _plan_moe_xbatch(self) -> None:
+        """The program's co-run spans (program.plan_coruns) issued as ONE grouped launch pair
+        at the span's first run: one MoE layer's expert nodes placed on this rank, over every
+        request. With data-parallel attention and expert parallelism every request's routed
+        rows reach this GPU in the same layer, so each expert's weights stream once per layer
+        instead of once per request. Re-checked against the instructions: only sends,
+        parameter loads and receives no member reads lie between the members."""
+        self._xbatch: Dict[int, Tuple[List[int], List[int]]] = {}
+        self._xskip: set = set()
+        self._xfirst: Dict[str, List[int]] = {}  # first member's output task -> member indices
+        self._xbatched_ids: set = set()
+        self._xbufs: Dict[int, tuple] = {}
+        self._xblock: Dict[str, Tuple[int, int, int]] = {}  # hidden state -> (block, rows, width)
+        self._xpb_shape: Tuple[int, int] = (0, 1)  # the batches' token matrix (one, shared)
+        if not MOE_XBATCH:
+            return
+        ins = self.prog.instrs
+        run_at = {x.task: i for i, x in enumerate(ins) if x.op == "run"}
+        for span in self.prog.coruns:
+            idx = [run_at.get(t) for t in span]
+            if None in idx or any(k in self._moe_batch or k in self._moe_skip for k in idx):
+                continue
+            ts = [self.tasks[ins[k].group[0]] for k in idx]
+            if len({t.op.inputs[1] for t in ts}) > ops.XBATCH_MAX_REQ or len(ts) > ops.XBATCH_MAX_GROUPS:
+                continue
+            reads = {d for t in ts for d in t.dependencies}
+            between = [k for k in range(idx[0], idx[-1]) if k not in idx]
+            if any(not (ins[k].op in ("send", "load") or (ins[k].op == "recv" and ins[k].task not in reads))
+                   or (ins[k].op == "load" and ins[k].peer >= 0) for k in between):
+                continue
+            self._xbatch[idx[0]] = (idx, [k for k in between if ins[k].op == "load"])
+            reqs = list(dict.fromkeys(t.op.inputs[0] for t in ts))
+            R = math.prod(self.tasks[reqs[0]].op.out_shape[:-1]) * ts[0].op.attrs["top_k"]
+            H = self.tasks[reqs[0]].op.out_shape[-1]
+            for q, h in enumerate(reqs):  # (a routed hidden state is pulled straight into its block)
+                self._xblock[h] = (q, R, H)
+            if len(reqs) * R * H > math.prod(self._xpb_shape):
+                self._xpb_shape = (len(reqs) * R, H)
+            self._xskip |= set(idx[1:])
+            self._xfirst[ins[idx[0]].task] = idx
+            self._xbatched_ids |= {t.id for t in ts}
+
+    def _run_moe_xbatch(self, i: int, stats: StepStats) -> None:
+        """A co-run span as one grouped launch pair: group g = (request q, expert e) with the
+        device-side row range of q's routing; each request's expert-sorted rows are gathered (over
+        the device transport: pulled, the local experts' routed rows only) into its block of one
+        token matrix, and one index launch maps the groups' rows into it (no host sync)."""
+        members, loads = self._xbatch[i]
+        for ld in loads:  # fixed regions (no evictions): map the span's groups up front
+            self._load(ld, self.prog.instrs[ld].param, stats)
+        tasks = [self.tasks[self.prog.instrs[m].group[0]] for m in members]
+        a = tasks[0].op.attrs
+        E, K, F = a["n_experts"], a["top_k"], a["ffn"]
+        reqs = list(dict.fromkeys((t.op.inputs[0], t.op.inputs[1]) for t in tasks))
+        routes = [self._moe_route(r, E, K) for _, r in reqs]
+        R = routes[0][2].numel()
+        xp = self._scratch("moe_xpb", self._xpb_shape)
+        for q, (h, r) in enumerate(reqs):
+            self._moe_permuted(h, r, E, K, out=xp[q * R:(q + 1) * R])
+        bufs = self._xbufs.get(i)
+        if bufs is None:  # (first, eager step: never allocated during capture)
+            bufs = (torch.zeros(len(tasks) + 1, dtype=torch.int32, device=self.device),
+                    torch.zeros(len(reqs) * R, dtype=torch.int32, device=self.device))
+            self._xbufs[i] = bufs
+        offsets, a_rows = bufs
+        ops.moe_xbatch_index([rt[4] for rt in routes], [reqs.index((t.op.inputs[0], t.op.inputs[1])) for t in tasks],
+                             [t.op.attrs["expert"] for t in tasks], [q * R for q in range(len(reqs))], offsets, a_rows)
+        w13 = [self._prep(t.op.weights["w_gate_up"], None, None, interleave=True)[0] for t in tasks]
+        w2 = [self._w(t.op.weights["w_down"]) for t in tasks]
+        outs = [self._flat(self._views[t.id]) for t in tasks]
+        hbuf = self._scratch("moe_h", (len(reqs) * R, F))
+        hint = max(1, R // E)
+        if not self.gpu:
+            ops.gemm_grouped(xp, w13, offsets, act="swiglu", out=hbuf, rows_hint=hint, a_rows=a_rows)
+            ops.gemm_grouped(hbuf, w2, offsets, outs=outs, rows_hint=hint)
+            return
+        ptrs = tuple(w.data_ptr() for w in w13 + w2 + outs)
+        cached = self._moe_bufs.get(("x", i))
+        if cached is None or cached[0] != ptrs:
+            mk = lambda ts: torch.tensor([x.data_ptr() for x in ts], dtype=torch.int64, device=self.device)  # noqa: E731
+            cached = (ptrs, mk(w13), mk(w2), mk(outs))
+            self._moe_bufs[("x", i)] = cached
+        ops.gemm_grouped(xp, w13, offsets, act="swiglu", out=hbuf, w_ptrs=cached[1], rows_hint=hint, a_rows=a_rows)
+        ops.gemm_grouped(hbuf, w2, offsets, outs=outs, w_ptrs=cached[2], out_ptrs=cached[3], rows_hint=hint)
 
     def _plan_mlp_fused(self) -> None:
         """Pairs (fc1 group i, fc2 group j) of a pre-norm MLP block that run as ONE launch:
@@ -638,7 +728,8 @@ class DAGExecutor:
                     N, K = spec[n].shape
                     if op.kind == "moe_expert":
                         hint = max(1, M * op.attrs["top_k"] // op.attrs["n_experts"])
-                        v = "g" if t.id in self._moe_batched_ids else "r"  # grouped launch or one range
+                        grouped = t.id in self._moe_batched_ids or t.id in self._xbatched_ids
+                        v = "g" if grouped else "r"  # grouped launch or one range
                         shapes.add((hint, N, K, ("s" if wk == "w_gate_up" else "") + v))
                     elif op.kind == "swiglu_mlp" and wk == "w_gate_up":
                         shapes.add((M, N, K, "s"))
@@ -1067,7 +1158,9 @@ class DAGExecutor:
             self._moe_memo[key] = r
         return r
 
-    def _moe_permuted(self, h_name: str, r_name: str, E: int, top_k: int):
+    def _moe_permuted(self, h_name: str, r_name: str, E: int, top_k: int, out: Optional[torch.Tensor] = None):
+        """The layer's hidden state in expert-sorted row order (once per step and request; into
+        ``out`` when given: a cross-request batch's block)."""
         key = ("perm", h_name, r_name)
         xp = self._moe_memo.get(key)
         if xp is None:
@@ -1076,12 +1169,16 @@ class DAGExecutor:
             rw = self._deferred.pop(h_name, None)
             if rw is not None:  # device transport: pull the local experts' routed rows only
                 H = self.tasks[h_name].op.out_shape[-1]
-                xp = self._scratch("moe_xp", (src.numel(), H))
+                # one buffer per request: another request's experts may run between two of this one's
+                xp = out if out is not None else self._scratch("moe_xp/" + h_name.split("/")[0], (src.numel(), H))
                 rw.pull_rows(xp.view(-1).view(torch.uint8), H * xp.element_size(), src.to(torch.int32), route[4],
                              self._routed_in[h_name], src.numel())
             else:
-                xp = ops.moe_permute(self._flat(self._x(h_name)), src)
+                xp = ops.moe_permute(self._flat(self._x(h_name)), src, out=out)
             self._moe_memo[key] = xp
+        elif out is not None and xp.data_ptr() != out.data_ptr():
+            out.copy_(xp)
+            xp = out
         return xp
 
     def _moe_expert(self, t: Task, out: torch.Tensor) -> None:
@@ -1108,12 +1205,6 @@ class DAGExecutor:
         ins_ = t.op.inputs
         experts, r_name, res_name = ins_[:-2], ins_[-2], ins_[-1]
         idx, gate, _, slot, off = self._moe_route(r_name, a["n_experts"], a["top_k"])
-        for x in experts:
-            rw = self._deferred.pop(x, None)
-            if rw is not None:  # device transport: only the expert's count of compact rows crosses
-                v = self._views[x]
-                M, H = math.prod(v.shape[:-1]), v.shape[-1]
-                rw.pull_rows(self._act_region(x), H * v.element_size(), None, off, self._exp_ids[x], M)
         bufs = [self._x(x) for x in experts]
         key = ("ptrs", t.id)
         ptrs = self._moe_ptrs.get(key)
@@ -1297,6 +1388,7 @@ class DAGExecutor:
                 if k not in pending:
                     self._prefetch(k, ev0, stats, pending, events)
         segs = self._segments if (events is None and not tr) else {}
+        pulls = sorted(self._pull_at)
         n_ins = len(self.prog.instrs)
         i = -1
         while i + 1 < n_ins:
@@ -1364,6 +1456,9 @@ class DAGExecutor:
                 else:
                     self._issue_run(i, ins, stats, events)
                 stats.kernels += 1
+            while pulls and pulls[0] <= i:  # routed hidden rows whose router logits are here now
+                for h in self._pull_at[pulls.pop(0)]:
+                    self._pull_hidden_rows(h)
             if hoist and i in self._carry_at:  # the next step's first refills, under this tail
                 evc = self._new_event()
                 self._record(evc)
@@ -1416,10 +1511,16 @@ class DAGExecutor:
                 stats.sends += 1
                 stats.bytes_sent += nbytes
             else:
-                if self._device_p2p and ins.task not in self._routed_in and ins.task not in self._routed_out:
+                if self._device_p2p and ins.task in self._routed_out:
+                    self._pull_expert_rows(ins.task, w)  # the home's routing is known: pull now
+                    continue
+                if self._device_p2p and ins.task in self._routed_in:
+                    self._deferred[ins.task] = w  # pulled once its router logits are here (_pull_at)
+                    continue
+                if self._device_p2p:
                     # pulled HERE, at the producer's position, as an RCCL receive completes once both
                     # ends posted: a pull deferred to the consumer could wait for a peer that is itself
-                    # waiting for this rank to release the source (routed EP rows wait for routing)
+                    # waiting for this rank to release the source (its ack comes with the pull)
                     w.wait()
                 recv_work[ins.task] = (w, t0)
                 stats.recvs += 1
@@ -1435,14 +1536,43 @@ class DAGExecutor:
         self._pn_done = None
         self._deferred = {}
 
+    def _pull_expert_rows(self, x: str, w) -> None:
+        """An expert's compact output rows, pulled at their post: the home's routing of the layer
+        is known there, so only the expert's count of rows crosses — and the producer's ack comes
+        as early as an RCCL receive's completion (a pull left to the combine could keep a peer
+        waiting for its region while this rank waits for one of that peer's)."""
+        t = self.tasks[x]
+        off = self._moe_route(t.op.inputs[1], t.op.attrs["n_experts"], t.op.attrs["top_k"])[4]
+        v = self._views[x]
+        M, H = math.prod(v.shape[:-1]), v.shape[-1]
+        w.pull_rows(self._act_region(x), H * v.element_size(), None, off, self._exp_ids[x], M)
+
+    def _pull_hidden_rows(self, h: str) -> None:
+        """A received hidden state's routed rows, pulled right after its router logits are on
+        this rank (``_pull_at``): into the cross-request batch's block when its experts run as
+        one (co-run span), else into the request's own buffer."""
+        if h not in self._deferred:
+            return
+        r, E, K = self._h_route[h]
+        blk = self._xblock.get(h)
+        out = None
+        if blk is not None:
+            q, R, H = blk
+            out = self._scratch("moe_xpb", self._xpb_shape)[q * R:(q + 1) * R]
+        self._moe_permuted(h, r, E, K, out=out)
+
     def _plan_routed_edges(self) -> None:
         """Expert-parallel edges that move ROUTED ROWS only (device transport): a hidden state
         received here whose every local consumer is an expert node reading it as its tokens, and
-        an expert's output received here whose consumer is the layer's combine. Their receives
-        are left to the MoE code, which pulls — after routing on the device — only the rows the
-        local experts were routed (gathered into the expert-sorted order) and only an expert's
-        count of compact output rows: bytes = routed rows, no capacity, no host sync."""
+        an expert's output received here whose consumer is the layer's combine. Only the rows the
+        local experts were routed move (gathered into the expert-sorted order), and only an
+        expert's count of compact output rows: bytes = routed rows, no capacity, no host sync.
+        Each is pulled as soon as the device-side routing it needs is on this rank — an expert
+        output at its post (the home's own routing), a hidden state right after its router
+        logits arrived (``_pull_at``) — so its producer's ack never waits for a later consumer
+        (the device analogue of RCCL's completion once both ends posted)."""
         received = {i.task for i in self.prog.instrs if i.op == "recv"}
+        self._h_route: Dict[str, Tuple[str, int, int]] = {}
         users: Dict[str, List[Task]] = {}
         for ins in self.prog.instrs:
             if ins.op == "run":
@@ -1455,15 +1585,32 @@ class DAGExecutor:
                           and u.id not in self._moe_batched_ids for u in us):
                 ex = sorted({u.op.attrs["expert"] for u in us})
                 self._routed_in[x] = torch.tensor(ex, dtype=torch.int32, device=self.device)
+                u = us[0]
+                self._h_route[x] = (u.op.inputs[1], u.op.attrs["n_experts"], u.op.attrs["top_k"])
             elif us and all(u.op is not None and u.op.kind == "moe_combine" for u in us) \
                     and self.tasks[x].op is not None and self.tasks[x].op.kind == "moe_expert":
                 self._routed_out.add(x)
                 self._exp_ids[x] = torch.tensor([self.tasks[x].op.attrs["expert"]], dtype=torch.int32,
                                                 device=self.device)
+        at: Dict[str, int] = {}  # where each tensor is on this rank: its run, or its receive
+        for i, ins in enumerate(self.prog.instrs):
+            if ins.op == "run":
+                for tid in ins.group:
+                    at.setdefault(tid, i)
+            elif ins.op == "recv":
+                at.setdefault(ins.task, i)
+        for h, (r, _, _) in self._h_route.items():
+            self._pull_at.setdefault(max(at[h], at[r]), []).append(h)
 
     def _pre_run(self, ins, recv_work, events) -> None:
         """What a run must wait for: copy-stream fills and peer receives of its parameter
-        groups, receives of its inputs, in-flight sends of the region it overwrites."""
+        groups, receives of its inputs, in-flight sends of the region it overwrites — for a
+        co-run span's first run, what every member waits for (they all run there)."""
+        span = self._xfirst.get(ins.task) if ins.op == "run" else None
+        for x in ([self.prog.instrs[k] for k in span] if span else [ins]):
+            self._pre_run_one(x, recv_work, events)
+
+    def _pre_run_one(self, ins, recv_work, events) -> None:
         for tid in ins.group:
             for pid in self.tasks[tid].params_needed:
                 self._await_fill(pid)
@@ -1495,7 +1642,9 @@ class DAGExecutor:
         run = self._run_group
         if i in self._moe_batch:  # the layer's experts in one grouped launch pair
             run = lambda _ins, _i=i: self._run_moe_batch(_i, stats)  # noqa: E731
-        elif i in self._moe_skip or i in self._mlp_skip:  # ran with its layer's batch / MLP block
+        elif i in self._xbatch:  # the layer's experts here over every request: one launch pair
+            run = lambda _ins, _i=i: self._run_moe_xbatch(_i, stats)  # noqa: E731
+        elif i in self._moe_skip or i in self._mlp_skip or i in self._xskip:  # ran with a batch / MLP block
             run = None
         elif i in self._mlp_fused:  # fc1 + fc2 of the MLP block in one launch
             run = lambda _ins, _i=i: self._run_mlp_fused(_i)  # noqa: E731
@@ -1763,6 +1912,12 @@ class DAGExecutor:
             try:
                 for k in range(i, seg_end):
                     self._issue_run(k, self.prog.instrs[k], stats, None)
+            except BaseException:
+                # an error inside a capture can end in an abort when the graph is torn down,
+                # which hides it: report the cause first
+                import traceback
+                traceback.print_exc()
+                raise
             finally:
                 g.capture_end()
             self.launches = (self.launches or 0) + ops.ext().graph_kernel_nodes(g.raw_cuda_graph())

@@ -77,6 +77,10 @@ class Program:
     # empty / a warm arena) or "planned" (plan_keep_sets: kept groups + streamed groups)
     residency: str = "cold"
     prefetch: bool = False  # planned with lookahead: loads are issued ahead for a copy stream
+    # co-run spans (plan_coruns): output tasks of runs the executor may issue TOGETHER at the
+    # span's first run — the expert nodes of one MoE layer placed on this rank, over every
+    # request — with the activation plan keeping their inputs and outputs live across the span
+    coruns: List[Tuple[str, ...]] = field(default_factory=list)
 
     @property
     def has_comm(self) -> bool:
@@ -350,6 +354,7 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
         prog.param_peak_bytes = par.peak
         prog.param_arena_bytes = extent
         sinks = {t for t in order if not consumers.get(t)}
+        prog.coruns = plan_coruns(prog, tmap)
         _plan_activations(core, prog, tmap, sinks)
         _plan_send_waits(prog)
         if prog.failed_loads:
@@ -368,16 +373,83 @@ def _group_kind(tmap: Dict[str, Task], grp: Tuple[str, ...]) -> str:
     return kind
 
 
+def _moe_layer_key(tmap: Dict[str, Task], ins: Instr) -> Optional[str]:
+    """The MoE layer an expert run belongs to (its router's id without the request prefix)."""
+    if ins.op != "run" or len(ins.group) != 1:
+        return None
+    op = tmap[ins.group[0]].op
+    if op is None or op.kind != "moe_expert":
+        return None
+    r = op.inputs[1]
+    head, _, rest = r.partition("/")
+    return rest if rest and head[:1] == "r" and head[1:].isdigit() else r
+
+
+def plan_coruns(prog: Program, tmap: Dict[str, Task]) -> List[Tuple[str, ...]]:
+    """Spans of expert runs that can be issued as ONE grouped launch pair at the span's first
+    run: consecutive runs of one MoE layer's expert nodes (any expert, any request — with
+    data-parallel attention every request's tokens reach the same expert GPU in the same
+    layer), with only sends, parameter loads and receives no member reads between them, and
+    every member's inputs present before the first member. Then each expert's weights stream
+    once per layer for all requests instead of once per request. Not planned for programs
+    that evict or fetch parameters from peers (regions must not move inside a span)."""
+    ins = prog.instrs
+    if any(x.op == "evict" or x.op == "psend" or (x.op == "load" and x.peer >= 0) for x in ins):
+        return []
+    defined: Dict[str, int] = {}
+    spans: List[Tuple[str, ...]] = []
+    i = 0
+    while i < len(ins):
+        key = _moe_layer_key(tmap, ins[i])
+        if key is None:
+            if ins[i].op in ("run", "recv"):
+                defined.setdefault(ins[i].task, i)
+            i += 1
+            continue
+        a, members, j = i, [i], i + 1
+        defined.setdefault(ins[i].task, i)
+        while j < len(ins):
+            x = ins[j]
+            if x.op in ("send", "load"):
+                j += 1
+                continue
+            if x.op == "recv":
+                defined.setdefault(x.task, j)
+                j += 1
+                continue
+            if _moe_layer_key(tmap, x) != key or any(defined.get(d, a) >= a for d in tmap[x.group[0]].dependencies):
+                break
+            members.append(j)
+            defined.setdefault(x.task, j)
+            j += 1
+        if len(members) > 1:
+            spans.append(tuple(ins[m].task for m in members))
+        i = members[-1] + 1
+    return spans
+
+
 def _plan_activations(core, prog: Program, tmap: Dict[str, Task], sinks=frozenset()) -> None:
     """Static activation lifetimes -> offsets in the rank's activation slab. DAG outputs
-    (``sinks``: tasks nobody consumes, e.g. the logits of every request) stay live."""
+    (``sinks``: tasks nobody consumes, e.g. the logits of every request) stay live. A co-run
+    span (``prog.coruns``) allocates every member's output at its first member and keeps every
+    member's inputs live to its last member."""
     # last use index of each activation on this rank
     last_use: Dict[str, int] = {}
+    run_at = {ins.task: i for i, ins in enumerate(prog.instrs) if ins.op == "run"}
+    alloc_at: Dict[int, List[str]] = {}
+    early: set = set()
+    span_end: Dict[str, int] = {}
+    for span in prog.coruns:
+        idx = [run_at[t] for t in span]
+        alloc_at[idx[0]] = list(span)
+        early |= set(span[1:])
+        for t in span:
+            span_end[t] = idx[-1]
     for i, ins in enumerate(prog.instrs):
         if ins.op == "run":
             for tid in ins.group:
                 for d in tmap[tid].dependencies:
-                    last_use[d] = i
+                    last_use[d] = max(last_use.get(d, i), span_end.get(ins.task, i))
             last_use.setdefault(ins.task, i)
         elif ins.op in ("send", "recv"):
             last_use[ins.task] = max(last_use.get(ins.task, i), i)
@@ -389,14 +461,14 @@ def _plan_activations(core, prog: Program, tmap: Dict[str, Task], sinks=frozense
     live: Dict[str, int] = {}
     extent = 0
     for i, ins in enumerate(prog.instrs):
-        if ins.op in ("run", "recv"):
-            tid = ins.task
-            nbytes = max(int(tmap[tid].out_bytes), 1)
-            off = act.alloc(nbytes)
-            prog.act_offset[tid] = off
-            prog.act_bytes[tid] = nbytes
-            live[tid] = off
-            extent = max(extent, off + nbytes)
+        if ins.op in ("run", "recv") and ins.task not in early:
+            for tid in alloc_at.get(i, [ins.task]):
+                nbytes = max(int(tmap[tid].out_bytes), 1)
+                off = act.alloc(nbytes)
+                prog.act_offset[tid] = off
+                prog.act_bytes[tid] = nbytes
+                live[tid] = off
+                extent = max(extent, off + nbytes)
         for tid in frees.get(i, []):
             if tid in live:
                 act.release(live.pop(tid))
@@ -411,17 +483,29 @@ def _plan_send_waits(prog: Program) -> None:
     executor completes them before the write, and the validator checks the list and the
     deadlock freedom of the waits (parallel/validate.py)."""
     inflight: List[Tuple[int, int, int]] = []  # (send index, lo, hi)
+    run_at = {ins.task: i for i, ins in enumerate(prog.instrs) if ins.op == "run"}
+    together: Dict[int, List[int]] = {}  # a co-run span's members write at its first run
+    later: set = set()
+    for span in prog.coruns:
+        idx = [run_at[t] for t in span]
+        together[idx[0]] = idx
+        later |= set(idx[1:])
     for i, ins in enumerate(prog.instrs):
         if ins.op == "send":
             lo = prog.act_offset[ins.task]
             inflight.append((i, lo, lo + prog.act_bytes[ins.task]))
-        elif ins.op in ("run", "recv") and inflight and ins.task in prog.act_offset:
-            lo = prog.act_offset[ins.task]
-            hi = lo + prog.act_bytes[ins.task]
-            hit = [s for s in inflight if s[1] < hi and lo < s[2]]
-            if hit:
-                ins.wait_sends = tuple(s[0] for s in hit)
-                inflight = [s for s in inflight if s not in hit]
+            continue
+        if i in later:
+            continue
+        for k in together.get(i, [i]):
+            w = prog.instrs[k]
+            if w.op in ("run", "recv") and inflight and w.task in prog.act_offset:
+                lo = prog.act_offset[w.task]
+                hi = lo + prog.act_bytes[w.task]
+                hit = [s for s in inflight if s[1] < hi and lo < s[2]]
+                if hit:
+                    w.wait_sends = tuple(s[0] for s in hit)
+                    inflight = [s for s in inflight if s not in hit]
 
 
 def plan_keep_sets(tasks: Sequence[Task], placement: Dict[str, int], order: Sequence[str], world: int,
@@ -767,6 +851,7 @@ def _insert_psends(pr: Program, sends: List[Tuple[int, str, int, int]], param_by
         new.append(Instr("psend", param=g, peer=dst, gpos=k, param_off=off))
     pr.instrs = new
     pr.param_offset = {(remap[i], pid): off for (i, pid), off in pr.param_offset.items()}
+    pr.coruns = []  # (regions move between peers: every run issues at its own position)
     for ins in new:
         ins.wait_sends = ()
     _plan_send_waits(pr)

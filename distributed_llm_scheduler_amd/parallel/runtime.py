@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import json
 import os
+from collections import defaultdict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -151,7 +152,10 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
         if placement == "pipeline" and world > 1 and os.environ.get("DLS_PIPELINE_STAGES", "balanced") != "layers":
             stage_of = pipeline_stages(tasks, world, param_bytes, caps_gb, node_speeds, n_req,
                                        task_times_key(cfg.name, seq, mb_batch))
-        schedule = _fixed_schedule(tasks, world, sched, placement, cfg, stage_of)
+        order_in = tasks
+        if placement == "expert" and world > 1 and n_req > 1:
+            order_in = _interleave_requests(tasks)  # every GPU steps through the layers together
+        schedule = _fixed_schedule(order_in, world, sched, placement, cfg, stage_of)
     else:
         raise ValueError(f"unknown placement {placement!r}")
     place = {tid: node_rank[sched.tasks[tid].assigned_node] for tid in sched.completed_tasks}
@@ -353,6 +357,23 @@ def measured_task_times(key: str) -> Dict[str, float]:
     if b.isdigit() and int(b) > 1 and (head + "b1") in _TASK_TIMES:
         return {t: v * int(b) for t, v in _TASK_TIMES[head + "b1"].items()}
     return {}
+
+
+def _interleave_requests(tasks: Sequence[Task]) -> List[Task]:
+    """Layer-major order of replicated requests (identical DAGs, ids ``r{k}/...``): the i-th
+    task of every request before the (i+1)-th of any. With data-parallel attention and expert
+    parallelism each GPU is home to one request and hosts experts of all of them; request-major
+    order would run the requests one after another across the whole job (each GPU's experts
+    serve request 0's 32 layers before its own request starts), whereas here every GPU works on
+    the same layer, and one layer's expert nodes of all requests sit next to each other in its
+    program — the co-run span (program.plan_coruns) that streams each expert's weights once."""
+    seen: Dict[str, int] = defaultdict(int)
+    keyed = []
+    for n, t in enumerate(tasks):
+        rep = t.id.split("/", 1)[0] if "/" in t.id else ""
+        keyed.append((seen[rep], n, t))
+        seen[rep] += 1
+    return [t for _, _, t in sorted(keyed, key=lambda x: (x[0], x[1]))]
 
 
 def _fixed_schedule(tasks: Sequence[Task], world: int, sched, mode: str, cfg,

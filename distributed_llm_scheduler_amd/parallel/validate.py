@@ -50,84 +50,22 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
         inflight: Dict[int, Tuple[int, int]] = {}  # send index -> buffer region, until waited
         pinflight: Dict[int, Tuple[int, int]] = {}  # psend index -> parameter region, until waited
         last_use: Dict[str, int] = {}
+        together, later, span_end = _coruns(prog)
         for i, ins in enumerate(prog.instrs):
             if ins.op == "run":
                 for tid in ins.group:
                     for d in tmap[tid].dependencies:
-                        last_use[d] = i
+                        last_use[d] = max(last_use.get(d, i), span_end.get(i, i))
             elif ins.op in ("send", "recv"):
                 last_use[ins.task] = max(last_use.get(ins.task, i), i)
-        for i, ins in enumerate(prog.instrs):
-            where = f"rank {r} instr {i} ({ins.op} {ins.task or ins.param})"
-            if ins.op == "psend":
-                if ins.param not in resident:
-                    errs.append(f"{where}: sends parameter group {ins.param} it does not hold")
-                elif resident[ins.param][0] != ins.param_off:
-                    errs.append(f"{where}: psend offset {ins.param_off} != resident offset {resident[ins.param][0]}")
-                sends[(r, ins.peer)].append(("param", ins.param))
-                pinflight[i] = (ins.param_off, ins.param_off + param_bytes.get(ins.param, 0))
+        for i, ins0 in enumerate(prog.instrs):
+            if i in later:  # issued with its co-run span's first run
                 continue
-            if ins.op == "load":
-                off = prog.param_offset.get((i, ins.param))
-                if off is None:
-                    errs.append(f"{where}: no arena offset for the load")
-                    continue
-                reg = (off, off + param_bytes.get(ins.param, 0))
-                if ins.peer >= 0:
-                    recvs[(ins.peer, r)].append(("param", ins.param))
-                for j in ins.wait_sends:
-                    pinflight.pop(j, None)
-                for j, preg in pinflight.items():
-                    if _overlap(reg, preg):
-                        errs.append(f"{where}: overwrites the region of in-flight parameter send {j} without waiting")
-                if reg[1] > prog.param_arena_bytes:
-                    errs.append(f"{where}: parameter region {reg} exceeds the arena ({prog.param_arena_bytes} B)")
-                for pid, other in resident.items():
-                    if pid != ins.param and _overlap(reg, other):
-                        errs.append(f"{where}: overlaps resident parameter group {pid}")
-                resident[ins.param] = reg
-            elif ins.op == "evict":
-                if ins.param not in resident:
-                    errs.append(f"{where}: evicting a group that is not resident")
-                resident.pop(ins.param, None)
-            elif ins.op == "recv":
-                sends_key = (ins.peer, r)
-                recvs[sends_key].append(ins.task)
-                have.add(ins.task)
-            elif ins.op == "send":
-                if ins.task not in have:
-                    errs.append(f"{where}: sends a tensor not produced/received on this rank")
-                sends[(r, ins.peer)].append(ins.task)
-                if ins.task in prog.act_offset:
-                    lo = prog.act_offset[ins.task]
-                    inflight[i] = (lo, lo + prog.act_bytes[ins.task])
-            elif ins.op == "run":
-                group = set(ins.group)
-                for tid in ins.group:
-                    t = tmap[tid]
-                    for d in t.dependencies:
-                        if d in tmap and d not in have and d not in group:
-                            errs.append(f"{where}: input {d} of {tid} is not available")
-                    for pid in t.params_needed:
-                        if pid not in resident:
-                            errs.append(f"{where}: parameter group {pid} of {tid} is not resident")
-                    have.add(tid)
-            # activation regions: define at run/recv, live until the last use
-            if ins.op in ("run", "recv") and ins.task in prog.act_offset:
-                lo = prog.act_offset[ins.task]
-                hi = lo + prog.act_bytes[ins.task]
-                for j in ins.wait_sends:
-                    inflight.pop(j, None)
-                for j, reg in inflight.items():
-                    if _overlap((lo, hi), reg):
-                        errs.append(f"{where}: writes the buffer of in-flight send {j} "
-                                    f"({prog.instrs[j].task}->gpu{prog.instrs[j].peer}) without waiting for it")
-                if hi > prog.act_arena_bytes:
-                    errs.append(f"{where}: activation region [{lo},{hi}) exceeds the arena ({prog.act_arena_bytes} B)")
-                for other, (olo, ohi, oend) in act_live.items():
-                    if oend >= i and _overlap((lo, hi), (olo, ohi)):
-                        errs.append(f"{where}: output {ins.task} overwrites live activation {other}")
-                act_live[ins.task] = (lo, hi, last_use.get(ins.task, len(prog.instrs)))
+            for k in together.get(i, [i]):
+                ins = prog.instrs[k]
+                where = f"rank {r} instr {k} ({ins.op} {ins.task or ins.param})"
+                _check_instr(k, ins, where, r, prog, tmap, param_bytes, errs, sends, recvs, have, resident,
+                             act_live, inflight, pinflight, last_use, i)
         if prog.start_resident:
             end = {pid: reg[0] for pid, reg in resident.items()}
             if end != prog.start_resident:
@@ -143,6 +81,99 @@ def validate_programs(tasks: Sequence[Task], programs: Sequence[Program],
     return errs
 
 
+def _coruns(prog: Program):
+    """Co-run spans (program.plan_coruns) as instruction indices: first run -> the span's
+    parameter loads and members (all take effect there), the later ones, each member's span end."""
+    run_at = {ins.task: i for i, ins in enumerate(prog.instrs) if ins.op == "run"}
+    together: Dict[int, List[int]] = {}
+    later: set = set()
+    span_end: Dict[int, int] = {}
+    for span in getattr(prog, "coruns", ()):
+        idx = [run_at[t] for t in span]
+        loads = [k for k in range(idx[0], idx[-1]) if prog.instrs[k].op == "load"]  # mapped up front
+        together[idx[0]] = loads + idx
+        later |= set(loads) | set(idx[1:])
+        for k in idx:
+            span_end[k] = idx[-1]
+    return together, later, span_end
+
+
+def _check_instr(i, ins, where, r, prog, tmap, param_bytes, errs, sends, recvs, have, resident, act_live, inflight,
+                 pinflight, last_use, at) -> None:
+    """One instruction of validate_programs (``at``: where it takes effect — a co-run span's
+    member writes its output at the span's first run)."""
+    if ins.op == "psend":
+        if ins.param not in resident:
+            errs.append(f"{where}: sends parameter group {ins.param} it does not hold")
+        elif resident[ins.param][0] != ins.param_off:
+            errs.append(f"{where}: psend offset {ins.param_off} != resident offset {resident[ins.param][0]}")
+        sends[(r, ins.peer)].append(("param", ins.param))
+        pinflight[i] = (ins.param_off, ins.param_off + param_bytes.get(ins.param, 0))
+        return
+    if ins.op == "load":
+        off = prog.param_offset.get((i, ins.param))
+        if off is None:
+            errs.append(f"{where}: no arena offset for the load")
+            return
+        reg = (off, off + param_bytes.get(ins.param, 0))
+        if ins.peer >= 0:
+            recvs[(ins.peer, r)].append(("param", ins.param))
+        for j in ins.wait_sends:
+            pinflight.pop(j, None)
+        for j, preg in pinflight.items():
+            if _overlap(reg, preg):
+                errs.append(f"{where}: overwrites the region of in-flight parameter send {j} without waiting")
+        if reg[1] > prog.param_arena_bytes:
+            errs.append(f"{where}: parameter region {reg} exceeds the arena ({prog.param_arena_bytes} B)")
+        for pid, other in resident.items():
+            if pid != ins.param and _overlap(reg, other):
+                errs.append(f"{where}: overlaps resident parameter group {pid}")
+        resident[ins.param] = reg
+        return
+    elif ins.op == "evict":
+        if ins.param not in resident:
+            errs.append(f"{where}: evicting a group that is not resident")
+        resident.pop(ins.param, None)
+    elif ins.op == "recv":
+        sends_key = (ins.peer, r)
+        recvs[sends_key].append(ins.task)
+        have.add(ins.task)
+    elif ins.op == "send":
+        if ins.task not in have:
+            errs.append(f"{where}: sends a tensor not produced/received on this rank")
+        sends[(r, ins.peer)].append(ins.task)
+        if ins.task in prog.act_offset:
+            lo = prog.act_offset[ins.task]
+            inflight[i] = (lo, lo + prog.act_bytes[ins.task])
+    elif ins.op == "run":
+        group = set(ins.group)
+        for tid in ins.group:
+            t = tmap[tid]
+            for d in t.dependencies:
+                if d in tmap and d not in have and d not in group:
+                    errs.append(f"{where}: input {d} of {tid} is not available")
+            for pid in t.params_needed:
+                if pid not in resident:
+                    errs.append(f"{where}: parameter group {pid} of {tid} is not resident")
+            have.add(tid)
+    # activation regions: define at run/recv, live until the last use
+    if ins.op in ("run", "recv") and ins.task in prog.act_offset:
+        lo = prog.act_offset[ins.task]
+        hi = lo + prog.act_bytes[ins.task]
+        for j in ins.wait_sends:
+            inflight.pop(j, None)
+        for j, reg in inflight.items():
+            if _overlap((lo, hi), reg):
+                errs.append(f"{where}: writes the buffer of in-flight send {j} "
+                            f"({prog.instrs[j].task}->gpu{prog.instrs[j].peer}) without waiting for it")
+        if hi > prog.act_arena_bytes:
+            errs.append(f"{where}: activation region [{lo},{hi}) exceeds the arena ({prog.act_arena_bytes} B)")
+        for other, (olo, ohi, oend) in act_live.items():
+            if oend >= at and _overlap((lo, hi), (olo, ohi)):
+                errs.append(f"{where}: output {ins.task} overwrites live activation {other}")
+        act_live[ins.task] = (lo, hi, last_use.get(ins.task, len(prog.instrs)))
+
+
 def _deadlock_check(programs: Sequence[Program]) -> List[str]:
     """Run all programs: a send is posted into a per-pair FIFO without blocking, a recv
     blocks until the matching message is at the head of its FIFO, and an instruction with
@@ -155,9 +186,11 @@ def _deadlock_check(programs: Sequence[Program]) -> List[str]:
         progress = False
         for prog in programs:
             r = prog.rank
+            together = _coruns(prog)[0]
             while pc[r] < len(prog.instrs):
                 ins = prog.instrs[pc[r]]
-                if any((r, j) not in taken for j in ins.wait_sends):
+                waits = [j for k in together.get(pc[r], [pc[r]]) for j in prog.instrs[k].wait_sends]
+                if any((r, j) not in taken for j in waits):
                     break
                 is_precv = ins.op == "load" and ins.peer >= 0
                 if ins.op in ("send", "psend"):
@@ -179,6 +212,100 @@ def _deadlock_check(programs: Sequence[Program]) -> List[str]:
     return []
 
 
-def check_plan(p) -> List[str]:
-    """validate_programs on a runtime.Plan."""
-    return validate_programs(p.tasks, p.programs, p.param_bytes)
+def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], eager: bool = True) -> List[str]:
+    """Deadlock freedom under the DEVICE transport's progress rules (parallel/devp2p.py), which
+    differ from RCCL's: a send completes when the consumer has PULLED it (its ack), not when the
+    receive was posted, and an expert-parallel receive is pulled only once the device-side routing
+    it needs is on the consumer — an expert's output at its post, a hidden state right after its
+    router logits (DAGExecutor._plan_routed_edges). Each rank's stream runs its program in
+    order: notifies never block, a pull waits for the producer's notify, and a write listed with
+    ``wait_sends`` (a co-run span's first run: every member's) waits for those sends' acks.
+    ``eager=False`` models pulling every routed receive at its first consumer instead (what the
+    transport did before; a layer-major expert-parallel plan deadlocks under it)."""
+    tmap = {t.id: t for t in tasks}
+    acts: List[List[Tuple[str, tuple, int]]] = []
+    for prog in programs:
+        r = prog.rank
+        users: Dict[str, List[Task]] = defaultdict(list)
+        at: Dict[str, int] = {}
+        for i, ins in enumerate(prog.instrs):
+            if ins.op == "run":
+                for tid in ins.group:
+                    at.setdefault(tid, i)
+                    for d in tmap[tid].dependencies:
+                        users[d].append(tmap[tid])
+            elif ins.op == "recv":
+                at.setdefault(ins.task, i)
+        pull_at: Dict[int, List[str]] = defaultdict(list)
+        out_rows = set()
+        for ins in prog.instrs:
+            if ins.op != "recv":
+                continue
+            us = users.get(ins.task, [])
+            if us and all(u.op is not None and u.op.kind == "moe_expert" and u.op.inputs[0] == ins.task for u in us):
+                pull_at[max(at[ins.task], at.get(us[0].op.inputs[1], 0))].append(ins.task)
+            elif us and all(u.op is not None and u.op.kind == "moe_combine" for u in us):
+                out_rows.add(ins.task)
+        if not eager:  # every routed receive pulled right before its first consumer runs
+            first = {x: min(at[u.id] for u in users[x]) for v in pull_at.values() for x in v}
+            first.update({x: min(at[u.id] for u in users[x]) for x in out_rows})
+            pull_at = defaultdict(list)
+            for x, i in first.items():
+                pull_at[i - 1].append(x)
+        together, later, _ = _coruns(prog)
+        deferred: Dict[str, tuple] = {}
+        send_key: Dict[int, tuple] = {}
+        a: List[Tuple[str, tuple, int]] = []
+        for i, ins in enumerate(prog.instrs):
+            waits = [j for k in together.get(i, [i]) for j in prog.instrs[k].wait_sends] if i not in later else []
+            if ins.op in ("run", "recv", "load"):
+                a.extend(("ack", send_key[j], i) for j in waits if j in send_key)
+            if ins.op == "send":
+                send_key[i] = (r, ins.peer, ("act", ins.task))
+                a.append(("notify", send_key[i], i))
+            elif ins.op == "psend":
+                send_key[i] = (r, ins.peer, ("param", ins.param, ins.gpos))
+                a.append(("notify", send_key[i], i))
+            elif ins.op == "load" and ins.peer >= 0:
+                a.append(("pull", (ins.peer, r, ("param", ins.param, ins.gpos)), i))
+            elif ins.op == "recv":
+                key = (ins.peer, r, ("act", ins.task))
+                if any(ins.task in v for v in pull_at.values()):
+                    deferred[ins.task] = key
+                else:
+                    a.append(("pull", key, i))
+            for h in pull_at.get(i, []):
+                if h in deferred:
+                    a.append(("pull", deferred.pop(h), i))
+        a.extend(("pull", key, -1) for key in deferred.values())
+        a.extend(("ack", key, -1) for key in send_key.values())
+        acts.append(a)
+    ready, acked = set(), set()
+    pc = [0] * len(programs)
+    progress = True
+    while progress:
+        progress = False
+        for k, prog in enumerate(programs):
+            while pc[k] < len(acts[k]):
+                kind, key, _ = acts[k][pc[k]]
+                if kind == "notify":
+                    ready.add(key)
+                elif kind == "pull":
+                    if key not in ready:
+                        break
+                    acked.add(key)
+                elif key not in acked:
+                    break
+                pc[k] += 1
+                progress = True
+    stuck = [(prog.rank, acts[k][pc[k]][0], acts[k][pc[k]][1], acts[k][pc[k]][2])
+             for k, prog in enumerate(programs) if pc[k] < len(acts[k])]
+    return [f"device transport deadlock: ranks blocked at {stuck[:4]}"] if stuck else []
+
+
+def check_plan(p, device: bool = True) -> List[str]:
+    """validate_programs on a runtime.Plan (plus the device transport's progress rules)."""
+    errs = validate_programs(p.tasks, p.programs, p.param_bytes)
+    if not errs and device:
+        errs = device_deadlock_check(p.tasks, p.programs)
+    return errs

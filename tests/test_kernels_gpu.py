@@ -742,3 +742,46 @@ def test_mlp_fused_one_launch():
     of = out.cpu().float()
     _close(so.cpu(), torch.stack([of.sum(1), (of * of).sum(1)], 1), 1e-2)
     assert int(sync[-1]) == 0 and int(sync[:-1].abs().sum()) == 0  # no timeout; counters reset
+
+
+def test_moe_xbatch_index_and_cross_request_experts():
+    """Cross-request expert batch (executor._run_moe_xbatch): the index launch maps groups
+    (request, expert) onto their requests' expert-sorted blocks exactly as the host reference
+    does, and ONE grouped gate/up + down pair over those groups — the same expert weights in
+    several groups — equals each request's expert computed alone in fp32."""
+    Q, M, E, k, H, F = 3, 200, 8, 2, 256, 384
+    g = torch.Generator().manual_seed(17)
+    routes, xs = [], []
+    for q in range(Q):
+        logits = torch.randn(M, E, generator=g).to(torch.bfloat16).to(DEV)
+        routes.append(ops.moe_route(logits, k, E))
+        xs.append(_rand(M, H, seed=60 + q))
+    R = M * k
+    pairs = [(0, 1), (1, 1), (2, 1), (0, 5), (2, 5), (1, 6)]  # (request, expert); expert 1 in three groups
+    reqs, experts = [q for q, _ in pairs], [e for _, e in pairs]
+    offsets = torch.zeros(len(pairs) + 1, dtype=torch.int32, device=DEV)
+    a_rows = torch.full((Q * R,), -1, dtype=torch.int32, device=DEV)
+    ops.moe_xbatch_index([r[4] for r in routes], reqs, experts, [q * R for q in range(Q)], offsets, a_rows)
+    o_ref, a_ref = torch.zeros(len(pairs) + 1, dtype=torch.int32), torch.zeros(Q * R, dtype=torch.int32)
+    ops.moe_xbatch_index([r[4].cpu() for r in routes], reqs, experts, [q * R for q in range(Q)], o_ref, a_ref)
+    torch.cuda.synchronize()
+    assert offsets.cpu().tolist() == o_ref.tolist()
+    n = int(o_ref[-1])
+    assert a_rows[:n].cpu().tolist() == a_ref[:n].tolist()
+    # the batch: each request's rows in its block of one token matrix
+    xp = torch.cat([ops.moe_permute(xs[q], routes[q][2]) for q in range(Q)])
+    w13 = {e: ops.interleave_gate_up(_rand(2 * F, H, scale=0.05, seed=80 + e)) for e in set(experts)}
+    w2 = {e: _rand(H, F, scale=0.05, seed=90 + e) for e in set(experts)}
+    h = torch.full((Q * R, F), 3.0, dtype=torch.bfloat16, device=DEV)
+    outs = [torch.full((M, H), 7.0, dtype=torch.bfloat16, device=DEV) for _ in pairs]
+    ops.gemm_grouped(xp, [w13[e] for e in experts], offsets, act="swiglu", out=h, rows_hint=R // E, a_rows=a_rows)
+    ops.gemm_grouped(h, [w2[e] for e in experts], offsets, outs=outs, rows_hint=R // E)
+    torch.cuda.synchronize()
+    for gi, (q, e) in enumerate(pairs):
+        off = routes[q][4].cpu().tolist()
+        rows = routes[q][2].cpu()[off[e]:off[e + 1]].long()
+        cnt = rows.numel()
+        ref = ops.ref_linear(ops.ref_linear(xs[q].cpu()[rows], w13[e].cpu(), act="swiglu").to(torch.bfloat16),
+                             w2[e].cpu())
+        _close(outs[gi][:cnt].cpu(), ref.float(), 3e-2)
+        assert (outs[gi][cnt:].cpu().float() == 7.0).all(), "rows past the group's count were written"

@@ -167,3 +167,18 @@ def test_planned_keep_set_refills_less_on_llama(regime):
     assert bound <= fa < bound + 0.5
     assert auto.programs[0].param_peak_bytes / 1e9 + max(t.memory_required for t in tasks) <= cap + 1e-6
     assert check_plan(auto) == []
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_device_transport_progress_rules_on_expert_parallel_plans(world):
+    """The device transport completes a send when the consumer PULLS it, not when it posts the
+    receive, so a plan valid under RCCL's rules can deadlock there: the layer-major
+    data-parallel-attention + expert plan did while expert outputs were pulled at the combine
+    (both ranks waiting for the ack of a region the other pulls later). Pulling each routed
+    receive as soon as its routing is on the rank (the executor's rule) is deadlock-free."""
+    from distributed_llm_scheduler_amd.parallel.validate import device_deadlock_check
+    p = runtime.plan("tiny-mixtral", world=world, placement="expert", replicas=world, seq=16)
+    assert check_plan(p) == []
+    assert device_deadlock_check(p.tasks, p.programs) == []
+    if world == 2:
+        assert device_deadlock_check(p.tasks, p.programs, eager=False), "the old pull rule should deadlock"
