@@ -969,7 +969,13 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
     // grouped MoE experts: block (g, tn) walks expert g's row range [rows[g], rows[g+1]) of
     // its column panel with expert g's weight; consecutive blocks share an expert (its rows
     // stay L2-resident while its weight panels stream)
-    const int g = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    // (w_stream bit 8: groups sharing weights — panel-major, the panel's groups on one XCD)
+    int g = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    if (ep.w_stream & 8) {
+      const int L = xcd_remap(blockIdx.x, gridDim.x), ng = gridDim.x / tiles_n;
+      tn = L / ng;
+      g = L % ng;
+    }
     const int r0 = rows[g], cnt = rows[g + 1] - r0;
     const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
     const bf16* Wg = reinterpret_cast<const bf16*>(ep.grp_w[g]);
@@ -983,7 +989,7 @@ __global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict_
 #define DLS_GROUPED_WALK(GA)                                                                                      \
   for (int t = 0; t * C::BM < Mr; ++t) {                                                                           \
     if (t) raw_barrier(); /* every wave is done reading the staging buffers of the previous tile */                \
-    if (C::BXS > 0 && ep.w_stream)                                                                                 \
+    if (C::BXS > 0 && (ep.w_stream & 1))                                                                           \
       glds_tile<C, 0, kPolStream, true, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, \
                                             act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep, ag);                \
     else                                                                                                           \
@@ -1241,7 +1247,7 @@ void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned
   // (the nt path DMAs the A rows by buffer loads with 32-bit offsets: an A of 2 GB or more
   // takes the default path)
   const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs,
-               (size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0};
+               a.grouped_shared ? 8 : ((size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0)};
   const int tiles_n = (a.N + C::BN - 1) / C::BN;
   hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(n_groups * tiles_n), dim3(C::T), 0, s, (const bf16*)a.A,
                      a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0,

@@ -32,6 +32,10 @@ struct GemmArgs {
   int config;    // -1 = auto
   int compact_rows = 0;  // > 0 with a device row range [r0, r1): write output rows 0..r1-r0-1 (not r0..),
                          // and at most compact_rows of them (the output's row capacity)
+  // grouped launches whose groups share weights (a cross-request expert batch: one group per
+  // (request, expert)): the groups of one weight panel run on consecutive workgroups of one XCD
+  // and the weights keep the default cache policy, so each panel comes from HBM once
+  int grouped_shared = 0;
   RopeArgs rope{};
   // Row statistics hand-off between a residual-producing GEMM and the next folded norm:
   // stats_out: fp32 [M][2] (zeroed by the caller) += (sum, sum of squares) of each FINAL

@@ -593,7 +593,7 @@ at::Tensor grouped_gemm(const at::Tensor& X, const at::Tensor& offsets, const at
 void gemm_grouped(const at::Tensor& x, const std::vector<at::Tensor>& weights, const at::Tensor& w_ptrs,
                   const at::Tensor& offsets, int64_t act, const c10::optional<at::Tensor>& out,
                   const std::vector<at::Tensor>& outs, const c10::optional<at::Tensor>& out_ptrs, int64_t config,
-                  const c10::optional<at::Tensor>& a_rows) {
+                  const c10::optional<at::Tensor>& a_rows, bool shared_weights) {
   const int64_t E = (int64_t)weights.size();
   check_bf16(x, "x");
   check_rows(x, "x");
@@ -629,6 +629,7 @@ void gemm_grouped(const at::Tensor& x, const std::vector<at::Tensor>& weights, c
   g.K = (int)K;
   g.act = (int)act;
   g.alpha = 1.0f;
+  g.grouped_shared = shared_weights ? 1 : 0;
   const unsigned long long* cp = nullptr;
   if (out_ptrs.has_value()) {
     TORCH_CHECK((int64_t)outs.size() == E && out_ptrs->is_cuda() && out_ptrs->scalar_type() == at::kLong &&
@@ -795,5 +796,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grouped_gemm", &grouped_gemm, py::arg("X"), py::arg("offsets"), py::arg("W"), py::arg("act") = 0);
   m.def("gemm_grouped", &gemm_grouped, py::arg("x"), py::arg("weights"), py::arg("w_ptrs"), py::arg("offsets"),
         py::arg("act") = 0, py::arg("out") = py::none(), py::arg("outs") = std::vector<at::Tensor>{},
-        py::arg("out_ptrs") = py::none(), py::arg("config") = -1, py::arg("a_rows") = py::none());
+        py::arg("out_ptrs") = py::none(), py::arg("config") = -1, py::arg("a_rows") = py::none(),
+        py::arg("shared_weights") = false);
 }

@@ -562,7 +562,6 @@ def moe_xbatch_index(offs, reqs, experts, bases, offsets, a_rows):
         offsets[g + 1] = o
     return offsets, a_rows
 
-
 def moe_combine(expert_out, slot_of, weights, slot_range=None, out=None):
     """y[m] = sum_j w[m,j] * expert_out[slot_of[m,j]]; with ``slot_range`` (device int32[2])
     only slots in [r0, r1) contribute (one expert's share, zero elsewhere)."""
@@ -624,7 +623,7 @@ def moe_expert(h, router_logits, w_gate_up, w_down, expert, n_experts, top_k, ou
 
 
 def gemm_grouped(x, weights, offsets, act=None, out=None, outs=None, w_ptrs=None, out_ptrs=None, rows_hint=None,
-                 a_rows=None):
+                 a_rows=None, shared_weights=False):
     """Every expert of an MoE layer in ONE GEMM launch (GPU: LDS-DMA kernel, grid = experts x
     column tiles). Expert e multiplies the expert-sorted rows [offsets[e], offsets[e+1]) of
     ``x`` by ``weights[e]`` ([N][K]; SwiGLU: gate/up-interleaved, N/2 outputs) and writes them
@@ -632,7 +631,9 @@ def gemm_grouped(x, weights, offsets, act=None, out=None, outs=None, w_ptrs=None
     count). ``a_rows`` (int32 [R]): ``x`` is the TOKEN matrix and sorted row r is token
     ``a_rows[r]`` (the permute happens in the kernel's loads). ``w_ptrs`` / ``out_ptrs``:
     cached int64 device tensors of the tensors' addresses (built here when omitted — pass
-    cached ones inside a hipGraph)."""
+    cached ones inside a hipGraph). ``shared_weights``: groups repeat weights (a cross-request
+    expert batch) — the launch runs each weight panel's groups together on one XCD and keeps
+    the weights cached, so a panel comes from HBM once."""
     a = ACT[act] if not isinstance(act, int) else act
     E = len(weights)
     N, K = weights[0].shape
@@ -651,7 +652,7 @@ def gemm_grouped(x, weights, offsets, act=None, out=None, outs=None, w_ptrs=None
         if cfg >= tuning.REGSTAGE:
             cfg = -1
         ext().gemm_grouped(x, list(weights), w_ptrs, offsets, a, out, list(outs) if outs is not None else [],
-                           out_ptrs, cfg, a_rows)
+                           out_ptrs, cfg, a_rows, shared_weights)
         return out if outs is None else outs
     if a_rows is not None:
         x = x[a_rows.long()]

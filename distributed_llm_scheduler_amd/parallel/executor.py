@@ -315,6 +315,7 @@ class DAGExecutor:
         self._capture_plan: Optional[Dict[int, int]] = None  # set while capture_segments runs
         self._seg_pool = None
         self._cap_stream = None  # side stream segment captures run on (_capture_segment)
+        self._empty_graphs: List[object] = []  # captures that recorded nothing (kept alive)
         self._rec: Optional[_Recorder] = None   # set while a step is recorded for the runner
         self._runner = None                     # native StepRunner replaying the recorded step
         self.issue_mode: Optional[str] = None  # "runner" / "python" for segment-replayed programs
@@ -487,14 +488,19 @@ class DAGExecutor:
         """A co-run span as one grouped launch pair: group g = (request q, expert e) with the
         device-side row range of q's routing; each request's expert-sorted rows are gathered (over
         the device transport: pulled, the local experts' routed rows only) into its block of one
-        token matrix, and one index launch maps the groups' rows into it (no host sync)."""
+        token matrix, and one index launch maps the groups' rows into it (no host sync). The
+        groups of one expert share its weights: the launches run each weight panel's groups side
+        by side on one XCD with the weights cached, so a panel streams from HBM once per layer
+        whatever the request count."""
         members, loads = self._xbatch[i]
         for ld in loads:  # fixed regions (no evictions): map the span's groups up front
             self._load(ld, self.prog.instrs[ld].param, stats)
         tasks = [self.tasks[self.prog.instrs[m].group[0]] for m in members]
+        # blocks in program order, as _plan_moe_xbatch numbered them (_xblock: eager pulls)
+        reqs = list(dict.fromkeys((t.op.inputs[0], t.op.inputs[1]) for t in tasks))
+        tasks.sort(key=lambda t: t.op.attrs["expert"])  # an expert's groups side by side
         a = tasks[0].op.attrs
         E, K, F = a["n_experts"], a["top_k"], a["ffn"]
-        reqs = list(dict.fromkeys((t.op.inputs[0], t.op.inputs[1]) for t in tasks))
         routes = [self._moe_route(r, E, K) for _, r in reqs]
         R = routes[0][2].numel()
         xp = self._scratch("moe_xpb", self._xpb_shape)
@@ -523,8 +529,10 @@ class DAGExecutor:
             mk = lambda ts: torch.tensor([x.data_ptr() for x in ts], dtype=torch.int64, device=self.device)  # noqa: E731
             cached = (ptrs, mk(w13), mk(w2), mk(outs))
             self._moe_bufs[("x", i)] = cached
-        ops.gemm_grouped(xp, w13, offsets, act="swiglu", out=hbuf, w_ptrs=cached[1], rows_hint=hint, a_rows=a_rows)
-        ops.gemm_grouped(hbuf, w2, offsets, outs=outs, w_ptrs=cached[2], out_ptrs=cached[3], rows_hint=hint)
+        ops.gemm_grouped(xp, w13, offsets, act="swiglu", out=hbuf, w_ptrs=cached[1], rows_hint=hint, a_rows=a_rows,
+                         shared_weights=True)
+        ops.gemm_grouped(hbuf, w2, offsets, outs=outs, w_ptrs=cached[2], out_ptrs=cached[3], rows_hint=hint,
+                         shared_weights=True)
 
     def _plan_mlp_fused(self) -> None:
         """Pairs (fc1 group i, fc2 group j) of a pre-norm MLP block that run as ONE launch:
@@ -1900,6 +1908,8 @@ class DAGExecutor:
         irecv / parameter send posted earlier in this step host-blocking — two ranks exchanging
         in opposite directions could then wait on each other at capture). The capture runs on
         a side stream ordered after the compute stream; the compute stream waits for it."""
+        if all(k in self._moe_skip or k in self._mlp_skip or k in self._xskip for k in range(i, seg_end)):
+            return None  # its runs issue with a batch elsewhere: no graph at all
         g = torch.cuda.CUDAGraph(keep_graph=True)
         cur = torch.cuda.current_stream(self.device)
         if self._cap_stream is None:
@@ -1923,8 +1933,11 @@ class DAGExecutor:
             self.launches = (self.launches or 0) + ops.ext().graph_kernel_nodes(g.raw_cuda_graph())
             if ops.ext().graph_nodes(g.raw_cuda_graph()) == 0:
                 # every run of the segment was folded into another launch (a norm written by its
-                # producer, say): nothing to replay — no graph launch per step for it
+                # producer, say): nothing to replay — no graph launch per step for it. The empty
+                # graph is kept, not destroyed here: tearing a graph down while another rank's
+                # thread of the single-GPU harness is capturing aborted the process
                 cur.wait_stream(cs)
+                self._empty_graphs.append(g)
                 return None
             g.instantiate()
         cur.wait_stream(cs)

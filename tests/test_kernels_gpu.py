@@ -744,11 +744,13 @@ def test_mlp_fused_one_launch():
     assert int(sync[-1]) == 0 and int(sync[:-1].abs().sum()) == 0  # no timeout; counters reset
 
 
-def test_moe_xbatch_index_and_cross_request_experts():
+@pytest.mark.parametrize("shared", [False, True])
+def test_moe_xbatch_index_and_cross_request_experts(shared):
     """Cross-request expert batch (executor._run_moe_xbatch): the index launch maps groups
     (request, expert) onto their requests' expert-sorted blocks exactly as the host reference
     does, and ONE grouped gate/up + down pair over those groups — the same expert weights in
-    several groups — equals each request's expert computed alone in fp32."""
+    several groups, run panel-major with cached weights when ``shared`` — equals each request's
+    expert computed alone in fp32."""
     Q, M, E, k, H, F = 3, 200, 8, 2, 256, 384
     g = torch.Generator().manual_seed(17)
     routes, xs = [], []
@@ -774,8 +776,9 @@ def test_moe_xbatch_index_and_cross_request_experts():
     w2 = {e: _rand(H, F, scale=0.05, seed=90 + e) for e in set(experts)}
     h = torch.full((Q * R, F), 3.0, dtype=torch.bfloat16, device=DEV)
     outs = [torch.full((M, H), 7.0, dtype=torch.bfloat16, device=DEV) for _ in pairs]
-    ops.gemm_grouped(xp, [w13[e] for e in experts], offsets, act="swiglu", out=h, rows_hint=R // E, a_rows=a_rows)
-    ops.gemm_grouped(h, [w2[e] for e in experts], offsets, outs=outs, rows_hint=R // E)
+    ops.gemm_grouped(xp, [w13[e] for e in experts], offsets, act="swiglu", out=h, rows_hint=R // E, a_rows=a_rows,
+                     shared_weights=shared)
+    ops.gemm_grouped(h, [w2[e] for e in experts], offsets, outs=outs, rows_hint=R // E, shared_weights=shared)
     torch.cuda.synchronize()
     for gi, (q, e) in enumerate(pairs):
         off = routes[q][4].cpu().tolist()
