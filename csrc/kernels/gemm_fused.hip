@@ -14,6 +14,8 @@
 // The last of a row block's 32 consumers resets its counters for the next launch. A poll that
 // exceeds its bound (a CU missing from the grid) sets an error word and proceeds (wrong numbers,
 // never a hang).
+#include <cstdlib>
+
 #include "gemm_glds_impl.h"
 
 namespace {
@@ -25,10 +27,12 @@ static_assert(F1::BM % F2::BM == 0, "an fc2 row tile lies inside one fc1 row blo
 constexpr int kSc1 = 16;  // cache policy: sc1
 constexpr int kLds = F1::LDS_UNITS > F2::LDS_UNITS ? F1::LDS_UNITS : F2::LDS_UNITS;
 
+template <bool PREFETCH>
 __global__ __launch_bounds__(F1::T) void mlp_fused_kernel(MlpFusedArgs p) {
   __shared__ bf16x8 smem[kLds];
   const int nt = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, nt);
+  DLS_STAMP(4)
   const int tm1 = p.M / F1::BM;
   const int t1m = bid % tm1, t1n = bid / tm1;
   const Epi ep1{RopeArgs{}, nullptr, p.ext_stats, nullptr};
@@ -39,10 +43,28 @@ __global__ __launch_bounds__(F1::T) void mlp_fused_kernel(MlpFusedArgs p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(p.ready + t1m, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  DLS_STAMP(5)
 
   // phase 2: fc2 tile of this block; wait for every fc1 tile of its rows
   const int tm2 = p.M / F2::BM;
   const int t2m = bid % tm2, t2n = bid / tm2;
+  if constexpr (PREFETCH) {
+    // The weights do not depend on fc1: before polling, DMA this block's 1/tm2 share of its
+    // fc2 weight panel (rows n0..n0+BN, a K slice) into the idle LDS. The tm2 blocks of one
+    // column tile are consecutive logical ids, i.e. one XCD (xcd_remap), so together they pull
+    // the panel into that XCD's L2 while fc1's last tiles finish; phase 2's DMA then hits L2.
+    const int ks = p.F / tm2, ck = ks / 8;  // K slice and its 16-B chunks per row
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = F1::T / 64;
+    const bf16* w2 = (const bf16*)p.w2 + (size_t)(t2n * F2::BN) * p.ldw2 + t2m * ks;
+    const int chunks = F2::BN * ck;
+    for (int i = 0; i * F1::T < chunks; ++i) {
+      const int c = i * F1::T + threadIdx.x;
+      auto* dst = (__attribute__((address_space(3))) void*)(smem + (i * waves + wave) * 64);
+      if (c < chunks)
+        __builtin_amdgcn_global_load_lds((const void*)(w2 + (size_t)(c / ck) * p.ldw2 + (c % ck) * 8), dst, 16, 0, 0);
+    }
+    (void)lane;
+  }
   const int rb = t2m * F2::BM / F1::BM;
   const int need = p.F / F1::BN;  // fc1 column tiles per row block
   if (threadIdx.x == 0) {
@@ -62,7 +84,9 @@ __global__ __launch_bounds__(F1::T) void mlp_fused_kernel(MlpFusedArgs p) {
       __hip_atomic_store(p.done + rb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if constexpr (PREFETCH) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS is phase 2's again
   __syncthreads();  // the block's other waves load h only after the poll has matched
+  DLS_STAMP(6)
   const Epi ep2{RopeArgs{}, p.stats_out, nullptr, nullptr};
   glds_tile<F2, 0, 0, false, false, kSc1, false>(smem, (const bf16*)p.h, p.ldh, (const bf16*)p.w2, p.ldw2,
                                                  (bf16*)p.out, p.ldo, (const bf16*)p.b2, (const bf16*)p.R, p.ldr,
@@ -74,12 +98,21 @@ __global__ __launch_bounds__(F1::T) void mlp_fused_kernel(MlpFusedArgs p) {
 
 bool mlp_fused_supported(int M, int H, int F, int Hout, int cus) {
   const long t1 = (long)(M / F1::BM) * (F / F1::BN), t2 = (long)(M / F2::BM) * (Hout / F2::BN);
+  const long ks = F / (M / F2::BM > 0 ? M / F2::BM : 1);  // the weight prefetch's K slice
+  const long pre = (long)F2::BN * (ks / 8) * 16;         // its bytes in LDS
   return M % F1::BM == 0 && F % F1::BN == 0 && Hout % F2::BN == 0 && H % (F1::BK * F1::KG) == 0 &&
          F % (F2::BK * F2::KG) == 0 && H / (F1::BK * F1::KG) >= 2 && F / (F2::BK * F2::KG) >= 2 && t1 == t2 &&
-         t1 <= cus;
+         t1 <= cus && F % ((M / F2::BM) * 8) == 0 && pre <= (long)kLds * 16;
 }
 
 void launch_mlp_fused(const MlpFusedArgs& p, hipStream_t s) {
+  static const int env_pre = [] {
+    const char* e = std::getenv("DLS_MLP_PREFETCH");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
   const int grid = (p.M / F1::BM) * (p.F / F1::BN);
-  hipLaunchKernelGGL(mlp_fused_kernel, dim3(grid), dim3(F1::T), 0, s, p);
+  if (p.prefetch_w2 < 0 ? env_pre : p.prefetch_w2)
+    hipLaunchKernelGGL(mlp_fused_kernel<true>, dim3(grid), dim3(F1::T), 0, s, p);
+  else
+    hipLaunchKernelGGL(mlp_fused_kernel<false>, dim3(grid), dim3(F1::T), 0, s, p);
 }

@@ -216,6 +216,10 @@ struct MlpFusedArgs {
   int* done;   // [M / 64]
   int* err;    // set if a poll exceeded spin_limit
   int spin_limit;
+  // before its poll, each workgroup DMAs its share of its fc2 weight panel (the panel is
+  // shared by the XCD's workgroups of that column tile) so phase 2 finds it in the XCD's L2;
+  // -1: DLS_MLP_PREFETCH (default on)
+  int prefetch_w2 = -1;
 };
 bool mlp_fused_supported(int M, int H, int F, int Hout, int cus);
 void launch_mlp_fused(const MlpFusedArgs& p, hipStream_t s);  // one wave spinning for ``us`` microseconds (loopback.cpp)
