@@ -26,7 +26,7 @@ def main():
         wbytes = tuning.GROUPS * N * K * 2
         rows = sorted(((round(t, 1), c) for (c, _), t in res.items()))
         print(json.dumps({"M": M, "N": N, "K": K, "swiglu": sw, "best": best[:2], "best_us": round(best[2], 1),
-                          "best_TBps": round(wbytes / best[2] / 1e6, 2), "all_us": rows[:12]}), flush=True)
+                          "best_TBps": round(wbytes / best[2] / 1e6, 2), "all_us": rows}), flush=True)
 
 
 if __name__ == "__main__":

@@ -343,11 +343,11 @@ constexpr Shape kShapes[] = {{256, 128}, {128, 128}, {128, 64},  {64, 64},   {64
                              {32, 48},   {64, 96},   {32, 144},  {32, 48},   {128, 128}, {192, 128},
                              {192, 128}, {192, 128}, {192, 128}, {192, 128}, {256, 256}, {256, 256},
                              {256, 224}, {256, 224}, {128, 96},  {128, 96},  {128, 64},  {192, 128},
-                             {256, 144}, {256, 192}, {160, 256}, {32, 48}};
+                             {256, 144}, {256, 192}, {160, 256}, {32, 48},   {128, 128}, {128, 128}};
 constexpr int kKStep[] = {64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64, 64,
                           64, 64, 128, 128, 128, 128, 256, 256, 64, 64, 64, 128, 128, 128, 128,
-                          64, 128, 64, 64, 64, 64, 64, 64, 64, 64, 128, 128, 64, 64, 64, 64, 256};
-constexpr int kNumCfg = 46;
+                          64, 128, 64, 64, 64, 64, 64, 64, 64, 64, 128, 128, 64, 64, 64, 64, 256, 64, 64};
+constexpr int kNumCfg = 48;
 constexpr bool swiglu_bad(int c) { return (c >= 22 && c <= 27) || c == 36 || c == 38 || c == 39 || c == 42 || c == 45; }
 static_assert(kNumCfg <= kGemmPersist, "config ids must stay below the persistent-launch flag");
 

@@ -1,0 +1,4 @@
+// Tile config 46 of the LDS-DMA GEMM (gemm_glds_impl.h).
+#include "gemm_glds_impl.h"
+
+DLS_GLDS_DEFINE(46)

@@ -62,10 +62,13 @@ __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "me
 // split-K: KG x the waves — and DMA issuers — per CU on a skinny grid, no reduce kernel; the
 // groups' accumulators are summed through LDS before the epilogue).
 // RING_ = 1: the 256x256 half-tile ring main loop (mainloop_ring) instead of whole-K-tile stages
-template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0, int KG_ = 1, int RING_ = 0>
+// OCC_: waves per SIMD the kernel must allow (__launch_bounds__' second argument): 2 for the
+// 4-wave tiles meant to run two workgroups per CU (at most 256 VGPRs + AGPRs per wave)
+template <int BM_, int BN_, int WM_, int WN_, int STAGES_, int PRIO_ = 0, int BXS_ = 0, int KG_ = 1, int RING_ = 0,
+          int OCC_ = 1>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, STAGES = STAGES_, PRIO = PRIO_, BXS = BXS_;
-  static constexpr int KG = KG_, RING = RING_;
+  static constexpr int KG = KG_, RING = RING_, OCC = OCC_;
   static constexpr int BK = 64, CH = 8;
   static constexpr int NW = WM * WN, T = 64 * NW * KG;
   static constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
@@ -941,7 +944,7 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 // POL (plain tiles only): streaming (nt) cache policy of the weight DMA (bit 0, split rings)
 // and of the output stores (bit 1) — GemmArgs::stream_pol
 template <class C, int LN, int RANGED, int POL = 0>
-__global__ __launch_bounds__(C::T) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
+__global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
                                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
                                                          int ldc, const bf16* __restrict__ bias,
                                                          const bf16* __restrict__ R, int ldr,
@@ -1230,6 +1233,12 @@ using C44 = Cfg<160, 256, 2, 4, 2, 0, 1>;
 // GPT-2's skinny N = 768 GEMMs: 32 x 48 tiles with FOUR K groups (8 waves issuing the LDS-DMA
 // of each 256-deep super-step instead of 4): more DMA issuers per CU for the intake-bound K loop
 using C45 = Cfg<32, 48, 2, 1, 3, 0, 0, 4>;
+// Two workgroups per CU (the MoE expert launches expose per-workgroup latency
+// with one 512-thread workgroup per CU): 4-wave 128 x 128 tiles in at most 80 KiB of LDS, so a
+// second workgroup's DMA and MFMAs run while the first waits at its barrier — joint rings of 2
+// stages (64 KiB), and split rings with the weight ring one deeper (2 x 16 KiB A + 3 x 16 KiB W)
+using C46 = Cfg<128, 128, 2, 2, 2, 0, 0, 1, 0, 2>;
+using C47 = Cfg<128, 128, 2, 2, 2, 0, 1, 1, 0, 2>;
 // (measured and dropped: the same tile with 2 or 4 stages, with eight K groups, and fc1 as one
 // round of 64 x 96 tiles with four K groups — profiles/r4_ab/gpt2_n768_cfg45.txt)
 // (and the MoE experts' 192 x 128 tile with two K groups, 16 waves: Mixtral 28.7 / 42.6 ms

@@ -160,7 +160,7 @@ def _graph_time(fn, reps: int = 10, rounds: int = 5) -> float:
 
 
 # csrc gemm_glds kKStep: K granularity per LDS-DMA config id (64; 128 / 256 for two / four K groups)
-_KSTEP = [64] * 16 + [128] * 4 + [256] * 2 + [64] * 3 + [128] * 4 + [64, 128, 64, 64, 64] + [64, 64] + [64, 64, 64, 128, 128, 64] + [64] + [64] + [64] + [256]
+_KSTEP = [64] * 16 + [128] * 4 + [256] * 2 + [64] * 3 + [128] * 4 + [64, 128, 64, 64, 64] + [64, 64] + [64, 64, 64, 128, 128, 64] + [64] + [64] + [64] + [256] + [64, 64]
 # configs whose 48- / 112- / 144-column wave tiles cannot pair SwiGLU gate/up fragments
 SWIGLU_BAD = frozenset(range(22, 28)) | {36, 38, 39, 42, 45}
 

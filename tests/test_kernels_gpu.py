@@ -52,7 +52,8 @@ def test_gemm_identity_asymmetric():
                                            (29, 1), (30, 1), (31, 1), (31, 2), (32, 1), (33, 1), (33, 2),
                                            (34, 1), (35, 1), (34, 2), (34, 3), (98, 1),
                                            (36, 1), (37, 1), (36, 2), (38, 1), (38, 2), (39, 1), (40, 1), (40, 3),
-                                           (41, 1), (41, 2), (12, 3), (31, 1), (42, 1), (43, 1), (43, 4), (44, 1), (44, 2), (45, 1)])
+                                           (41, 1), (41, 2), (12, 3), (31, 1), (42, 1), (43, 1), (43, 4), (44, 1), (44, 2), (45, 1),
+                                           (46, 1), (46, 2), (47, 1), (47, 3)])
 def test_gemm_shapes(M, N, K, config, splitk):
     if K % 64 == 0 and config >= 0 and config < 100 and K % ops.ext().gemm_glds_kstep(config):
         pytest.skip("K-group config needs K % 128 == 0")
@@ -305,7 +306,7 @@ def test_gemm_row_range_compact(config, splitk):
     _close(out.cpu().float(), ops.ref_linear(x[:cap].cpu(), w.cpu()).float(), 2e-2)
 
 
-@pytest.mark.parametrize("config", [-1, 3, 15, 17, 25, 1, 28, 29, 30, 31, 32, 33, 41, 37, 44])
+@pytest.mark.parametrize("config", [-1, 3, 15, 17, 25, 1, 28, 29, 30, 31, 32, 33, 41, 37, 44, 46, 47])
 def test_gemm_grouped_experts(config):
     """All experts of a layer in one launch: SwiGLU gate/up into shared rows, then the down
     GEMM into per-expert compact outputs — against per-expert fp32 references."""
@@ -393,7 +394,7 @@ def test_moe_gate_route_many_blocks():
         _close(logits.cpu().float(), ops.ref_linear(x.cpu(), wg.cpu()).float(), 2e-2)
 
 
-@pytest.mark.parametrize("config", [-1, 3, 17, 30, 31, 33, 41, 44])
+@pytest.mark.parametrize("config", [-1, 3, 17, 30, 31, 33, 41, 44, 46, 47])
 def test_gemm_grouped_gathered_rows(config):
     """Gate/up grouped GEMM reading its expert-sorted rows straight from the token matrix
     (a_rows = src rows of the routing) equals the permute-then-GEMM path."""
