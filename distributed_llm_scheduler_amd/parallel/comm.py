@@ -137,10 +137,12 @@ def make_comm(pg):
         return None
     if isinstance(pg, LoopbackGroup):
         return LoopComm(pg)
-    from .devp2p import DeviceComm, DeviceP2PGroup
+    from .devp2p import DeviceComm, DeviceP2PGroup, HostDeviceComm, HostP2PGroup
 
     if isinstance(pg, DeviceP2PGroup):
         return DeviceComm(pg)
+    if isinstance(pg, HostP2PGroup):
+        return HostDeviceComm(pg)
     return DistComm(pg)
 
 

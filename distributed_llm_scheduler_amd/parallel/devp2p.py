@@ -301,3 +301,185 @@ class DeviceComm:
         """The rank's error word (host read: synchronises): bit 0 a pull, bit 1 an ack wait
         timed out."""
         return int(self.mb.err.item())
+
+
+# ---------------------------------------------------------------------------------------------
+# The same protocol on the HOST (CPU tensors, every rank a thread of one process): one flag per
+# message slot and step number, a pull that waits for its producer's notify, a send whose
+# completion is the consumer's pull (its ack) — with a condition variable where the GPU spins.
+# The executor takes the device transport's code paths unchanged (regions pulled at their post,
+# routed expert rows pulled once their routing is on the rank, co-run expert batches), so the CPU
+# suite exercises them; a progress error (a send waiting for a pull that comes later) shows up
+# as a wait that times out, and the error word records it as on the GPU.
+
+
+class HostP2PWorld:
+    """Slots, source regions and every rank's flags and arenas of a job whose ranks are threads
+    of this process (parallel/loopback.py, ``transport="device"`` on the CPU)."""
+
+    def __init__(self, plan, local_ranks: Sequence[int], poison: bool = False, timeout_s: float = 30.0):
+        import threading
+
+        self.world = plan.world
+        self.slots = edge_slots(plan.programs)
+        self.sources = source_regions(plan.programs, plan.param_bytes)
+        self.poison, self.timeout_s = bool(poison), float(timeout_s)
+        S = len(self.slots)
+        self.cv = threading.Condition()
+        self.ready = {r: [0] * S for r in local_ranks}
+        self.ack = {r: [0] * S for r in local_ranks}
+        self.step = {r: 0 for r in local_ranks}
+        self.err = {r: 0 for r in local_ranks}
+        self.moved = {r: 0 for r in local_ranks}
+        self.arenas: Dict[int, Dict[str, torch.Tensor]] = {}
+
+    def attach(self, rank: int, act: torch.Tensor, param: torch.Tensor) -> None:
+        self.arenas[rank] = {"act": act.view(-1).view(torch.uint8), "param": param.view(-1).view(torch.uint8)}
+
+    def wait_for(self, pred, rank: int, code: int) -> bool:
+        """Block until ``pred()`` (under the condition's lock); on timeout fold ``code`` into the
+        rank's error word and give up (wrong numbers, as on the GPU, never a hang)."""
+        with self.cv:
+            if self.cv.wait_for(pred, self.timeout_s):
+                return True
+            self.err[rank] |= code
+            return False
+
+    def close(self) -> None:
+        pass
+
+
+class HostP2PGroup:
+    def __init__(self, world: HostP2PWorld, rank: int):
+        self.world, self.rank = world, rank
+
+    def size(self) -> int:
+        return self.world.world
+
+
+class _HostSend:
+    __slots__ = ("comm", "slot", "step", "done")
+
+    def __init__(self, comm, slot: int, step: int):
+        self.comm, self.slot, self.step, self.done = comm, slot, step, False
+
+    def wait(self):
+        if not self.done:
+            self.done = True
+            w, r = self.comm.w, self.comm.rank
+            w.wait_for(lambda: w.ack[r][self.slot] >= self.step, r, ERR_ACK)
+
+
+class _HostRecv:
+    __slots__ = ("comm", "slot", "buf", "src", "step", "done")
+
+    def __init__(self, comm, slot: int, buf: torch.Tensor, src: Tuple[int, str, int], step: int):
+        self.comm, self.slot, self.buf, self.src, self.step, self.done = comm, slot, buf, src, step, False
+
+    def _arrived(self):
+        w, r = self.comm.w, self.comm.rank
+        ok = w.wait_for(lambda: w.ready[r][self.slot] >= self.step, r, ERR_PULL)
+        peer, arena, off = self.src
+        return ok, w.arenas[peer][arena][off:off + self.buf.numel()]
+
+    def _acked(self, nbytes: int):
+        w, r = self.comm.w, self.comm.rank
+        with w.cv:
+            w.ack[self.src[0]][self.slot] = max(w.ack[self.src[0]][self.slot], self.step)
+            w.moved[r] += int(nbytes)
+            w.cv.notify_all()
+
+    def wait(self):
+        """Pull the whole region."""
+        if not self.done:
+            self.done = True
+            ok, src = self._arrived()
+            if ok:
+                self.buf.copy_(src)
+            self._acked(self.buf.numel())
+
+    def pull_rows(self, dst: torch.Tensor, row_bytes: int, idx: Optional[torch.Tensor], off: torch.Tensor,
+                  experts: torch.Tensor, max_rows: int) -> None:
+        """Routed rows only (the DeviceComm contract): for each listed expert, rows
+        [off[e], off[e+1]) of the expert-sorted order — gathered through ``idx`` into the same
+        rows of ``dst``, or (``idx`` None) compact rows 0.. of the source into rows 0.. of dst."""
+        if self.done:
+            return
+        self.done = True
+        ok, src = self._arrived()
+        moved = 0
+        if ok:
+            s = src[:src.numel() // row_bytes * row_bytes].view(-1, row_bytes)
+            d = dst.view(-1).view(torch.uint8)
+            d = d[:d.numel() // row_bytes * row_bytes].view(-1, row_bytes)
+            o = [int(v) for v in off.tolist()]
+            for e in experts.tolist():
+                lo, hi = o[e], o[e + 1]
+                if hi <= lo:
+                    continue
+                if idx is not None:
+                    d[lo:hi] = s[idx[lo:hi].long()]
+                else:
+                    d[:hi - lo] = s[:hi - lo]
+                moved += (hi - lo) * row_bytes
+        self._acked(moved)
+
+
+class HostDeviceComm:
+    """DeviceComm's contract on the host (see HostP2PWorld)."""
+    kind = "device"
+
+    def __init__(self, group: HostP2PGroup):
+        self.w = group.world
+        self.rank = group.rank
+        self.dry = False
+
+    def attach(self, ex) -> None:
+        self.w.attach(self.rank, ex.act_slab, ex.param_slab)
+
+    def begin_step(self) -> None:
+        if not self.dry:
+            with self.w.cv:
+                self.w.step[self.rank] += 1
+
+    def _slot(self, src: int, dst: int, key) -> int:
+        try:
+            return self.w.slots[(src, dst, key)]
+        except KeyError:
+            raise RuntimeError(f"device p2p: no message {key} from rank {src} to rank {dst} in the plan") from None
+
+    def isend(self, buf: torch.Tensor, peer: int, key=None):
+        slot = self._slot(self.rank, peer, key)
+        if self.dry:
+            return _NoWork()
+        w = self.w
+        with w.cv:
+            step = w.step[self.rank]
+            w.ready[peer][slot] = max(w.ready[peer][slot], step)
+            w.cv.notify_all()
+        return _HostSend(self, slot, step)
+
+    def irecv(self, buf: torch.Tensor, peer: int, key=None):
+        slot = self._slot(peer, self.rank, key)
+        arena, off, nbytes = self.w.sources[(peer, self.rank, key)]
+        region = buf.view(torch.uint8) if buf.is_contiguous() and buf.dim() == 1 else None
+        if region is None or region.numel() != nbytes:
+            raise RuntimeError(f"device p2p: receive region of {key} does not match the producer's "
+                               f"({None if region is None else region.numel()} vs {nbytes} bytes)")
+        if self.dry:
+            return _NoWork()
+        if self.w.poison:
+            region.fill_(0xFF)  # bf16 NaN until the pull lands
+        return _HostRecv(self, slot, region, (peer, arena, off), self.w.step[self.rank])
+
+    def batch(self, ops_: Sequence[Tuple[bool, torch.Tensor, int, object]]) -> List[object]:
+        return [self.isend(b, p, k) if s else self.irecv(b, p, k) for s, b, p, k in ops_]
+
+    def reset_errors(self) -> None:
+        self.w.err[self.rank] = 0
+
+    def bytes_pulled(self) -> int:
+        return self.w.moved[self.rank]
+
+    def errors(self) -> int:
+        return self.w.err[self.rank]

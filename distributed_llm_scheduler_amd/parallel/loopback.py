@@ -55,22 +55,26 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     the timed steps run under torch's sync debug mode "error" (any device->host synchronising
     call inside a step raises). ``autotune``: tune GEMM shapes missing from the table first (off:
     the kernel's heuristic config — the harness checks ordering and numerics, not speed).
-    ``transport="device"`` (GPU): the edges are moved by kernels (parallel/devp2p.py) — notify,
+    ``transport="device"``: the edges are moved by kernels (parallel/devp2p.py) — notify,
     pull and ack flags, no host pairing — and each rank's whole step captures into ONE hipGraph;
     ``delay_us`` then delays every notify and ``poison`` fills each receive region with NaN
     when the receive is posted. ``single_issue`` (captured whole-step graphs only): after
     warm-up, ONE host thread issues every rank's timed steps round-robin (graph launches are
     asynchronous), so ``host_us`` is the issue cost of a step without GIL contention between
-    rank threads."""
+    rank threads. On the CPU the same protocol runs with host waits (devp2p.HostP2PWorld)."""
     from . import executor as exm
     from . import runtime
 
     device = torch.device(device)
     gpu = device.type == "cuda"
     world = plan.world
-    if transport == "device":
-        if not gpu:
-            raise ValueError("the device p2p transport needs a GPU")
+    if transport == "device" and not gpu:
+        # the device transport's protocol with host waits (devp2p.HostP2PWorld): the executor's
+        # device-transport paths on the CPU, a progress error as a timed-out wait
+        from .devp2p import HostP2PGroup, HostP2PWorld
+        dw = HostP2PWorld(plan, range(world), poison=poison, timeout_s=min(timeout_s, 30.0))
+        groups = [HostP2PGroup(dw, r) for r in range(world)]
+    elif transport == "device":
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
         if 4 * world > queues:
             # a pull / ack wait spins on its rank's stream; a peer's stream (compute, refill copy
@@ -101,7 +105,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
             exs.append(runtime.make_executor(plan, r, device, store, pg=groups[r], use_graph=False))
     if gpu:
         torch.cuda.synchronize(device)
-    if transport == "device":
+    if transport == "device" and gpu:
         # one DRY step per rank, one rank at a time (no p2p, garbage numbers): first-step
         # allocations and weight transforms — some synchronise the whole device — happen before
         # any rank's kernels spin on a peer's flag in this shared process (a multi-process job
@@ -135,7 +139,8 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
                 if capture and gpu:
                     ex.capture()
                 if transport == "device":
-                    streams[r].synchronize()
+                    if gpu:
+                        streams[r].synchronize()
                     start.wait()  # every rank past its warm-up before any error word is cleared
                     warm_err[r] = ex.comm.errors()
                     ex.comm.reset_errors()

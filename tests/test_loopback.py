@@ -111,6 +111,53 @@ def test_loopback_cpu(case, world, cpu_runner):
     _check(p, run, store, ids, 0.03)
 
 
+@pytest.mark.parametrize("case", sorted(CASES))
+@pytest.mark.parametrize("world", [2, 4])
+def test_loopback_cpu_device_transport(case, world):
+    """The device transport's protocol with host waits (devp2p.HostP2PWorld): every placement
+    runs the executor's device-transport paths on the CPU — regions pulled at their post, routed
+    expert rows pulled once their routing is here, sends completed by the consumer's pull — with
+    NaN-poisoned receive regions, no wait timing out, and logits matching fp32."""
+    p, ids = _plan(case, world, 32 if case == "sequence" else 16)
+    store = runtime.make_store(p)
+    run = run_loopback(p, "cpu", steps=2, warmup=1, store=store, transport="device", timeout_s=20.0)
+    assert [ex.comm.errors() for ex in run.executors] == [0] * world
+    assert run.warmup_errors == [0] * world
+    assert sum(ex.comm.bytes_pulled() for ex in run.executors) > 0 or case == "peer_fill"
+    _check(p, run, store, ids, 0.03)
+
+
+def test_loopback_cpu_device_transport_catches_late_expert_pulls(monkeypatch):
+    """Negative control of the host device transport: with expert outputs pulled at the combine
+    again (the rule before round 5), the layer-major config-5 plan stalls — both ranks wait for
+    the ack of a region the other pulls only later — and the waits time out into the error words
+    (validate.device_deadlock_check(eager=False) predicts it)."""
+    from distributed_llm_scheduler_amd.parallel import executor as exm
+    p, ids = _plan("expert_dp", 2, 16)
+    store = runtime.make_store(p)
+    orig = exm.DAGExecutor._pull_expert_rows
+
+    def late(self, x, w):  # defer to the combine, as the old executor did
+        self._deferred[x] = w
+
+    def combine(self, t, out, _orig=exm.DAGExecutor._moe_combine):
+        a = t.op.attrs
+        off = self._moe_route(t.op.inputs[-2], a["n_experts"], a["top_k"])[4]
+        for x in t.op.inputs[:-2]:
+            w = self._deferred.pop(x, None)
+            if w is not None:
+                v = self._views[x]
+                w.pull_rows(self._act_region(x), v.shape[-1] * v.element_size(), None, off, self._exp_ids[x],
+                            v.numel() // v.shape[-1])
+        _orig(self, t, out)
+
+    monkeypatch.setattr(exm.DAGExecutor, "_pull_expert_rows", late)
+    monkeypatch.setattr(exm.DAGExecutor, "_moe_combine", combine)
+    run = run_loopback(p, "cpu", steps=1, warmup=0, store=store, transport="device", timeout_s=2.0)
+    assert any(ex.comm.errors() for ex in run.executors), "the old pull rule should stall"
+    assert orig is not late
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_expert_dp_batches_every_request_per_layer(world, monkeypatch):
     """Config 5 (data-parallel attention + expert parallelism): the requests are placed layer by
