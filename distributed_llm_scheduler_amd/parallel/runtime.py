@@ -138,8 +138,12 @@ def plan(model: str = "gpt2", world: int = 1, scheduler: str = "EFT", cap_gb: fl
     if cls.__name__ == "EFTScheduler":
         kw["link_bw_gbps"] = link_bw_gbps
         kw["refill_gb"] = {pid: b / 1e9 for pid, b in param_bytes.items()}  # what a refill really moves
-        if cost_model != "bytes":  # the steady-state model needs real seconds, not abstract constants
-            kw["real_time"] = {t.id: real_time_s(t, param_bytes) for t in tasks}
+        # the steady-state model needs real seconds, not abstract constants: the per-task kernel
+        # times measured on an MI355X (ops/task_times.json, as the pipeline balancer uses) where
+        # the table has the model, the roofline estimate elsewhere
+        measured = measured_task_times(task_times_key(cfg.name, seq, mb_batch))
+        if measured or cost_model != "bytes":
+            kw["real_time"] = {t.id: measured.get(_base_id(t.id), real_time_s(t, param_bytes)) for t in tasks}
     sched = cls([n.fresh() for n in nodes], **kw)
     for t in tasks:
         sched.add_task(t.clone())
