@@ -182,3 +182,44 @@ def test_device_transport_progress_rules_on_expert_parallel_plans(world):
     assert device_deadlock_check(p.tasks, p.programs) == []
     if world == 2:
         assert device_deadlock_check(p.tasks, p.programs, eager=False), "the old pull rule should deadlock"
+
+
+def test_layer_major_order_is_topological_and_keeps_request_order():
+    """runtime._interleave_requests: the i-th task of every request before the (i+1)-th of
+    any; each request keeps its own order, and every dependency comes first."""
+    from distributed_llm_scheduler_amd.models import registry
+    tasks, _, _ = registry.build("tiny-mixtral", batch=1, seq=16, replicas=3)
+    order = runtime._interleave_requests(tasks)
+    assert sorted(t.id for t in order) == sorted(t.id for t in tasks)
+    pos = {t.id: i for i, t in enumerate(order)}
+    assert all(pos[d] < pos[t.id] for t in order for d in t.dependencies if d in pos)
+    for r in range(3):
+        mine = [t.id for t in order if t.id.startswith(f"r{r}/")]
+        assert mine == [t.id for t in tasks if t.id.startswith(f"r{r}/")]
+    # a layer's expert nodes of all requests are adjacent
+    e0 = [i for i, t in enumerate(order) if t.id.endswith("layer_0_expert_0")]
+    assert e0 == list(range(e0[0], e0[0] + 3))
+
+
+def test_corun_span_stops_at_a_member_input_received_inside_it():
+    """program.plan_coruns: a receive of a later member's input between two members ends the
+    span before that member (it could not run at the span's first run)."""
+    from distributed_llm_scheduler_amd.parallel.program import Instr, Program, plan_coruns
+    p = runtime.plan("tiny-mixtral", world=2, placement="expert", replicas=2, seq=16)
+    pr = p.programs[0]
+    tmap = {t.id: t for t in p.tasks}
+    span = pr.coruns[0]
+    idx = [next(i for i, x in enumerate(pr.instrs) if x.op == "run" and x.task == t) for t in span]
+    # move the hidden-state receive of the second member's request right before that member
+    second = tmap[span[1]]
+    h = second.op.inputs[0]
+    recv = [i for i, x in enumerate(pr.instrs) if x.op == "recv" and x.task == h]
+    if not recv:  # the member's input is local: nothing to move in this layout
+        pytest.skip("second member's input is produced on this rank")
+    instrs = list(pr.instrs)
+    rv = instrs.pop(recv[0])
+    at = next(i for i, x in enumerate(instrs) if x.op == "run" and x.task == span[1])
+    instrs.insert(at, rv)
+    spans = plan_coruns(Program(rank=0, instrs=instrs), tmap)
+    assert all(span[1] not in s or s[0] == span[1] for s in spans)
+    assert idx[0] < idx[1]
