@@ -77,6 +77,18 @@ void p2p_pull_rows(int64_t src, at::Tensor dst, int64_t row_bytes, c10::optional
                        step.data_ptr<int64_t>(), err.data_ptr<int>(), timeout_ticks, moved_ptr(moved), cur(dst));
 }
 
+// the sends of one program point: one notify launch (p2p_device.hpp)
+void p2p_notify_many(const std::vector<int64_t>& flags, at::Tensor step) {
+  TORCH_CHECK(!flags.empty() && (int)flags.size() <= kP2PBatch, "p2p_notify_many: 1..", kP2PBatch, " flags");
+  check_i64(step, "p2p_notify_many step");
+  int64_t* f[kP2PBatch];
+  for (size_t i = 0; i < flags.size(); ++i) {
+    TORCH_CHECK(flags[i] != 0 && flags[i] % 8 == 0, "p2p_notify_many: flag address");
+    f[i] = reinterpret_cast<int64_t*>(flags[i]);
+  }
+  launch_p2p_notify_many(f, (int)flags.size(), step.data_ptr<int64_t>(), cur(step));
+}
+
 void p2p_delay(double us, at::Tensor like) { launch_delay(us, cur(like)); }
 
 void p2p_wait(at::Tensor flag, at::Tensor step, at::Tensor err, int64_t timeout_ticks, int64_t code) {
@@ -139,6 +151,7 @@ void register_p2p(py::module& m) {
   m.def("p2p_pull_rows", &p2p_pull_rows, py::arg("src"), py::arg("dst"), py::arg("row_bytes"), py::arg("idx"),
         py::arg("off"), py::arg("experts"), py::arg("max_rows"), py::arg("ready"), py::arg("ack_remote"),
         py::arg("ticket"), py::arg("step"), py::arg("err"), py::arg("timeout_ticks"), py::arg("moved") = py::none());
+  m.def("p2p_notify_many", &p2p_notify_many);
   m.def("p2p_wait", &p2p_wait);
   m.def("p2p_delay", &p2p_delay);
   m.def("p2p_pull_blocks", &p2p_pull_blocks);

@@ -54,12 +54,12 @@ __global__ __launch_bounds__(64) void p2p_notify_kernel(int64_t* remote_flag, co
 // so the kernel boundary between them — not an in-kernel fence — orders every load here after
 // the producer's data: a wait and its reads inside ONE kernel could read lines a co-running
 // kernel pulled into another XCD's L2 before the producer wrote them (ranks sharing a GPU).
-__global__ __launch_bounds__(256) void p2p_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                       int64_t n16, int64_t* ack_remote, unsigned* ticket,
-                                                       const int64_t* step, unsigned long long* moved) {
-  const int64_t s = step[0];
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// block `bi` of `nb` copying one region (shared by the single and the batched pulls)
+__device__ __forceinline__ void copy_region(const u32x4* __restrict__ src, u32x4* __restrict__ dst, int64_t n16,
+                                            int64_t* ack_remote, unsigned* ticket, int64_t s,
+                                            unsigned long long* moved, int bi, int nb) {
+  const int64_t stride = (int64_t)nb * 256;
+  int64_t i = (int64_t)bi * 256 + threadIdx.x;
   for (; i + 3 * stride < n16; i += 4 * stride) {
     const u32x4 a = src[i];
     const u32x4 b = src[i + stride];
@@ -73,10 +73,29 @@ __global__ __launch_bounds__(256) void p2p_copy_kernel(const u32x4* __restrict__
   for (; i < n16; i += stride) dst[i] = src[i];
   __syncthreads();  // every lane's loads of the source have returned (their values were stored)
   if (threadIdx.x == 0) {
-    if (moved && blockIdx.x == 0)
+    if (moved && bi == 0)
       __hip_atomic_fetch_add(moved, (unsigned long long)n16 * 16u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if ((old + 1u) % gridDim.x == 0u) store_flag(ack_remote, s);  // the last workgroup: source free
+    if ((old + 1u) % (unsigned)nb == 0u) store_flag(ack_remote, s);  // the last workgroup: source free
+  }
+}
+
+__global__ __launch_bounds__(256) void p2p_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       int64_t n16, int64_t* ack_remote, unsigned* ticket,
+                                                       const int64_t* step, unsigned long long* moved) {
+  copy_region(src, dst, n16, ack_remote, ticket, step[0], moved, blockIdx.x, gridDim.x);
+}
+
+struct FlagBatch {
+  const int64_t* flag[kP2PBatch];
+  int n;
+};
+
+__global__ __launch_bounds__(64) void p2p_notify_many_kernel(FlagBatch b, const int64_t* step) {
+  if (threadIdx.x == 0) {
+    const int64_t s = step[0];
+    __threadfence_system();
+    for (int i = 0; i < b.n; ++i) store_flag(const_cast<int64_t*>(b.flag[i]), s);
   }
 }
 
@@ -156,4 +175,11 @@ void launch_p2p_pull_rows(const void* src, void* dst, int64_t row_bytes, const i
   p2p_wait_kernel<<<1, 64, 0, s>>>(ready, step, err, timeout_ticks, 1);
   p2p_pull_rows_kernel<<<blocks, 256, 0, s>>>(static_cast<const char*>(src), static_cast<char*>(dst), row_bytes, idx,
                                               off, experts, n_exp, ack_remote, ticket, step, moved);
+}
+
+void launch_p2p_notify_many(int64_t* const* flags, int n, const int64_t* step, hipStream_t s) {
+  FlagBatch b{};
+  b.n = n;
+  for (int i = 0; i < n; ++i) b.flag[i] = flags[i];
+  p2p_notify_many_kernel<<<1, 64, 0, s>>>(b, step);
 }

@@ -33,3 +33,9 @@ void launch_p2p_pull_rows(const void* src, void* dst, int64_t row_bytes, const i
 void launch_p2p_wait(const int64_t* flag, const int64_t* step, int* err, int64_t timeout_ticks, int code,
                      hipStream_t s);
 int p2p_pull_blocks(int64_t bytes);
+
+// The sends posted at one program point notify their consumers from ONE launch (up to
+// kP2PBatch flags; a notify never waits). Pulls are not batched: a pull of one edge must not wait
+// for another edge's flag before it acks (parallel/validate.py device_deadlock_check, batched).
+constexpr int kP2PBatch = 16;
+void launch_p2p_notify_many(int64_t* const* flags, int n, const int64_t* step, hipStream_t s);

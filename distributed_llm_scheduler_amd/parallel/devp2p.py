@@ -41,6 +41,7 @@ import torch
 TIMEOUT_S = float(os.environ.get("DLS_P2P_TIMEOUT_S", "10"))
 _TICKS = int(TIMEOUT_S * 1e8)  # wall_clock64 runs at 100 MHz
 ERR_PULL, ERR_ACK = 1, 2
+BATCH = 16  # kP2PBatch (p2p_device.hpp): flags per batched notify launch
 
 
 def edge_slots(programs) -> Dict[Tuple[int, int, tuple], int]:
@@ -285,7 +286,23 @@ class DeviceComm:
         return _RecvWork(self, slot, region, (peer, arena, off))
 
     def batch(self, ops_: Sequence[Tuple[bool, torch.Tensor, int, object]]) -> List[object]:
-        return [self.isend(b, p, k) if s else self.irecv(b, p, k) for s, b, p, k in ops_]
+        """One program point's sends and receives; two or more sends notify from ONE launch (a
+        notify never waits). Receives are pulled one by one, each after its own flag: one wait for
+        all of a point's flags would make an ack wait for other producers (validate.py,
+        ``device_deadlock_check(batched=True)``)."""
+        sends = [k for k, (snd, _, _, _) in enumerate(ops_) if snd]
+        if len(sends) < 2 or self.dry:
+            return [self.isend(b, p, k) if snd else self.irecv(b, p, k) for snd, b, p, k in ops_]
+        out: List[object] = [None if snd else self.irecv(b, p, k) for snd, b, p, k in ops_]
+        slots = {k: self._slot(self.rank, ops_[k][2], ops_[k][3]) for k in sends}
+        if self.w.delay_us > 0:
+            self.e.p2p_delay(self.w.delay_us, self.mb.step)
+        flags = [self.mb.ready_addr(self.w.bases[ops_[k][2]]["mail"], slots[k]) for k in sends]
+        for i in range(0, len(flags), BATCH):
+            self.e.p2p_notify_many(flags[i:i + BATCH], self.mb.step)
+        for k in sends:
+            out[k] = _SendWork(self, slots[k])
+        return out
 
     def reset_errors(self) -> None:
         """Clear the error word (after warm-up: a first step's lazy code-object loading on one

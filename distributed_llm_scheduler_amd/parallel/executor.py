@@ -1519,20 +1519,23 @@ class DAGExecutor:
                 stats.sends += 1
                 stats.bytes_sent += nbytes
             else:
-                if self._device_p2p and ins.task in self._routed_out:
-                    self._pull_expert_rows(ins.task, w)  # the home's routing is known: pull now
-                    continue
-                if self._device_p2p and ins.task in self._routed_in:
-                    self._deferred[ins.task] = w  # pulled once its router logits are here (_pull_at)
-                    continue
-                if self._device_p2p:
-                    # pulled HERE, at the producer's position, as an RCCL receive completes once both
-                    # ends posted: a pull deferred to the consumer could wait for a peer that is itself
-                    # waiting for this rank to release the source (its ack comes with the pull)
-                    w.wait()
-                recv_work[ins.task] = (w, t0)
                 stats.recvs += 1
                 stats.bytes_recv += nbytes
+                if self._device_p2p and ins.task in self._routed_out:
+                    self._pull_expert_rows(ins.task, w)  # the home's routing is known: pull now
+                elif self._device_p2p and ins.task in self._routed_in:
+                    self._deferred[ins.task] = w  # pulled once its router logits are here (_pull_at)
+                else:
+                    if self._device_p2p:
+                        # pulled HERE, at the producer's position, as an RCCL receive completes once
+                        # both ends posted: a pull deferred to the consumer could wait for a peer that
+                        # is itself waiting for this rank to release the source (its ack comes with
+                        # the pull); each after its own flag, in order (one wait for all: validate.py)
+                        w.wait()
+                    recv_work[ins.task] = (w, t0)
+                if self._device_p2p:  # hidden states whose router logits just came: right away
+                    for h in self._pull_at.get(k, ()):
+                        self._pull_hidden_rows(h)
 
     def _run_snapshot(self, i, ins, snap) -> None:
         self._params, self._wflat, self._region, self._valid = (dict(snap[0]), dict(snap[1]), dict(snap[2]),

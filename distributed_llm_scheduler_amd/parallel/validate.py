@@ -212,7 +212,8 @@ def _deadlock_check(programs: Sequence[Program]) -> List[str]:
     return []
 
 
-def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], eager: bool = True) -> List[str]:
+def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], eager: bool = True,
+                          batched: bool = False) -> List[str]:
     """Deadlock freedom under the DEVICE transport's progress rules (parallel/devp2p.py), which
     differ from RCCL's: a send completes when the consumer has PULLED it (its ack), not when the
     receive was posted, and an expert-parallel receive is pulled only once the device-side routing
@@ -221,7 +222,10 @@ def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], ea
     order: notifies never block, a pull waits for the producer's notify, and a write listed with
     ``wait_sends`` (a co-run span's first run: every member's) waits for those sends' acks.
     ``eager=False`` models pulling every routed receive at its first consumer instead (what the
-    transport did before; a layer-major expert-parallel plan deadlocks under it)."""
+    transport did before; a layer-major expert-parallel plan deadlocks under it). ``batched``
+    models one wait for ALL of a program point's flags before any of its copies — fewer graph
+    nodes, but an ack then waits for flags of other producers, and the 4-rank config-5 plan
+    deadlocks under it: the executor pulls each receive after its own flag only."""
     tmap = {t.id: t for t in tasks}
     acts: List[List[Tuple[str, tuple, int]]] = []
     for prog in programs:
@@ -256,28 +260,63 @@ def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], ea
         deferred: Dict[str, tuple] = {}
         send_key: Dict[int, tuple] = {}
         a: List[Tuple[str, tuple, int]] = []
-        for i, ins in enumerate(prog.instrs):
-            waits = [j for k in together.get(i, [i]) for j in prog.instrs[k].wait_sends] if i not in later else []
-            if ins.op in ("run", "recv", "load"):
-                a.extend(("ack", send_key[j], i) for j in waits if j in send_key)
-            if ins.op == "send":
-                send_key[i] = (r, ins.peer, ("act", ins.task))
-                a.append(("notify", send_key[i], i))
-            elif ins.op == "psend":
+        ins_ = prog.instrs
+        i = 0
+        while i < len(ins_):
+            ins = ins_[i]
+            if ins.op in ("send", "recv"):
+                # one p2p group, as DAGExecutor._post_p2p posts it: each receive's own send waits,
+                # every notify, then each receive in order pulled after its own flag (an expert's
+                # output rows too), each followed by the hidden states its router logits unlock
+                j = i
+                while j + 1 < len(ins_) and ins_[j + 1].op in ("send", "recv") \
+                        and not any(i <= w <= j for w in ins_[j + 1].wait_sends):
+                    j += 1
+                pulls = []
+                for k in range(i, j + 1):
+                    x = ins_[k]
+                    if x.op == "recv":
+                        a.extend(("ack", send_key[w], k) for w in x.wait_sends if w in send_key)
+                for k in range(i, j + 1):
+                    x = ins_[k]
+                    if x.op == "send":
+                        send_key[k] = (r, x.peer, ("act", x.task))
+                        a.append(("notify", send_key[k], k))
+                due = []
+                for k in range(i, j + 1):
+                    x = ins_[k]
+                    if x.op != "recv":
+                        continue
+                    key = (x.peer, r, ("act", x.task))
+                    if any(x.task in v for v in pull_at.values()):
+                        deferred[x.task] = key
+                    else:
+                        pulls.append(key)
+                    now = [deferred.pop(h) for h in pull_at.get(k, []) if h in deferred]
+                    if batched:
+                        due += now
+                    else:
+                        a.extend(("pull", (key2,), k) for key2 in pulls + now)
+                        pulls = []
+                if batched:
+                    a.extend(("pull", tuple(b), j) for b in (pulls, due) if b)
+                i = j + 1
+                continue
+            waits = [w for k in together.get(i, [i]) for w in ins_[k].wait_sends] if i not in later else []
+            if ins.op in ("run", "load"):
+                a.extend(("ack", send_key[w], i) for w in waits if w in send_key)
+            if ins.op == "psend":
                 send_key[i] = (r, ins.peer, ("param", ins.param, ins.gpos))
                 a.append(("notify", send_key[i], i))
             elif ins.op == "load" and ins.peer >= 0:
-                a.append(("pull", (ins.peer, r, ("param", ins.param, ins.gpos)), i))
-            elif ins.op == "recv":
-                key = (ins.peer, r, ("act", ins.task))
-                if any(ins.task in v for v in pull_at.values()):
-                    deferred[ins.task] = key
-                else:
-                    a.append(("pull", key, i))
-            for h in pull_at.get(i, []):
-                if h in deferred:
-                    a.append(("pull", deferred.pop(h), i))
-        a.extend(("pull", key, -1) for key in deferred.values())
+                a.append(("pull", ((ins.peer, r, ("param", ins.param, ins.gpos)),), i))
+            due = [deferred.pop(h) for h in pull_at.get(i, []) if h in deferred]
+            if due and batched:
+                a.append(("pull", tuple(due), i))
+            else:
+                a.extend(("pull", (key,), i) for key in due)
+            i += 1
+        a.extend(("pull", (key,), -1) for key in deferred.values())
         a.extend(("ack", key, -1) for key in send_key.values())
         acts.append(a)
     ready, acked = set(), set()
@@ -290,10 +329,10 @@ def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], ea
                 kind, key, _ = acts[k][pc[k]]
                 if kind == "notify":
                     ready.add(key)
-                elif kind == "pull":
-                    if key not in ready:
+                elif kind == "pull":  # a batch: every flag before any copy (and its ack)
+                    if any(k2 not in ready for k2 in key):
                         break
-                    acked.add(key)
+                    acked.update(key)
                 elif key not in acked:
                     break
                 pc[k] += 1

@@ -104,3 +104,22 @@ def test_device_transport_across_processes_via_ipc():
     assert len(checks) == 2
     for err, scale in checks:
         assert err < 0.03 * scale, (err, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+def test_batched_notify_kernel():
+    """The sends of one program point notify from ONE launch (p2p_notify_many): every consumer
+    flag carries the producer's step, step after step."""
+    from distributed_llm_scheduler_amd import ops
+    from distributed_llm_scheduler_amd.parallel.devp2p import Mailbox
+
+    e = ops.ext()
+    dev = torch.device("cuda:0")
+    n = 5
+    cons, prod = Mailbox(n, dev), Mailbox(n, dev)
+    for step in (1, 2, 3):
+        e.p2p_tick(prod.step)
+        e.p2p_notify_many([cons.ready_addr(cons.base, k) for k in range(n)], prod.step)
+        torch.cuda.synchronize()
+        assert cons.ready.tolist() == [step] * n

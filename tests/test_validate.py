@@ -182,6 +182,8 @@ def test_device_transport_progress_rules_on_expert_parallel_plans(world):
     assert device_deadlock_check(p.tasks, p.programs) == []
     if world == 2:
         assert device_deadlock_check(p.tasks, p.programs, eager=False), "the old pull rule should deadlock"
+    if world == 4:  # one wait for all of a program point's flags: an ack waits for other producers
+        assert device_deadlock_check(p.tasks, p.programs, batched=True), "batched waits should deadlock"
 
 
 def test_layer_major_order_is_topological_and_keeps_request_order():
