@@ -1,7 +1,11 @@
 // Probe: can a stream wait on a memory value (hipStreamWaitValue64, executed by the command
 // processor, no CU spinning) and write one (hipStreamWriteValue64) inside a captured hipGraph?
 // If so, the device p2p transport's wait kernels (parallel/devp2p.py) could become CP waits.
-// Prints what capture / instantiation / replay returned and whether the replay waited.
+// Prints what capture / instantiation / replay returned and whether two replays waited.
+// Measured on MI355X / ROCm 7.2: both replays wait, yet the graph holds ONE node (the memory
+// operations ride on the kernel node), and a whole device-transport step built from them
+// (a set / wait-equal / reset handshake per edge) produced wrong numbers in the loopback
+// harness: mid-graph ordering of captured stream memory operations is not what the transport needs.
 //
 //   hipcc -O2 -std=c++17 --offload-arch=gfx950 benchmarks/cp_wait_probe.hip -o gpubin/cp_wait_probe
 #include <hip/hip_runtime.h>
@@ -67,7 +71,20 @@ int main() {
     std::this_thread::sleep_for(std::chrono::milliseconds(1));
   CK(hipMemcpy(&early, out, 4, hipMemcpyDeviceToHost));
   printf("after release: out %d (want 7), wflag %llu (want 5)\n", early, (unsigned long long)*wflag);
-  printf("RESULT: %s\n", (ok && early == 7 && *wflag == 5 && q != hipSuccess) ? "CP wait/write captured and replayed"
-                                                                                 : "not usable as captured");
+  (void)q;
+  // second replay with the flag reset: a wait that is part of the graph must block again
+  *flag = 0;
+  *wflag = 0;
+  CK(hipMemsetAsync(out, 0, 4, s));
+  CK(hipStreamSynchronize(s));
+  CK(hipGraphLaunch(ge, s));
+  std::this_thread::sleep_for(std::chrono::milliseconds(200));
+  const hipError_t q2 = hipStreamQuery(s);
+  printf("second replay, flag reset: stream %s, wflag %llu\n", q2 == hipSuccess ? "DONE (did not wait)" : "busy (waiting)",
+         (unsigned long long)*wflag);
+  *flag = 1;
+  CK(hipStreamSynchronize(s));
+  printf("RESULT: %s (%zu graph node(s) for kernel + wait + write)\n",
+         q2 != hipSuccess ? "replays wait for the value" : "replays do NOT wait (the operations ran at capture only)", n);
   return 0;
 }
