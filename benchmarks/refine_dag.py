@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="gpt2")
     ap.add_argument("--seq", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=1, help="batch of the one request (8: bench.py's merged strong run)")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=1, help="coordinate-descent passes over the shapes")
     ap.add_argument("--cfgs", default=None, help="only candidates with these config ids (comma list)")
@@ -28,7 +29,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    plan = runtime.plan(args.model, world=1, seq=args.seq)
+    plan = runtime.plan(args.model, world=1, seq=args.seq, batch=args.batch)
     store = runtime.make_store(plan, device_init=True)
     ex = runtime.make_executor(plan, 0, dev, store)
     for _ in range(3):

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(F1::T) void mlp_fused_kernel(MlpFusedArgs p) {
     // column tile are consecutive logical ids, i.e. one XCD (xcd_remap), so together they pull
     // the panel into that XCD's L2 while fc1's last tiles finish; phase 2's DMA then hits L2.
     const int ks = p.F / tm2, ck = ks / 8;  // K slice and its 16-B chunks per row
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, waves = F1::T / 64;
+    const int wave = threadIdx.x >> 6, waves = F1::T / 64;
     const bf16* w2 = (const bf16*)p.w2 + (size_t)(t2n * F2::BN) * p.ldw2 + t2m * ks;
     const int chunks = F2::BN * ck;
     for (int i = 0; i * F1::T < chunks; ++i) {
@@ -63,7 +63,6 @@ __global__ __launch_bounds__(F1::T) void mlp_fused_kernel(MlpFusedArgs p) {
       if (c < chunks)
         __builtin_amdgcn_global_load_lds((const void*)(w2 + (size_t)(c / ck) * p.ldw2 + (c % ck) * 8), dst, 16, 0, 0);
     }
-    (void)lane;
   }
   const int rb = t2m * F2::BM / F1::BM;
   const int need = p.F / F1::BN;  // fc1 column tiles per row block
