@@ -552,3 +552,49 @@ def test_multi_gpu_placements_keep_the_fused_groups(model, kw):
         p = runtime.plan(model, world=world, **kw)
         assert p.stats["cross_gpu_edges"] > 0
         assert sum(p.stats["kernels_per_rank"]) == one, (world, p.stats["kernels_per_rank"], one)
+
+
+def _ep_dp_worker(rank, world, port, q, seq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from distributed_llm_scheduler_amd.parallel import executor as exm
+        from distributed_llm_scheduler_amd.parallel.validate import check_plan
+
+        exm.RUNNER_CPU = True
+        p = runtime.plan("tiny-mixtral", world=world, placement="expert", replicas=world, seq=seq)
+        assert not check_plan(p)
+        store = runtime.make_store(p)
+        ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
+        for _ in range(2):
+            ex.step()
+        runner = ex.build_runner()
+        for _ in range(2):
+            ex.step()
+        q.put({"rank": rank, "runner": runner, "xbatch": len(ex._xbatch), "layers": p.cfg.n_layer,
+               "err": _ref_check(p, ex, store, f"r{rank}/")})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_expert_dp_gloo_ranks(world):
+    """BASELINE config 5 as a process-per-rank job (gloo, 2 / 4 ranks): request r's attention on
+    rank r, the experts spread, requests placed layer by layer; every rank runs its experts for
+    ALL requests of a layer as one batch (co-run spans), the steps replay from the native runner,
+    and every request's logits match the fp32 reference."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ep_dp_worker, args=(r, world, port, q, 24)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    res = sorted([q.get(timeout=5) for _ in range(world)], key=lambda r: r["rank"])
+    for r in res:
+        assert r["runner"] and r["xbatch"] == r["layers"], r
+        err, scale = r["err"]
+        assert err < 0.03 * scale, r
