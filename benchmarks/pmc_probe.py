@@ -41,9 +41,17 @@ def lmhead():
     torch.cuda.synchronize()
 
 
-def moe():
+def moe(cfg_gateup=None, cfg_down=None):
+    """``moe [gate/up config] [down config]``: the table's tiles, or the named configs (to
+    compare e.g. the two-workgroups-per-CU tiles 46 / 47 against the table's)."""
     E, T, k, H, F = 8, 512, 2, 4096, 14336
     R = T * k
+    if cfg_gateup is not None:
+        tuning.set_choice(R // E, 2 * F, H, "sg", (int(cfg_gateup), 1))
+    if cfg_down is not None:
+        tuning.set_choice(R // E, H, F, "g", (int(cfg_down), 1))
+    print("moe gate/up cfg", tuning.lookup_fused(R // E, 2 * F, H, "sg")[0], "down cfg",
+          tuning.lookup_fused(R // E, H, F, "g")[0], flush=True)
     g = torch.Generator().manual_seed(7)
     cnt = torch.bincount(torch.randint(0, E, (R,), generator=g), minlength=E)
     off = torch.cat([torch.zeros(1, dtype=torch.long), cnt.cumsum(0)]).to(torch.int32).cuda()
@@ -84,7 +92,7 @@ if __name__ == "__main__":
     if what == "lmhead":
         lmhead()
     elif what == "moe":
-        moe()
+        moe(*sys.argv[2:4])
     elif what == "attn":
         attn()
     else:

@@ -11,6 +11,9 @@ dispatches, and derives what the raw numbers mean on gfx950:
 * ``hbm_rd_MB``  = TCC_EA0_RDREQ_DRAM x 64 B  (MI355X_MICROARCH.md: EA read requests are
   tallied at 64 B while a wide read moves 128 B — double it against a byte count)
 * ``lds_conf``   = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS
+* ``waves_cu``   = 4 x SQ_WAVE_CYCLES / SQ_BUSY_CU_CYCLES: mean waves resident on a busy CU
+  (calibrated on the 8-wave, one-workgroup-per-CU expert tiles, which read 8.0; a 4-wave
+  workgroup reads ~4 at one workgroup per CU and ~8 at two)
 
     python tools/pmc_summary.py gpurun_out/pmc_lmhead_* [--match gemm]     (files or directories)
 """
@@ -53,7 +56,7 @@ def main():
                 continue
             for c, v in cs.items():
                 vals[(kern, grid)][c].append(v)
-    cols = ["n", "waves", "mfma_util", "wait_share", "l2_hit", "hbm_rd_MB", "lds_conf"]
+    cols = ["n", "waves", "mfma_util", "wait_share", "l2_hit", "hbm_rd_MB", "lds_conf", "waves_cu"]
     print(f"{'kernel':56s} {'grid':>9s} " + " ".join(f"{c:>10s}" for c in cols))
     for (kern, grid), cs in sorted(vals.items(), key=lambda kv: -max((len(v) for v in kv[1].values()), default=0)):
         m = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -70,6 +73,7 @@ def main():
                        if m.get("TCC_HIT_sum", 0) + m.get("TCC_MISS_sum", 0) else "-"),
             "hbm_rd_MB": f"{m['TCC_EA0_RDREQ_DRAM_sum'] * 64 / 1e6:.2f}" if "TCC_EA0_RDREQ_DRAM_sum" in m else "-",
             "lds_conf": ratio("SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS"),
+            "waves_cu": ratio("SQ_WAVE_CYCLES", "SQ_BUSY_CU_CYCLES", 0.25),
         }
         print(f"{kern:56s} {grid:>9s} " + " ".join(f"{row[c]:>10s}" for c in cols))
         raw = " ".join(f"{c}={v:.4g}" for c, v in sorted(m.items()))
