@@ -554,14 +554,17 @@ def test_multi_gpu_placements_keep_the_fused_groups(model, kw):
         assert sum(p.stats["kernels_per_rank"]) == one, (world, p.stats["kernels_per_rank"], one)
 
 
-def _ep_dp_worker(rank, world, port, q, seq):
+def _ep_dp_worker(rank, world, port, q, seq, max_req=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from distributed_llm_scheduler_amd import ops
         from distributed_llm_scheduler_amd.parallel import executor as exm
         from distributed_llm_scheduler_amd.parallel.validate import check_plan
 
         exm.RUNNER_CPU = True
+        if max_req is not None:  # a batch limit below the request count: spans run per node
+            ops.XBATCH_MAX_REQ = max_req
         p = runtime.plan("tiny-mixtral", world=world, placement="expert", replicas=world, seq=seq)
         assert not check_plan(p)
         store = runtime.make_store(p)
@@ -596,5 +599,27 @@ def test_expert_dp_gloo_ranks(world):
     res = sorted([q.get(timeout=5) for _ in range(world)], key=lambda r: r["rank"])
     for r in res:
         assert r["runner"] and r["xbatch"] == r["layers"], r
+        err, scale = r["err"]
+        assert err < 0.03 * scale, r
+
+
+@pytest.mark.timeout(300)
+def test_expert_dp_gloo_over_batch_limit():
+    """More requests per layer than one cross-request batch takes (the index kernel's request
+    limit, lowered to 1 here): no span is batched, the members run node by node, and the logits
+    still match the fp32 reference."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ep_dp_worker, args=(r, world, port, q, 24, 1)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=240)
+    assert all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    res = sorted([q.get(timeout=5) for _ in range(world)], key=lambda r: r["rank"])
+    for r in res:
+        assert r["runner"] and r["xbatch"] == 0, r
         err, scale = r["err"]
         assert err < 0.03 * scale, r
