@@ -42,6 +42,11 @@ WEIGHT_NT_MB = float(os.environ.get("DLS_WEIGHT_NT_MB", "0"))
 # back: GPT-2 0.620 vs 0.640 ms, Llama-3-8B 9.46 vs 9.49 ms (profiles/r4_ab/write_through.txt);
 # nt output stores cost GPT-2 5 %
 ACT_POL = int(os.environ.get("DLS_ACT_POL", "4"))
+# per-model default where the measurement disagrees (DLS_ACT_POL, when set, wins): Mixtral-8x7B's
+# step is faster with default-policy output stores, 24.40 / 24.50 vs 24.68 / 24.75 ms
+# (profiles/r5_ab/knob_recheck.txt)
+ACT_POL_MODEL = {"mixtral-8x7b": 0}
+_ACT_POL_SET = "DLS_ACT_POL" in os.environ
 # attention flags: bit 0 output stores write-through (no measurable difference), bit 1 the
 # blocks of one head grouped on one XCD (A/B knob)
 ATTN_FLAGS = int(os.environ.get("DLS_ATTN_FLAGS", "0"))
@@ -58,7 +63,7 @@ LMHEAD_POL_MAX_MB = 128
 
 def _stream_pol(N: int, K: int) -> int:
     lm = N >= LMHEAD_MIN_N and N * K * 2 <= LMHEAD_POL_MAX_MB * 1e6
-    pol = LMHEAD_POL if lm else ACT_POL
+    pol = LMHEAD_POL if lm else (ACT_POL if _ACT_POL_SET else ACT_POL_MODEL.get(tuning._model, ACT_POL))
     if WEIGHT_NT_MB > 0 and N * K * 2 >= WEIGHT_NT_MB * 1e6:
         pol |= 1
     return pol
