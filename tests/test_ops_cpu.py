@@ -83,12 +83,24 @@ def test_stream_policy_selection(monkeypatch):
     monkeypatch.setattr(ops, "LMHEAD_POL", 3)
     monkeypatch.setattr(ops, "ACT_POL", 4)
     monkeypatch.setattr(ops, "WEIGHT_NT_MB", 0.0)
+    monkeypatch.setattr(ops, "_ACT_POL_SET", False)
+    monkeypatch.setattr(ops.tuning, "_model", None)
     assert ops._stream_pol(50257, 768) == 3      # GPT-2's 77 MB LM head
     assert ops._stream_pol(128256, 4096) == 4    # Llama-3's 1 GB LM head: an ordinary GEMM
     assert ops._stream_pol(2304, 768) == 4
     monkeypatch.setattr(ops, "WEIGHT_NT_MB", 20.0)
     assert ops._stream_pol(28672, 4096) == 5  # 235 MB gate/up weight: nt DMA + write-through
     assert ops._stream_pol(2304, 768) == 4    # 3.5 MB: below the threshold
+    monkeypatch.setattr(ops, "WEIGHT_NT_MB", 0.0)
+    # per-model output-store default (Mixtral measured faster with default-policy stores) ...
+    monkeypatch.setattr(ops.tuning, "_model", "mixtral-8x7b")
+    assert ops._stream_pol(6144, 4096) == 0
+    monkeypatch.setattr(ops.tuning, "_model", "llama3-8b")
+    assert ops._stream_pol(6144, 4096) == 4
+    # ... which an explicit DLS_ACT_POL overrides
+    monkeypatch.setattr(ops, "_ACT_POL_SET", True)
+    monkeypatch.setattr(ops.tuning, "_model", "mixtral-8x7b")
+    assert ops._stream_pol(6144, 4096) == 4
 
 
 def test_gemm_config_tables_agree():
