@@ -158,6 +158,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     if captured:
         ex.step()
     ctx.sync()
+    ex.reset_transport_errors()  # device transport: a cold first step may outlast a peer's wait
     log(f"[bench{tag}] rank {ctx.rank}: warmup done ({warmup} steps, hipGraph={captured})")
 
     ctx.sync()
@@ -169,8 +170,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     mine = elapsed / steps * 1e3
     ms, per_rank = ctx.gather(mine)
     launches = ctx.gather_list(ex.launches if ex.launches is not None else -1)
-    dev_p2p = getattr(getattr(ex, "comm", None), "kind", None) == "device"
-    p2p_err = ctx.gather_list(ex.comm.errors() if dev_p2p else 0)  # a timed-out device wait: numbers invalid
+    p2p_err = ctx.gather_list(ex.transport_errors())  # a timed-out device-transport wait: numbers invalid
     st = plan.stats
     res = {
         "ms_per_step": round(ms, 5),
@@ -355,6 +355,10 @@ def main():
             "cross_gpu_bytes": head["cross_gpu_bytes"],
             "cross_gpu_bytes_routed": head["cross_gpu_bytes_routed"],
             "p2p_transport": head["p2p"] or "none",
+            # device transport: every rank's error word after the timed steps (non-zero: a wait
+            # gave up, the step's numbers are wrong and ``valid`` is false)
+            "p2p_errors": head["p2p_errors"],
+            "valid": not any(head["p2p_errors"]),
             "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
             "per_rank_ms": head["per_rank_ms"],
             "hip_graph": head["hip_graph"],

@@ -248,6 +248,16 @@ Partition steady_partition(const Instance& I, int max_stages, int min_stages) {
       }
   }
   const size_t W = static_cast<size_t>(T + 1);
+  // The stage tables hold (T+1)^2 doubles each: two per distinct node plus comp / comm. Beyond
+  // kMaxTableBytes (multi-replica or heterogeneous DAGs of thousands of tasks) the partition is
+  // not attempted and EFT keeps its cold plan — GBs of tables and O(T^2 N) time per plan would
+  // cost more than the steady-state refills they could save.
+  {
+    constexpr double kMaxTableBytes = 512.0 * (1 << 20);
+    int distinct = 0;
+    for (int n = 0; n < N; ++n) distinct += rep[n] == n;
+    if (double(2 * distinct + 2) * double(W) * double(W) * sizeof(double) > kMaxTableBytes) return out;
+  }
   std::vector<std::vector<double>> cost(N);
   std::vector<std::vector<double>> refill_tab(N);
   for (int n = 0; n < N; ++n)

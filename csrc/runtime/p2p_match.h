@@ -56,9 +56,12 @@ class P2PMatcher {
         on_match(s.op, r.op);  // may throw (size mismatch)
       } catch (const std::exception& ex) {
         // both ends fail with the real error: the counterpart was already taken off its FIFO,
-        // so its wait() must not run into the timeout and report "never matched"
-        e.error = o.error = ex.what();
-        e.matched = o.matched = true;
+        // so its wait() must not run into the timeout and report "never matched". The posting
+        // op's own entry is dropped here: its id is never returned, so nobody could wait() it
+        // (it would stay outstanding for the hub's lifetime)
+        o.error = ex.what();
+        o.matched = true;
+        ops_.erase(id);
         cv_.notify_all();
         throw;
       }

@@ -385,6 +385,8 @@ int main(int argc, char** argv) {
       peer_threw = std::string(e.what()).find("size mismatch") != std::string::npos;
     }
     CHECK(peer_threw, "the counterpart's wait reports the size mismatch");
+    CHECK(m.outstanding() == 0, "p2p: %lld ops left after a failed match (the posting op leaked)",
+          (long long)m.outstanding());
   }
   // the step runner's action loop over the loopback pairing: 2 / 4 / 8 rank threads
   for (int world : {2, 4, 8}) p2p_pipeline(world, 4, 257, 20);

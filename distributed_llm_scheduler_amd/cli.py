@@ -6,7 +6,9 @@ Commands (defaults reproduce the reference's settings where one exists, SURVEY Â
             placement statistics, optionally save the plan (``--save``) for ``run --resume``
   run       execute a plan on this machine: one process per GPU under torchrun
             (RANK/WORLD_SIZE from the environment), or one CPU/GPU process; prints the
-            measured step makespan; ``--trace`` writes a Chrome trace, ``--gantt`` a PNG
+            measured step makespan; ``--trace`` writes a Chrome trace, ``--gantt`` a PNG;
+            ``--loopback N`` runs an N-rank plan in one process (``--transport hub|device``).
+            A device-transport wait that timed out makes the run invalid: exit code 3
   simulate  the reference evaluation sweep (raw_results.csv + 2x2 figure); --execute runs each
             policy's placement of a model DAG on the devices (measured makespan column)
   extract   the reference GPT-2 DAG (test_gpt2.py semantics) to JSON (test_gpt2.py also pickles it)
@@ -70,12 +72,61 @@ def cmd_plan(a) -> int:
     return 0
 
 
+def _transport_failure(e: BaseException) -> Optional[str]:
+    """The TransportError message in ``e`` or its cause chain (a rank thread's error is re-raised
+    by the single-GPU harness as the cause of its RuntimeError), else None."""
+    from .parallel.executor import TransportError
+
+    while e is not None:
+        if isinstance(e, TransportError):
+            return str(e)
+        e = e.__cause__
+    return None
+
+
+def cmd_run_loopback(a) -> int:
+    """``run --loopback N``: the N-rank plan in THIS process on one device (the single-GPU
+    multi-rank harness, parallel/loopback.py): every rank its own executor and thread, edges over
+    the loopback hub (``--transport hub``, RCCL's p2p semantics) or moved by kernels (``--transport
+    device``, parallel/devp2p.py; on the CPU the same protocol with host waits). A device-transport
+    wait that gave up makes the run INVALID: the JSON line says so and the exit code is 3."""
+    import torch
+
+    from .parallel.loopback import run_loopback
+
+    gpu = a.device != "cpu" and torch.cuda.is_available()
+    dev = torch.device("cuda:0") if gpu else torch.device("cpu")
+    p = _plan(a, a.loopback, resume=a.resume)
+    out = {"model": a.model, "world": a.loopback, "scheduler": p.scheduler_name, "harness": "loopback",
+           "transport": a.transport, "tasks_completed": p.stats["tasks_completed"],
+           "tasks_total": p.stats["tasks_total"], "device": str(dev)}
+    try:
+        from .parallel.devp2p import TIMEOUT_S
+
+        run = run_loopback(p, dev, steps=a.steps, warmup=a.warmup, capture=gpu and not a.no_graph,
+                           transport=a.transport, delay_us=0.0, poison=False, p2p_timeout_s=TIMEOUT_S)
+        errs = [ex.transport_errors() for ex in run.executors]
+        for ex in run.executors:
+            ex.check_transport()
+    except Exception as e:  # noqa: BLE001
+        msg = _transport_failure(e)
+        if msg is None:
+            raise
+        print(json.dumps({**out, "valid": False, "error": msg}))
+        print(f"run: INVALID â€” {msg}", file=sys.stderr)
+        return 3
+    print(json.dumps({**out, "ms_per_step": round(max(run.step_ms), 4), "p2p_errors": errs, "valid": True}))
+    return 0
+
+
 def cmd_run(a) -> int:
     import torch
     import torch.distributed as dist
 
     from .parallel import runtime
 
+    if a.loopback:
+        return cmd_run_loopback(a)
     world = int(os.environ.get("WORLD_SIZE", a.devices if a.device == "cpu" else 1))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -103,22 +154,40 @@ def cmd_run(a) -> int:
         if world > 1:
             dist.barrier()
 
-    for _ in range(a.warmup):
-        ex.step()
+    failed: Optional[str] = None  # a device-transport wait gave up on this rank (TransportError)
+    try:
+        for _ in range(a.warmup):
+            ex.step()
+    except Exception as e:  # noqa: BLE001
+        failed = _transport_failure(e)
+        if failed is None:
+            raise
     sync()
-    if gpu and not a.no_graph:
+    if gpu and not a.no_graph and failed is None:
         ex.capture()
     sync()
+    ex.reset_transport_errors()  # a cold first step may outlast a peer's wait (warm-up only)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        ex.step()
+    try:
+        for _ in range(a.steps if failed is None else 0):
+            ex.step()
+    except Exception as e:  # noqa: BLE001
+        failed = _transport_failure(e)
+        if failed is None:
+            raise
     sync()
     ms = (time.perf_counter() - t0) / max(a.steps, 1) * 1e3
-    t = torch.tensor([ms], dtype=torch.float64, device=dev if (gpu and world > 1) else "cpu")
+    err = ex.transport_errors()
+    if err and failed is None:
+        failed = ex._transport_msg(err)
+    if failed:
+        print(f"run: rank {rank}: INVALID â€” {failed}", file=sys.stderr)
+    t = torch.tensor([ms, 1.0 if failed else 0.0], dtype=torch.float64, device=dev if (gpu and world > 1) else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    invalid = bool(t[1].item())
     events = None
-    if a.trace or a.gantt:
+    if (a.trace or a.gantt) and not invalid:
         st = ex.step(profile=True)
         events = [None] * world
         if world > 1:
@@ -128,7 +197,8 @@ def cmd_run(a) -> int:
     if rank == 0:
         print(json.dumps({"model": a.model, "world": world, "scheduler": p.scheduler_name,
                           "tasks_completed": p.stats["tasks_completed"], "tasks_total": p.stats["tasks_total"],
-                          "ms_per_step": round(float(t.item()), 4), "device": str(dev)}))
+                          "ms_per_step": round(float(t[0].item()), 4), "device": str(dev),
+                          "p2p": getattr(ex.comm, "kind", None), "valid": not invalid}))
         if events is not None:
             from .utils.tracing import chrome_trace, kernel_timeline
 
@@ -141,7 +211,7 @@ def cmd_run(a) -> int:
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return 3 if invalid else 0
 
 
 def cmd_simulate(a) -> int:
@@ -228,6 +298,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     r.add_argument("--roctx", action="store_true")
     r.add_argument("--trace", default=None, help="Chrome trace JSON path")
     r.add_argument("--gantt", default=None, help="measured Gantt PNG path")
+    r.add_argument("--loopback", type=int, default=0,
+                   help="run an N-rank plan in THIS process on one device (single-GPU multi-rank harness)")
+    r.add_argument("--transport", default="hub", choices=["hub", "device"],
+                   help="--loopback edges: the loopback hub (RCCL semantics) or kernels (device transport)")
     r.set_defaults(fn=cmd_run)
     s = sub.add_parser("simulate", help="reference evaluation sweep")
     s.add_argument("--runs", type=int, default=3)

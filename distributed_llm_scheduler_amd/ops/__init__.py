@@ -270,11 +270,11 @@ def linear(x, w, bias=None, act=None, residual=None, alpha=1.0, out=None, rows=N
         shp = x.shape[:-1] + (n_out,)
         M = x.numel() // x.shape[-1]
         cfg, sk = tuning.lookup(rows_hint or M, w.shape[0], w.shape[1], tuning.tag(a, rows is not None))
-        if cfg == tuning.LIB:
-            if a == 0 and residual is None and rows is None and rope is None and stats_out is None \
-                    and post_norm is None:
-                # a PLAIN GEMM (no fused epilogue) whose tuned choice is the vendor library
-                # (hipBLASLt via torch); every fused-epilogue GEMM stays on the HIP kernels
+        if cfg == tuning.LIB:  # (only with DLS_ALLOW_VENDOR_GEMM=1: tuning.lookup)
+            if tuning.VENDOR and a == 0 and residual is None and rows is None and rope is None \
+                    and stats_out is None and post_norm is None:
+                # opt-in: a PLAIN GEMM (no fused epilogue) whose tuned choice is the vendor
+                # library (hipBLASLt via torch); every fused-epilogue GEMM stays on the HIP kernels
                 x2 = x.reshape(M, x.shape[-1])
                 o2 = out.view(M, n_out) if out is not None else torch.empty(M, n_out, dtype=x.dtype, device=x.device)
                 if bias is not None:

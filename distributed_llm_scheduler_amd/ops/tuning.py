@@ -34,9 +34,11 @@ _overrides: Dict[str, Dict[str, Tuple[int, int]]] = {}
 _model: Optional[str] = None
 REGSTAGE = 100  # config ids >= 100 select the register-staged kernel (csrc ops_binding kRegStage)
 PERSIST = 64    # config | 64: the same LDS-DMA tile config as a persistent launch (kernels.h kGemmPersist)
-LIB = 200       # the vendor library (hipBLASLt through torch.mm): a candidate for PLAIN GEMMs only —
-                # a GEMM with a fused epilogue (activation, residual, folded norm, RoPE, row
-                # statistics, SwiGLU, row range) always runs on the HIP kernels
+LIB = 200       # the vendor library (hipBLASLt through torch.mm): OFF unless DLS_ALLOW_VENDOR_GEMM=1
+                # (then a candidate for PLAIN GEMMs only — a GEMM with a fused epilogue always
+                # runs on the HIP kernels). Default: every GEMM runs on the hand-written kernels,
+                # and a table entry naming LIB resolves to the best HIP candidate (lookup)
+VENDOR = os.environ.get("DLS_ALLOW_VENDOR_GEMM", "0") == "1"
 
 
 def _key(M: int, N: int, K: int, tg: str = "") -> str:
@@ -87,7 +89,17 @@ def lookup(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
         v = t.get(_key(M, N, K))
         if v is not None and v[0] >= REGSTAGE:
             v = None
+    if v is not None and v[0] == LIB and not VENDOR:
+        v = _hip_candidate(M, N, K, tg)
     return v if v is not None else (-1, 0)
+
+
+def _hip_candidate(M: int, N: int, K: int, tg: str = ""):
+    """The fastest hand-written-kernel candidate of the shape's microbenchmark, else None."""
+    for c in _cands.get(_key(M, N, K, tg), []):
+        if c[0] != LIB:
+            return tuple(c)
+    return None
 
 
 def col_split(M: int, N: int, K: int, tg: str = ""):
@@ -106,11 +118,7 @@ def lookup_fused(M: int, N: int, K: int, tg: str = "") -> Tuple[int, int]:
     cfg, sk = lookup(M, N, K, tg)
     if cfg != LIB:
         return cfg, sk
-    table()
-    for c in _cands.get(_key(M, N, K, tg), []):
-        if c[0] != LIB:
-            return tuple(c)
-    return -1, 0
+    return _hip_candidate(M, N, K, tg) or (-1, 0)
 
 
 def _save() -> None:
@@ -172,7 +180,7 @@ def kstep(cfg: int) -> int:
 
 
 def candidates(M: int, N: int, K: int, n_cfg: int, tg: str = ""):
-    out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1), (LIB, 1)]
+    out = [] if tg else [(REGSTAGE + 0, 1), (REGSTAGE + 2, 1), (REGSTAGE + 3, 1)] + ([(LIB, 1)] if VENDOR else [])
     for cfg in range(n_cfg):
         ks = kstep(cfg)
         if cfg in SWIGLU_BAD and "s" in tg:
@@ -282,7 +290,7 @@ def set_choice(M: int, N: int, K: int, tg: str, choice: Tuple[int, int]) -> None
 
 
 def runner_ups(M: int, N: int, K: int, tg: str = "", n: int = 3) -> list:
-    return list(_cands.get(_key(M, N, K, tg), []))[:n]
+    return [c for c in _cands.get(_key(M, N, K, tg), []) if VENDOR or c[0] != LIB][:n]
 
 
 def mark_refined(M: int, N: int, K: int, tg: str = "") -> None:

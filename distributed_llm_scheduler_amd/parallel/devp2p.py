@@ -38,10 +38,28 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
+from . import lifetime
+
 TIMEOUT_S = float(os.environ.get("DLS_P2P_TIMEOUT_S", "10"))
 _TICKS = int(TIMEOUT_S * 1e8)  # wall_clock64 runs at 100 MHz
 ERR_PULL, ERR_ACK = 1, 2
 BATCH = 16  # kP2PBatch (p2p_device.hpp): flags per batched notify launch
+# fault injection for negative controls ONLY: message slots whose producer never notifies (the
+# consumer's pull then times out into the error word and the executor raises TransportError)
+DROP_NOTIFY = frozenset(int(v) for v in os.environ.get("DLS_P2P_DROP_NOTIFY", "").split(",") if v.strip())
+
+
+def stalled_edges(slots, rank: int, step: int, ready, ack) -> List[str]:
+    """The messages of ``rank`` still behind at ``step``: receives whose producer's notify has
+    not arrived (ready[slot] < step) and sends whose consumer has not pulled (ack[slot] < step)."""
+    out = []
+    for (src, dst, key), slot in slots.items():
+        what = "/".join(str(k) for k in key[1:])
+        if dst == rank and ready[slot] < step:
+            out.append(f"receive of {what} from rank {src} (slot {slot}): producer's notify not seen")
+        elif src == rank and ack[slot] < step:
+            out.append(f"send of {what} to rank {dst} (slot {slot}): consumer has not pulled it")
+    return out
 
 
 def edge_slots(programs) -> Dict[Tuple[int, int, tuple], int]:
@@ -89,7 +107,7 @@ class Mailbox:
         n64 = 2 + 2 * n_slots
         n32 = n_slots + 1
         nbytes = (n64 * 8 + n32 * 4 + 255) // 256 * 256
-        self.raw = ops.ext().alloc_device(nbytes, 3)  # hipDeviceMallocUncached
+        self.raw = lifetime.keep(self, ops.ext().alloc_device(nbytes, 3))  # hipDeviceMallocUncached
         self.raw.zero_()
         i64 = self.raw[:n64 * 8].view(torch.int64)
         i32 = self.raw[n64 * 8:n64 * 8 + n32 * 4].view(torch.int32)
@@ -268,7 +286,8 @@ class DeviceComm:
             return _NoWork()
         if self.w.delay_us > 0:  # single-GPU harness: the notify lands late (a missing wait shows)
             self.e.p2p_delay(self.w.delay_us, self.mb.step)
-        self.e.p2p_notify(self.mb.ready_addr(self.w.bases[peer]["mail"], slot), self.mb.step)
+        if slot not in DROP_NOTIFY:
+            self.e.p2p_notify(self.mb.ready_addr(self.w.bases[peer]["mail"], slot), self.mb.step)
         return _SendWork(self, slot)
 
     def irecv(self, buf: torch.Tensor, peer: int, key=None):
@@ -297,7 +316,8 @@ class DeviceComm:
         slots = {k: self._slot(self.rank, ops_[k][2], ops_[k][3]) for k in sends}
         if self.w.delay_us > 0:
             self.e.p2p_delay(self.w.delay_us, self.mb.step)
-        flags = [self.mb.ready_addr(self.w.bases[ops_[k][2]]["mail"], slots[k]) for k in sends]
+        flags = [self.mb.ready_addr(self.w.bases[ops_[k][2]]["mail"], slots[k]) for k in sends
+                 if slots[k] not in DROP_NOTIFY]
         for i in range(0, len(flags), BATCH):
             self.e.p2p_notify_many(flags[i:i + BATCH], self.mb.step)
         for k in sends:
@@ -318,6 +338,11 @@ class DeviceComm:
         """The rank's error word (host read: synchronises): bit 0 a pull, bit 1 an ack wait
         timed out."""
         return int(self.mb.err.item())
+
+    def stalled(self) -> List[str]:
+        """This rank's messages still behind its step counter (host reads: synchronises)."""
+        return stalled_edges(self.w.slots, self.rank, int(self.mb.step.item()), self.mb.ready.tolist(),
+                             self.mb.ack.tolist())
 
 
 # ---------------------------------------------------------------------------------------------
@@ -348,19 +373,34 @@ class HostP2PWorld:
         self.step = {r: 0 for r in local_ranks}
         self.err = {r: 0 for r in local_ranks}
         self.moved = {r: 0 for r in local_ranks}
+        self.aborted = False
         self.arenas: Dict[int, Dict[str, torch.Tensor]] = {}
 
     def attach(self, rank: int, act: torch.Tensor, param: torch.Tensor) -> None:
         self.arenas[rank] = {"act": act.view(-1).view(torch.uint8), "param": param.view(-1).view(torch.uint8)}
 
     def wait_for(self, pred, rank: int, code: int) -> bool:
-        """Block until ``pred()`` (under the condition's lock); on timeout fold ``code`` into the
-        rank's error word and give up (wrong numbers, as on the GPU, never a hang)."""
+        """Block until ``pred()`` (under the condition's lock); on timeout — or once a rank of
+        the job has failed (:meth:`abort`) — fold ``code`` into the rank's error word and give
+        up (wrong numbers, as on the GPU, never a hang)."""
         with self.cv:
-            if self.cv.wait_for(pred, self.timeout_s):
+            if self.cv.wait_for(lambda: pred() or self.aborted, self.timeout_s) and not self.aborted:
+                return True
+            if pred():
                 return True
             self.err[rank] |= code
+            # the job's protocol is broken from here on: later waits give up at once (a second
+            # full timeout per wait would only delay the failure the executor now reports)
+            self.aborted = True
+            self.cv.notify_all()
             return False
+
+    def abort(self) -> None:
+        """A rank of the job failed: every wait still pending (or posted later) gives up at
+        once instead of after its full timeout."""
+        with self.cv:
+            self.aborted = True
+            self.cv.notify_all()
 
     def close(self) -> None:
         pass
@@ -472,7 +512,8 @@ class HostDeviceComm:
         w = self.w
         with w.cv:
             step = w.step[self.rank]
-            w.ready[peer][slot] = max(w.ready[peer][slot], step)
+            if slot not in DROP_NOTIFY:
+                w.ready[peer][slot] = max(w.ready[peer][slot], step)
             w.cv.notify_all()
         return _HostSend(self, slot, step)
 
@@ -500,3 +541,8 @@ class HostDeviceComm:
 
     def errors(self) -> int:
         return self.w.err[self.rank]
+
+    def stalled(self) -> List[str]:
+        w = self.w
+        with w.cv:
+            return stalled_edges(w.slots, self.rank, w.step[self.rank], w.ready[self.rank], w.ack[self.rank])

@@ -42,6 +42,7 @@ from ..core.task import Task
 from ..ops import tuning as _tuning
 from ..models.params import ParamStore, group_layout
 from ..utils.tracing import Roctx
+from . import lifetime
 from .comm import make_comm
 from .program import Program
 
@@ -161,7 +162,16 @@ REFILL_BLOCKS = int(os.environ.get("DLS_REFILL_BLOCKS", "64"))
 # a pre-norm MLP block (folded norm + fc1 + GELU, then fc2 + residual) as ONE launch
 # (ops.mlp_fused, csrc/kernels/gemm_fused.hip) where the shape fits its grid (GPU)
 MLP_FUSED = os.environ.get("DLS_MLP_FUSED", "0") == "1"
+# device p2p transport: every P2P_CHECK_EVERY-th step the rank's error word is mirrored into
+# pinned host memory (an asynchronous copy, no host sync) and the mirror of the previous check
+# is read; a set word fails the step loudly (TransportError). check_transport() reads it
+# synchronously (the CLI, the bench and the evaluation harness call it after their steps).
+P2P_CHECK_EVERY = max(1, int(os.environ.get("DLS_P2P_CHECK_EVERY", "8")))
 
+
+class TransportError(RuntimeError):
+    """A device-transport wait gave up after DLS_P2P_TIMEOUT_S (devp2p.py): the wait stopped
+    spinning and the step went on, so this rank's outputs of that step are wrong."""
 
 
 class DAGExecutor:
@@ -236,6 +246,8 @@ class DAGExecutor:
         self.launches: Optional[int] = None  # kernel launches of one captured step (hipGraph kernel nodes)
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
+        self._err_mirror: Optional[torch.Tensor] = None  # device transport: pinned copy of the error word
+        self._watch_n = 0
         self._setup()
         self._exp_ids: Dict[str, torch.Tensor] = {}
         self._routed_in: Dict[str, torch.Tensor] = {}  # received hidden state -> local experts (int32)
@@ -315,7 +327,6 @@ class DAGExecutor:
         self._capture_plan: Optional[Dict[int, int]] = None  # set while capture_segments runs
         self._seg_pool = None
         self._cap_stream = None  # side stream segment captures run on (_capture_segment)
-        self._empty_graphs: List[object] = []  # captures that recorded nothing (kept alive)
         self._rec: Optional[_Recorder] = None   # set while a step is recorded for the runner
         self._runner = None                     # native StepRunner replaying the recorded step
         self.issue_mode: Optional[str] = None  # "runner" / "python" for segment-replayed programs
@@ -1718,6 +1729,8 @@ class DAGExecutor:
             self._fast[0](self._fast[1], self._fast[2])
             if self._mlp_fused:
                 self.check_mlp_fused()
+            if self._fast[4]:
+                self._watch_transport()
             self.last = self._fast[3]
             return self._fast[3]
         stats = StepStats()
@@ -1757,10 +1770,68 @@ class DAGExecutor:
                 stats.timeline = [(n, a, b) for n, c, a, b in stats.events if c == "kernel"]
         if self._mlp_fused:
             self.check_mlp_fused()
+        if self._device_p2p:
+            self._watch_transport()
         if self.debug:
             self.check_guards()
         self.last = stats
         return stats
+
+    # ------------------------------------------------------------ device-transport health
+    def transport_errors(self) -> int:
+        """This rank's device-transport error word (bit 0: a pull, bit 1: an ack wait timed
+        out); 0 for RCCL / the loopback hub. A host read (synchronises on the GPU)."""
+        return int(self.comm.errors()) if self._device_p2p and not self.comm.dry else 0
+
+    def check_transport(self) -> None:
+        """Raise :class:`TransportError` (naming the rank and the edges still behind) if any
+        device-transport wait of this rank gave up since the last reset."""
+        err = self.transport_errors()
+        if err:
+            raise TransportError(self._transport_msg(err))
+
+    def reset_transport_errors(self) -> None:
+        """Clear the error word and its host mirror (after warm-up: a cold first step's
+        code-object loading on one rank can outlast a peer's wait)."""
+        if self._device_p2p:
+            self.comm.reset_errors()
+            if self._err_mirror is not None:
+                self._err_mirror.zero_()
+
+    def _transport_msg(self, err: int) -> str:
+        from .devp2p import ERR_ACK, ERR_PULL, TIMEOUT_S
+
+        what = [n for bit, n in ((ERR_PULL, "a pull"), (ERR_ACK, "an ack wait")) if err & bit]
+        behind = self.comm.stalled() if hasattr(self.comm, "stalled") else []
+        msg = (f"rank {self.prog.rank}: device transport: {' and '.join(what) or 'a wait'} timed out "
+               f"(error word {err}, DLS_P2P_TIMEOUT_S={TIMEOUT_S}); this rank's outputs are wrong")
+        if behind:
+            msg += "; edges behind: " + "; ".join(behind[:8]) + (" ..." if len(behind) > 8 else "")
+        return msg
+
+    def _watch_transport(self) -> None:
+        """Device transport, after a step is issued: every P2P_CHECK_EVERY-th step read the
+        error word's host mirror (written by an asynchronous copy issued at the previous check,
+        behind that step's kernels) and issue the next copy — a timed-out wait fails a later
+        step loudly without a host synchronisation per step. The host transport (CPU) reads
+        its word directly, every step."""
+        if self.comm.dry:
+            return
+        if not self.gpu:
+            err = self.comm.errors()
+            if err:
+                raise TransportError(self._transport_msg(err))
+            return
+        self._watch_n += 1
+        if self._watch_n % P2P_CHECK_EVERY:
+            return
+        m = self._err_mirror
+        if m is None:
+            m = self._err_mirror = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        seen = int(m[0])
+        if seen:
+            raise TransportError(self._transport_msg(seen))
+        m.copy_(self.comm.mb.err, non_blocking=True)
 
     def check_mlp_fused(self) -> None:
         """The one-launch MLP block (DLS_MLP_FUSED=1, off by default) gives up a poll after its
@@ -1826,7 +1897,8 @@ class DAGExecutor:
         self._sync()
         # captured on a side stream without torch.cuda.graph's device-wide synchronize (ranks
         # sharing one GPU may be capturing their own graphs meanwhile)
-        g = torch.cuda.CUDAGraph(keep_graph=True)
+        # (kept until this executor dies, then destroyed at a quiesce point: parallel/lifetime.py)
+        g = lifetime.keep(self, torch.cuda.CUDAGraph(keep_graph=True))
         cur = torch.cuda.current_stream(self.device)
         if self._cap_stream is None:
             self._cap_stream = torch.cuda.Stream(self.device)
@@ -1847,7 +1919,7 @@ class DAGExecutor:
             # step()'s fast path: the launch function, its arguments, the (static) stats
             # (the stream current at capture: the rank's own, where every later step is issued)
             self._fast = (ops.ext().graph_launch, self._graph_exec, cur.cuda_stream,
-                          StepStats(kernels=self.prog.n_kernels))
+                          StepStats(kernels=self.prog.n_kernels), self._device_p2p)
         return True
 
     def _sync(self) -> None:
@@ -1913,7 +1985,7 @@ class DAGExecutor:
         a side stream ordered after the compute stream; the compute stream waits for it."""
         if all(k in self._moe_skip or k in self._mlp_skip or k in self._xskip for k in range(i, seg_end)):
             return None  # its runs issue with a batch elsewhere: no graph at all
-        g = torch.cuda.CUDAGraph(keep_graph=True)
+        g = lifetime.keep(self, torch.cuda.CUDAGraph(keep_graph=True))
         cur = torch.cuda.current_stream(self.device)
         if self._cap_stream is None:
             self._cap_stream = torch.cuda.Stream(self.device)
@@ -1937,10 +2009,9 @@ class DAGExecutor:
             if ops.ext().graph_nodes(g.raw_cuda_graph()) == 0:
                 # every run of the segment was folded into another launch (a norm written by its
                 # producer, say): nothing to replay — no graph launch per step for it. The empty
-                # graph is kept, not destroyed here: tearing a graph down while another rank's
-                # thread of the single-GPU harness is capturing aborted the process
+                # graph is not destroyed here (lifetime.keep): tearing a graph down while another
+                # rank's thread of the single-GPU harness is capturing aborted the process
                 cur.wait_stream(cs)
-                self._empty_graphs.append(g)
                 return None
             g.instantiate()
         cur.wait_stream(cs)
@@ -1970,7 +2041,7 @@ class DAGExecutor:
             return False
         if self.gpu:
             self._sync()  # the previous steps' cross-step fills are complete
-        r = ops.ext().StepRunner()
+        r = lifetime.keep(self, ops.ext().StepRunner())
         if self._copy_stream is not None:
             r.set_copy_stream(self._copy_stream.cuda_stream)
         if self.comm is not None and self.comm.kind == "loopback":

@@ -46,7 +46,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
                  poison: bool = True, store=None, timeout_s: float = 120.0,
                  before_steps: Optional[Callable] = None, cpu_runner: bool = False,
                  sync_debug: bool = False, autotune: bool = False, transport: str = "hub",
-                 single_issue: bool = False) -> LoopbackRun:
+                 single_issue: bool = False, p2p_timeout_s: Optional[float] = None) -> LoopbackRun:
     """Build one executor per rank of ``plan`` on ``device``, then drive every rank from its own
     thread: ``warmup`` eager steps, capture (segment hipGraphs + native runner for programs with
     p2p), ``steps`` timed steps. ``before_steps(executors)`` may patch the executors first
@@ -58,21 +58,37 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     ``transport="device"``: the edges are moved by kernels (parallel/devp2p.py) — notify,
     pull and ack flags, no host pairing — and each rank's whole step captures into ONE hipGraph;
     ``delay_us`` then delays every notify and ``poison`` fills each receive region with NaN
-    when the receive is posted. ``single_issue`` (captured whole-step graphs only): after
+    when the receive is posted (``p2p_timeout_s``: the host transport's wait limit on the CPU;
+    on the GPU devp2p's DLS_P2P_TIMEOUT_S). ``single_issue`` (captured whole-step graphs only): after
     warm-up, ONE host thread issues every rank's timed steps round-robin (graph launches are
     asynchronous), so ``host_us`` is the issue cost of a step without GIL contention between
     rank threads. On the CPU the same protocol runs with host waits (devp2p.HostP2PWorld)."""
+    from . import lifetime
+
+    with lifetime.quiesced():
+        # garbage of earlier runs (executors, their hipGraphs / runners / buffers) is collected and
+        # destroyed here, on the calling thread, and the cyclic collector stays paused while the
+        # rank threads capture: a graph torn down by a finaliser on one rank thread while another
+        # is inside a capture aborted the process (parallel/lifetime.py)
+        return _run_loopback(plan, device, steps, warmup, capture, delay_us, poison, store, timeout_s,
+                             before_steps, cpu_runner, sync_debug, autotune, transport, single_issue, p2p_timeout_s)
+
+
+def _run_loopback(plan, device, steps, warmup, capture, delay_us, poison, store, timeout_s, before_steps,
+                  cpu_runner, sync_debug, autotune, transport, single_issue, p2p_timeout_s) -> LoopbackRun:
     from . import executor as exm
     from . import runtime
 
     device = torch.device(device)
     gpu = device.type == "cuda"
     world = plan.world
+    dw = None
     if transport == "device" and not gpu:
         # the device transport's protocol with host waits (devp2p.HostP2PWorld): the executor's
         # device-transport paths on the CPU, a progress error as a timed-out wait
         from .devp2p import HostP2PGroup, HostP2PWorld
-        dw = HostP2PWorld(plan, range(world), poison=poison, timeout_s=min(timeout_s, 30.0))
+        dw = HostP2PWorld(plan, range(world), poison=poison,
+                          timeout_s=p2p_timeout_s if p2p_timeout_s is not None else min(timeout_s, 30.0))
         groups = [HostP2PGroup(dw, r) for r in range(world)]
     elif transport == "device":
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
@@ -143,7 +159,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
                         streams[r].synchronize()
                     start.wait()  # every rank past its warm-up before any error word is cleared
                     warm_err[r] = ex.comm.errors()
-                    ex.comm.reset_errors()
+                    ex.reset_transport_errors()
                 elif cpu_runner and not gpu and not ex.build_runner():
                     raise RuntimeError("CPU step runner refused the program")
                 start.wait()
@@ -166,8 +182,22 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
                     streams[r].synchronize()
                 ms[r] = (time.perf_counter() - t0) / max(steps, 1) * 1e3
         except BaseException as e:  # noqa: BLE001 — reported below, with the rank
+            # a step that failed after one of this rank's device-transport waits gave up failed
+            # BECAUSE of it (it computed on data that never arrived): report the transport error
+            code = 0
+            if transport == "device" and not isinstance(e, exm.TransportError):
+                try:
+                    code = exs[r].transport_errors()
+                except Exception:  # noqa: BLE001
+                    code = 0
+            if code:
+                te = exm.TransportError(exs[r]._transport_msg(code))
+                te.__cause__ = e
+                e = te
             errors.append((r, e))
             start.abort()
+            if hasattr(dw, "abort"):  # host transport: the peers' pending waits give up now
+                dw.abort()
             if sync_debug and gpu:
                 torch.cuda.set_sync_debug_mode(0)
 
@@ -201,6 +231,7 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     if gpu:
         torch.cuda.synchronize(device)
     real = [(r, e) for r, e in errors if not isinstance(e, threading.BrokenBarrierError)]
+    real.sort(key=lambda re_: not isinstance(re_[1], exm.TransportError))  # the root cause first
     if real or errors:
         r, e = (real or errors)[0]
         raise RuntimeError(f"loopback harness: rank {r} failed: {e!r}") from e

@@ -171,3 +171,53 @@ def test_bench_extras_watchdog_keeps_headline():
     assert len(lines) == 1
     _check(lines[0], 2)
     assert "unfinished" in lines[0]["extras_error"]
+
+
+# ------------------------------------------------- device transport: a timed-out wait fails loudly
+RUN_DEV = [sys.executable, "-m", "distributed_llm_scheduler_amd", "run", "--placement", "pipeline", "--replicas",
+           "2", "--loopback", "2", "--transport", "device", "--steps", "2", "--warmup", "1"]
+
+
+def _cli(extra, env_extra, device_args):
+    env = dict(os.environ, PYTHONPATH=REPO, **env_extra)
+    r = subprocess.run(RUN_DEV + device_args + extra, cwd=REPO, env=env, capture_output=True, text=True,
+                       timeout=300)
+    return r.returncode, _json_lines(r.stdout), r.stderr
+
+
+@pytest.mark.parametrize("drop", [False, True])
+def test_cli_run_device_transport_timeout_exits_nonzero_cpu(drop):
+    """``run --loopback 2 --transport device`` on the CPU (devp2p.HostP2PWorld): with every
+    notify it prints a valid line and exits 0; with the first message's notify dropped
+    (DLS_P2P_DROP_NOTIFY, negative control) the consumer's pull times out, the executor raises
+    TransportError naming the rank and the edge, and the CLI exits 3 with ``valid: false``."""
+    env = {"DLS_P2P_TIMEOUT_S": "0.5"}
+    if drop:
+        env["DLS_P2P_DROP_NOTIFY"] = "0"
+    rc, lines, err = _cli(["--model", "tiny-gpt2", "--seq", "16"], env, ["--device", "cpu"])
+    assert len(lines) == 1, err[-3000:]
+    if drop:
+        assert rc == 3 and lines[0]["valid"] is False, (rc, lines, err[-2000:])
+        assert "timed out" in lines[0]["error"] and "slot 0" in lines[0]["error"] and "rank 1" in lines[0]["error"]
+    else:
+        assert rc == 0 and lines[0]["valid"] is True and lines[0]["p2p_errors"] == [0, 0], (rc, err[-2000:])
+
+
+@pytest.mark.gpu
+@pytest.mark.isolated
+@pytest.mark.timeout(280)
+@pytest.mark.parametrize("drop", [False, True])
+def test_cli_run_device_transport_timeout_exits_nonzero_gpu(drop):
+    """The same on one MI355X: two ranks of one process, each rank's step one hipGraph with the
+    edges moved by kernels; a dropped notify makes the pull kernel give up into the error word,
+    the CLI reads it after the timed steps and exits 3."""
+    env = {"DLS_P2P_TIMEOUT_S": "0.2", "GPU_MAX_HW_QUEUES": "16"}
+    if drop:
+        env["DLS_P2P_DROP_NOTIFY"] = "0"
+    rc, lines, err = _cli(["--model", "mini-gpt2", "--seq", "64"], env, [])
+    assert len(lines) == 1, err[-3000:]
+    if drop:
+        assert rc == 3 and lines[0]["valid"] is False, (rc, lines, err[-2000:])
+        assert "timed out" in lines[0]["error"] and "rank 1" in lines[0]["error"]
+    else:
+        assert rc == 0 and lines[0]["valid"] is True and lines[0]["p2p_errors"] == [0, 0], (rc, err[-2000:])

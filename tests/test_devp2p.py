@@ -83,6 +83,7 @@ def _ipc_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
+@pytest.mark.isolated
 @pytest.mark.timeout(240)
 def test_device_transport_across_processes_via_ipc():
     """Two rank PROCESSES on one MI355X: arenas and mailboxes exchanged as IPC handles, edges
@@ -107,6 +108,7 @@ def test_device_transport_across_processes_via_ipc():
 
 
 @pytest.mark.gpu
+@pytest.mark.isolated
 @pytest.mark.timeout(120)
 def test_batched_notify_kernel():
     """The sends of one program point notify from ONE launch (p2p_notify_many): every consumer

@@ -1,0 +1,142 @@
+"""Deferred destruction of native GPU objects (parallel/lifetime.py).
+
+Round 5's driver GPU suite ended mid-run, with no summary line, at the first 4-rank case of the
+single-GPU multi-rank harness. The harness captures hipGraphs on several rank threads of one
+process; the cyclic garbage collector runs on whichever thread allocates and finalises
+executors left over from earlier tests, and destroying a hipGraph while another thread is
+inside a capture had already aborted the process once (round 4). The fix: executors hand their
+graphs / runners / device buffers to ``lifetime.keep``; a dead executor's objects go to a
+graveyard that only ``lifetime.release`` empties at quiesce points, and the harness pauses the
+collector across its concurrent captures (``lifetime.quiesced``)."""
+import gc
+import threading
+
+import pytest
+import torch
+
+from distributed_llm_scheduler_amd.parallel import lifetime
+
+
+class _Res:
+    destroyed = []
+
+    def __init__(self, name):
+        self.name = name
+
+    def __del__(self):
+        _Res.destroyed.append(self.name)
+
+
+class _Owner:
+    def __init__(self):
+        self.me = self  # a reference cycle: only the cyclic collector frees it
+
+
+def test_kept_objects_outlive_their_owner_until_release():
+    lifetime.release()
+    _Res.destroyed.clear()
+    o = _Owner()
+    lifetime.keep(o, _Res("g1"))
+    lifetime.keep(o, _Res("g2"))
+    del o
+    gc.collect()  # the owner dies here (any thread could run this): nothing is destroyed
+    assert _Res.destroyed == [] and lifetime.graveyard_size() == 2
+    assert lifetime.release() == 2
+    assert sorted(_Res.destroyed) == ["g1", "g2"] and lifetime.graveyard_size() == 0
+
+
+def test_quiesced_collects_first_and_pauses_the_collector():
+    lifetime.release()
+    _Res.destroyed.clear()
+    o = _Owner()
+    lifetime.keep(o, _Res("old"))
+    del o
+    with lifetime.quiesced():
+        # garbage from before the section was collected AND destroyed on entry
+        assert _Res.destroyed == ["old"]
+        assert not gc.isenabled()
+        o2 = _Owner()
+        lifetime.keep(o2, _Res("new"))
+        del o2
+        gc.collect()  # an explicit collection inside: buried, and release() is a no-op here
+        assert lifetime.release() == 0 and _Res.destroyed == ["old"]
+    assert gc.isenabled()
+    assert lifetime.release() == 1 and _Res.destroyed == ["old", "new"]
+
+
+def test_executor_graphs_are_kept_by_the_executor():
+    """The executor registers every hipGraph and native runner it builds (CPU: the runner)."""
+    from distributed_llm_scheduler_amd.parallel import executor as exm
+    from distributed_llm_scheduler_amd.parallel import runtime
+
+    p = runtime.plan("tiny-gpt2", world=1, seq=16)
+    ex = runtime.make_executor(p, 0, torch.device("cpu"), runtime.make_store(p), use_graph=False)
+    saved = exm.RUNNER_CPU
+    exm.RUNNER_CPU = True
+    try:
+        ex.step()
+        assert ex.build_runner()
+    finally:
+        exm.RUNNER_CPU = saved
+    assert ex._runner in ex.__dict__["_native_keep"]
+
+
+@pytest.mark.gpu
+@pytest.mark.isolated
+@pytest.mark.timeout(180)
+def test_gc_during_capture_on_another_thread():
+    """The failing ordering, forced: thread T is inside a hipGraph capture when the main thread
+    runs the cyclic collector over a dead executor that owns captured hipGraphs. The executor's
+    graphs are buried, not destroyed, T's capture completes and replays correctly, and the
+    graphs are destroyed later at a quiesce point."""
+    from distributed_llm_scheduler_amd.parallel import runtime
+
+    dev = torch.device("cuda:0")
+    lifetime.release()
+    p = runtime.plan("mini-gpt2", world=1, seq=64)
+    ex = runtime.make_executor(p, 0, dev, runtime.make_store(p), use_graph=True)
+    ex.step()
+    assert ex.capture() and ex._graph is not None
+    ex.step()
+    torch.cuda.synchronize()
+    ex._cycle = ex  # only the cyclic collector can free it
+    kept = len(ex.__dict__["_native_keep"])
+    assert kept >= 1
+    del ex
+
+    inside, collected, err = threading.Event(), threading.Event(), []
+    x = torch.randn(256, 256, device=dev)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(dev)
+
+    def capture():
+        try:
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                g.capture_begin(capture_error_mode="thread_local")
+                try:
+                    y = x @ x
+                    inside.set()
+                    assert collected.wait(60), "main thread never collected"
+                    capture.out = torch.relu(y) + 1
+                finally:
+                    g.capture_end()
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+            inside.set()
+
+    t = threading.Thread(target=capture)
+    t.start()
+    assert inside.wait(60)
+    gc.collect()  # finalises the executor while T is capturing: its graphs go to the graveyard
+    buried = lifetime.graveyard_size()
+    collected.set()
+    t.join(60)
+    assert not t.is_alive() and not err, err
+    assert buried >= kept, (buried, kept)
+    g.replay()
+    torch.cuda.synchronize()
+    ref = torch.relu(x @ x) + 1
+    assert torch.allclose(capture.out, ref, rtol=1e-3, atol=1e-2)
+    assert lifetime.release() >= kept  # destroyed here, with no capture in flight
+    torch.cuda.synchronize()

@@ -153,8 +153,10 @@ def test_loopback_cpu_device_transport_catches_late_expert_pulls(monkeypatch):
 
     monkeypatch.setattr(exm.DAGExecutor, "_pull_expert_rows", late)
     monkeypatch.setattr(exm.DAGExecutor, "_moe_combine", combine)
-    run = run_loopback(p, "cpu", steps=1, warmup=0, store=store, transport="device", timeout_s=2.0)
-    assert any(ex.comm.errors() for ex in run.executors), "the old pull rule should stall"
+    # the stalled wait fails the step loudly (executor.TransportError, re-raised by the harness)
+    with pytest.raises(RuntimeError, match="timed out") as ei:
+        run_loopback(p, "cpu", steps=1, warmup=0, store=store, transport="device", timeout_s=2.0)
+    assert isinstance(ei.value.__cause__, exm.TransportError), repr(ei.value.__cause__)
     assert orig is not late
 
 
@@ -184,7 +186,10 @@ def test_expert_dp_batches_every_request_per_layer(world, monkeypatch):
 
 
 # --------------------------------------------------------------------------- GPU
-gpu = pytest.mark.gpu
+def gpu(f):
+    """GPU harness tests: several ranks capture on threads of ONE process, so each runs in a
+    fresh child process of its own with GPU_MAX_HW_QUEUES=16 (tests/conftest.py ``isolated``)."""
+    return pytest.mark.isolated(pytest.mark.gpu(f))
 
 
 def _gpu_plan(case, world, seq=64):

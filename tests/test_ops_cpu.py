@@ -118,3 +118,25 @@ def test_gemm_config_tables_agree():
     bad = re.search(r"constexpr bool swiglu_bad\(int c\) \{ return ([^;]*); \}", src).group(1)
     lib_bad = {c for c in range(ncfg) if eval(bad.replace("&&", " and ").replace("||", " or "), {"c": c})}
     assert lib_bad == set(tuning.SWIGLU_BAD)
+
+
+def test_no_tuning_entry_resolves_to_the_vendor_library_by_default():
+    """Every GEMM the table knows runs on the hand-written kernels unless DLS_ALLOW_VENDOR_GEMM=1:
+    no entry (plain, variant, per-model override, runner-up) resolves to hipBLASLt."""
+    from distributed_llm_scheduler_amd.ops import tuning
+
+    assert not tuning.VENDOR
+    t = tuning.table()
+    assert t, "tuning table missing"
+    for key in t:
+        shape, tg = key, ""
+        while shape[-1].isalpha():
+            shape, tg = shape[:-1], shape[-1] + tg
+        M, N, K = (int(v) for v in shape.split("x"))
+        assert tuning.lookup(M, N, K, tg)[0] != tuning.LIB, key
+        assert all(c[0] != tuning.LIB for c in tuning.runner_ups(M, N, K, tg, 10)), key
+        for m in tuning._overrides:
+            tuning.set_model(m)
+            assert tuning.lookup(M, N, K, tg)[0] != tuning.LIB, (m, key)
+        tuning.set_model(None)
+        assert (tuning.LIB, 1) not in tuning.candidates(M, N, K, 48, tg)
