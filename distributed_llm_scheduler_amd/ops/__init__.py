@@ -321,7 +321,11 @@ def derive_norm_gemm(w, ln_w, ln_b=None, bias=None):
     cs = wd.float().sum(1).contiguous()
     b = torch.zeros(w.shape[0], device=w.device) if bias is None else bias.float()
     if ln_b is not None:
-        b = b + wf @ ln_b.float()
+        # an elementwise product + row sum, NOT ``wf @ ln_b``: that GEMV would run in the vendor
+        # BLAS (hipBLASLt), which EXITS the process (status 1, "operation not permitted when
+        # stream is capturing") when first used while another rank thread of the single-GPU
+        # harness is capturing a graph — the round-5 driver GPU suite's silent death
+        b = b + (wf * ln_b.float()[None, :]).sum(1)
     return wd, cs, b.to(w.dtype).contiguous()
 
 

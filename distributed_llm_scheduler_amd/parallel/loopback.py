@@ -152,6 +152,9 @@ def _run_loopback(plan, device, steps, warmup, capture, delay_us, poison, store,
                 ex = exs[r]
                 for _ in range(warmup):
                     ex.step()
+                # every rank's eager warm-up (first-step allocations and weight transforms) is
+                # over before ANY rank starts capturing: nothing eager runs beside a capture
+                start.wait()
                 if capture and gpu:
                     ex.capture()
                 if transport == "device":

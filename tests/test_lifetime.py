@@ -115,7 +115,10 @@ def test_gc_during_capture_on_another_thread():
             with torch.cuda.stream(side):
                 g.capture_begin(capture_error_mode="thread_local")
                 try:
-                    y = x @ x
+                    # (elementwise kernels only: hipBLASLt first used inside a capture prints
+                    # "operation not permitted when stream is capturing" and EXITS the process
+                    # with status 1 — test_vendor_gemm_first_used_inside_a_capture_exits_the_process)
+                    y = x * 2.0
                     inside.set()
                     assert collected.wait(60), "main thread never collected"
                     capture.out = torch.relu(y) + 1
@@ -136,7 +139,60 @@ def test_gc_during_capture_on_another_thread():
     assert buried >= kept, (buried, kept)
     g.replay()
     torch.cuda.synchronize()
-    ref = torch.relu(x @ x) + 1
+    ref = torch.relu(x * 2.0) + 1
     assert torch.allclose(capture.out, ref, rtol=1e-3, atol=1e-2)
     assert lifetime.release() >= kept  # destroyed here, with no capture in flight
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+@pytest.mark.isolated
+@pytest.mark.timeout(120)
+def test_vendor_gemm_first_used_inside_a_capture_exits_the_process():
+    """Why the executor never calls hipBLASLt (torch.mm) in a captured step by default
+    (ops/tuning.py VENDOR): hipBLASLt's first use in a process, inside a
+    stream capture, prints "operation not permitted when stream is capturing" and ends the
+    process with exit status 1 — no Python exception, no pytest summary: the exact signature of
+    round 5's driver GPU-suite record (rc 1, output ending mid-line). Checked in a child process."""
+    import subprocess
+    import sys
+
+    code = ("import torch\n"
+            "x = torch.randn(256, 256, device='cuda')\n"
+            "g = torch.cuda.CUDAGraph()\n"
+            "s = torch.cuda.Stream()\n"
+            "with torch.cuda.stream(s):\n"
+            "    g.capture_begin()\n"
+            "    y = x @ x\n"
+            "    g.capture_end()\n"
+            "print('survived')\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100)
+    out = r.stdout + r.stderr
+    assert "survived" not in out or r.returncode == 0, out[-2000:]
+    if r.returncode != 0:  # this ROCm's behaviour: the library exits the process
+        assert "stream is capturing" in out, out[-2000:]
+
+
+def test_weight_transforms_call_no_vendor_blas():
+    """The executor's first-step weight transforms (norm folding) use elementwise kernels only:
+    a BLAS call there ran hipBLASLt on a rank thread while another rank thread captured, and
+    hipBLASLt exits the process in that case (the test above)."""
+    from torch.overrides import TorchFunctionMode
+
+    from distributed_llm_scheduler_amd import ops
+
+    seen = []
+
+    class Spy(TorchFunctionMode):
+        def __torch_function__(self, func, types, args=(), kwargs=None):
+            seen.append(getattr(func, "__name__", str(func)))
+            return func(*args, **(kwargs or {}))
+
+    w = torch.randn(48, 32).bfloat16()
+    lw, lb, bias = torch.randn(32), torch.randn(32), torch.randn(48)
+    with Spy():
+        wd, cs, b = ops.derive_norm_gemm(w, lw, lb, bias)
+    blas = {"matmul", "mm", "addmm", "mv", "addmv", "bmm", "__matmul__", "linear", "einsum"}
+    assert not blas & set(seen), seen
+    ref = bias.float() + w.float() @ lb.float()
+    assert torch.allclose(b.float(), ref.bfloat16().float(), rtol=2e-2, atol=2e-2)
