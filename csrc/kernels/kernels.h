@@ -190,6 +190,31 @@ void launch_delay(double us, hipStream_t s);
 
 // GPT-2 MLP block in one launch (gemm_fused.hip): h = act1(LN(x) W1'^T + b1) (folded norm with
 // handed-over row statistics), out = h W2^T + b2 + R (+ row statistics of out into stats_out)
+// One-launch pre-norm attention block (attn_block.hip): QKV GEMM with a folded norm, causal
+// MHA (head_dim 64), out-proj + bias + residual (+ next-norm row statistics), linked in-launch.
+struct AttnBlockArgs {
+  const void* x; int ldx;              // block input rows [M][H] (raw: the norm is folded)
+  const void* w1; const void* b1;      // derived QKV weight [3H][H], bias' [3H] (or null)
+  const float* colsum1;                // colsum(W') [3H]
+  const float* ext_stats;              // (sum, sum of squares) of x's rows [M][2], from x's producer
+  int ln_mode; float ln_eps;           // 1 LayerNorm, 2 RMSNorm
+  void* qkv; int ldqkv;                // workspace [M][3H]
+  void* o; int ldo;                    // workspace [M][H]
+  const void* wo; const void* bo;      // out-proj [H][H], bias [H] (or null)
+  const void* R; int ldr;              // residual [M][H]
+  void* out; int ldout;                // block output [M][H]
+  float* stats_out;                    // row statistics of out for the next folded norm (or null)
+  int M, H, B, S, n_head;
+  float scale;
+  int* sync;                           // attn_block_sync_ints() ints, zero before the first launch
+  int* err;                            // set when a poll exceeds spin_limit
+  int spin_limit;
+  unsigned long long* stamps = nullptr;  // diagnostic: [grid][4] (item, start, wait done, end) ticks
+};
+int attn_block_sync_ints(int M, int S, int B, int n_head);
+bool attn_block_supported(int M, int H, int B, int S, int n_head, int n_kv_head, int D);
+void launch_attn_block(const AttnBlockArgs& p, hipStream_t s);
+
 struct MlpFusedArgs {
   const void* x;
   int ldx;

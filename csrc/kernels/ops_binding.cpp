@@ -739,6 +739,71 @@ at::Tensor alloc_device(int64_t nbytes, int64_t flags) {
                           at::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
 }
 
+bool attn_block_ok(int64_t M, int64_t H, int64_t B, int64_t S, int64_t n_head, int64_t n_kv_head, int64_t D) {
+  return attn_block_supported((int)M, (int)H, (int)B, (int)S, (int)n_head, (int)n_kv_head, (int)D);
+}
+
+int64_t attn_block_sync_size(int64_t M, int64_t S, int64_t B, int64_t n_head) {
+  return attn_block_sync_ints((int)M, (int)S, (int)B, (int)n_head) + 1;  // + the error word
+}
+
+// The one-launch attention block (attn_block.hip). ``sync``: attn_block_sync_size() int32,
+// zeroed once (the launch resets its counters; the last element is the error word).
+void attn_block(const at::Tensor& x_in, const at::Tensor& w1, const c10::optional<at::Tensor>& b1,
+                const at::Tensor& colsum1, const at::Tensor& ext_stats, int64_t ln_mode, double eps,
+                const at::Tensor& qkv_in, const at::Tensor& o_in, const at::Tensor& wo,
+                const c10::optional<at::Tensor>& bo, const at::Tensor& res_in, const at::Tensor& out_in,
+                const c10::optional<at::Tensor>& stats_out, int64_t B, int64_t S, int64_t n_head, double scale,
+                const at::Tensor& sync, int64_t spin_limit, const c10::optional<at::Tensor>& stamps) {
+  at::Tensor x = as2d(x_in), qkv = as2d(qkv_in), o = as2d(o_in), r = as2d(res_in), out = as2d(out_in);
+  for (auto* t : {&x, &qkv, &o, &r, &out}) {
+    check_bf16(*t, "attn_block operand");
+    check_rows(*t, "attn_block operand");
+  }
+  check_bf16(w1, "w1");
+  check_bf16(wo, "wo");
+  check_rows(w1, "w1");
+  check_rows(wo, "wo");
+  const int64_t M = x.size(0), H = x.size(1);
+  TORCH_CHECK(w1.size(0) == 3 * H && w1.size(1) == H && wo.size(0) == H && wo.size(1) == H && qkv.size(0) == M &&
+                  qkv.size(1) == 3 * H && o.size(0) == M && o.size(1) == H && r.size(0) == M && r.size(1) == H &&
+                  out.size(0) == M && out.size(1) == H,
+              "attn_block: x [M][H], w1 [3H][H], qkv [M][3H], o [M][H], wo [H][H], residual / out [M][H]");
+  TORCH_CHECK(H % n_head == 0 && attn_block_ok(M, H, B, S, n_head, n_head, H / n_head),
+              "attn_block: shape not supported (M ", M, ", H ", H, ", B ", B, ", S ", S, ", heads ", n_head, ")");
+  TORCH_CHECK(ln_mode == 1 || ln_mode == 2, "attn_block: ln_mode 1 LayerNorm, 2 RMSNorm");
+  auto f32 = [&](const at::Tensor& t, int64_t n, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n, name,
+                " must be a contiguous fp32 GPU tensor of ", n, " elements");
+  };
+  f32(colsum1, 3 * H, "colsum1");
+  f32(ext_stats, 2 * M, "ext_stats");
+  if (stats_out.has_value()) f32(*stats_out, 2 * M, "stats_out");
+  for (auto* b : {&b1, &bo})
+    if (b->has_value()) {
+      check_bf16(**b, "bias");
+      TORCH_CHECK((*b)->is_contiguous(), "bias must be contiguous");
+    }
+  TORCH_CHECK(!b1.has_value() || b1->numel() == 3 * H, "b1 must be [3H]");
+  TORCH_CHECK(!bo.has_value() || bo->numel() == H, "bo must be [H]");
+  const int64_t n_sync = attn_block_sync_size(M, S, B, n_head);
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == at::kInt && sync.is_contiguous() && sync.numel() >= n_sync,
+              "sync must be a zeroed int32 GPU tensor of >= ", n_sync, " elements");
+  AttnBlockArgs p{x.data_ptr(), (int)x.stride(0), w1.data_ptr(), b1.has_value() ? b1->data_ptr() : nullptr,
+                  colsum1.data_ptr<float>(), ext_stats.data_ptr<float>(), (int)ln_mode, (float)eps,
+                  qkv.data_ptr(), (int)qkv.stride(0), o.data_ptr(), (int)o.stride(0), wo.data_ptr(),
+                  bo.has_value() ? bo->data_ptr() : nullptr, r.data_ptr(), (int)r.stride(0), out.data_ptr(),
+                  (int)out.stride(0), stats_out.has_value() ? stats_out->data_ptr<float>() : nullptr, (int)M, (int)H,
+                  (int)B, (int)S, (int)n_head, (float)scale, sync.data_ptr<int>(),
+                  sync.data_ptr<int>() + (n_sync - 1), (int)spin_limit};
+  if (stamps.has_value()) {
+    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->is_contiguous(),
+                "stamps must be a contiguous int64 GPU tensor");
+    p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
+  }
+  launch_attn_block(p, cur_stream());
+}
+
 void register_runner(py::module& m);  // runner.cpp
 void register_p2p(py::module& m);     // p2p_binding.cpp
 
@@ -746,6 +811,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "Hand-written HIP/CDNA4 (gfx950) kernels for distributed_llm_scheduler_amd";
   register_runner(m);
   register_p2p(m);
+  m.def("attn_block_ok", &attn_block_ok);
+  m.def("attn_block_sync_size", &attn_block_sync_size);
+  m.def("attn_block", &attn_block, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("colsum1"),
+        py::arg("ext_stats"), py::arg("ln_mode"), py::arg("eps"), py::arg("qkv"), py::arg("o"), py::arg("wo"),
+        py::arg("bo"), py::arg("residual"), py::arg("out"), py::arg("stats_out"), py::arg("B"), py::arg("S"),
+        py::arg("n_head"), py::arg("scale"), py::arg("sync"), py::arg("spin_limit"),
+        py::arg("stamps") = py::none());
   m.def("alloc_device", &alloc_device, py::arg("nbytes"), py::arg("flags") = 3);
   m.def("host_pull", &host_pull, py::arg("dst"), py::arg("src"), py::arg("blocks") = 256);
   m.def("gemm", &gemm, py::arg("a"), py::arg("w"), py::arg("bias") = py::none(), py::arg("residual") = py::none(),

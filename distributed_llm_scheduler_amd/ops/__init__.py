@@ -393,6 +393,35 @@ def mlp_fused(x, w1_derived, b1_derived, colsum1, ext_stats, mode, eps, h, w2, b
     return out
 
 
+def attn_block_ok(M, H, B, S, n_head, n_kv_head, head_dim) -> bool:
+    """Does the one-launch attention block (attn_block.hip) take this shape?"""
+    return bool(ext().attn_block_ok(int(M), int(H), int(B), int(S), int(n_head), int(n_kv_head), int(head_dim)))
+
+
+def attn_block_sync(M, S, B, n_head, device) -> torch.Tensor:
+    """A zeroed counter buffer for :func:`attn_block` (the launch resets it; last word: error)."""
+    return torch.zeros(int(ext().attn_block_sync_size(int(M), int(S), int(B), int(n_head))), dtype=torch.int32,
+                       device=device)
+
+
+def attn_block(x, w_qkv_derived, b_qkv_derived, colsum, ext_stats, mode, eps, qkv, o, w_o, b_o, residual, out,
+               B, S, n_head, stats_out=None, sync=None, scale=None, spin_limit=1 << 22):
+    """A pre-norm attention block as ONE launch (GPU, attn_block.hip): ``qkv = W'.norm(x) + b'``
+    (norm folded as in :func:`linear_norm`, row statistics of x in ``ext_stats``), causal MHA
+    over ``qkv`` into ``o``, ``out = o W_o^T + b_o + residual`` (+ each output row's statistics
+    into ``stats_out``) — the three stages linked inside the launch by per-row-block arrival
+    counters (a query tile starts once the q / k / v tiles of its rows and earlier ones exist;
+    an out-proj tile once every head of its rows is done). ``qkv`` and ``o`` are written too."""
+    m = {"layernorm": 1, "rmsnorm": 2}[mode]
+    H = x.shape[-1]
+    if sync is None:
+        sync = attn_block_sync(x.numel() // H, S, B, n_head, x.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(H // n_head)
+    ext().attn_block(x, w_qkv_derived, b_qkv_derived, colsum, ext_stats, m, float(eps), qkv, o, w_o, b_o, residual,
+                     out, stats_out, int(B), int(S), int(n_head), float(scale), sync, int(spin_limit))
+    return out
+
+
 def layernorm(x, w, b, eps=1e-5, residual=None, out=None, sum_out=None):
     """LayerNorm; with ``residual`` returns ``(LN(x + residual), x + residual)``."""
     if _gpu(x):

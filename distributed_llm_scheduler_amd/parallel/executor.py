@@ -162,6 +162,11 @@ REFILL_BLOCKS = int(os.environ.get("DLS_REFILL_BLOCKS", "64"))
 # a pre-norm MLP block (folded norm + fc1 + GELU, then fc2 + residual) as ONE launch
 # (ops.mlp_fused, csrc/kernels/gemm_fused.hip) where the shape fits its grid (GPU)
 MLP_FUSED = os.environ.get("DLS_MLP_FUSED", "0") == "1"
+# a pre-norm attention block (folded norm + QKV GEMM, causal MHA, out-proj + residual) as ONE
+# launch (ops.attn_block, csrc/kernels/attn_block.hip) where the shape fits (GPU). Off by default:
+# measured 36.3 vs 25.3 us for the three launches at GPT-2's block (profiles/r6_status/
+# attn_block_stamps_v3.txt: the heaviest query tiles wait for the last q/k/v tile of every row)
+ATTN_BLOCK = os.environ.get("DLS_ATTN_BLOCK", "0") == "1"
 # device p2p transport: every P2P_CHECK_EVERY-th step the rank's error word is mirrored into
 # pinned host memory (an asynchronous copy, no host sync) and the mirror of the previous check
 # is read; a set word fails the step loudly (TransportError). check_transport() reads it
@@ -247,6 +252,8 @@ class DAGExecutor:
         self._rope: Dict[Tuple[int, int, float], Tuple[torch.Tensor, torch.Tensor]] = {}
         self.last = StepStats()
         self._err_mirror: Optional[torch.Tensor] = None  # device transport: pinned copy of the error word
+        self._attn_sync: Optional[torch.Tensor] = None   # one-launch attention blocks' counters + error word
+        self._attn_mirror: Optional[torch.Tensor] = None
         self._watch_n = 0
         self._setup()
         self._exp_ids: Dict[str, torch.Tensor] = {}
@@ -1233,6 +1240,22 @@ class DAGExecutor:
         ops.moe_gather_combine(bufs, idx, slot, off, gate, residual=self._x(res_name), out=out, ptrs=ptrs,
                                post_norm=self._post_norm_out(self._flat(out)))
 
+    def _attn_block_ok(self, head: Task, norm: Optional[Task], x, residual, out, B: int, S: int) -> bool:
+        """Can this attention group run as the one-launch block (ops.attn_block)? GPU, MHA with
+        head_dim 64, no RoPE, causal, a norm folded with row statistics handed over by x's
+        producer, the residual in the group, no post-norm of the output, a shape the kernel
+        takes, and a weight no other reader shares."""
+        a, W = head.op.attrs, head.op.weights
+        if not (self.gpu and ATTN_BLOCK) or norm is None or residual is None or a.get("rope") \
+                or not a.get("causal", True) or a["n_kv_head"] != a["n_head"]:
+            return False
+        if self._ext_stats.get(norm.op.inputs[0]) is None or x.shape[-1] > FOLD_MAX_K \
+                or self._pn_given == norm.id or self._pn is not None:
+            return False
+        if self._w_users.get(W["w_qkv"], 1) > 1:
+            return False
+        return ops.attn_block_ok(x.shape[0], x.shape[-1], B, S, a["n_head"], a["n_kv_head"], a["head_dim"])
+
     def _run_group(self, ins) -> None:
         grp = [self.tasks[t] for t in ins.group]
         norm = None
@@ -1296,6 +1319,15 @@ class DAGExecutor:
             width = (nh + 2 * nkv) * D
             qkv = self._ws(0, (M, width))
             o = self._ws(M * width, (M, nh * D))
+            if self._attn_block_ok(head, norm, x, residual, out, B, S):
+                W1, cs, bd = self._prep(W["w_qkv"], norm, W.get("b_qkv"))
+                if self._attn_sync is None:  # (first, eager step: never allocated during capture)
+                    self._attn_sync = ops.attn_block_sync(M, S, B, nh, self.device)
+                ops.attn_block(x, W1, bd, cs, self._ext_stats[norm.op.inputs[0]], norm.op.kind,
+                               norm.op.attrs.get("eps", 1e-5), qkv, o, self._w(W["w_o"]),
+                               self._w(W["b_o"]) if "b_o" in W else None, residual, self._flat(out), B, S, nh,
+                               stats_out=st_out, sync=self._attn_sync)
+                return
             if a.get("rope"):
                 # RoPE in the QKV GEMM epilogue (q/k rows pair-interleaved at load time)
                 cos, sin = self._rope_tables(S, D, a.get("rope_theta", 10000.0))
@@ -1730,7 +1762,7 @@ class DAGExecutor:
             if self._mlp_fused:
                 self.check_mlp_fused()
             if self._fast[4]:
-                self._watch_transport()
+                self._watch()
             self.last = self._fast[3]
             return self._fast[3]
         stats = StepStats()
@@ -1770,8 +1802,8 @@ class DAGExecutor:
                 stats.timeline = [(n, a, b) for n, c, a, b in stats.events if c == "kernel"]
         if self._mlp_fused:
             self.check_mlp_fused()
-        if self._device_p2p:
-            self._watch_transport()
+        if self._device_p2p or self._attn_sync is not None:
+            self._watch()
         if self.debug:
             self.check_guards()
         self.last = stats
@@ -1809,29 +1841,47 @@ class DAGExecutor:
             msg += "; edges behind: " + "; ".join(behind[:8]) + (" ..." if len(behind) > 8 else "")
         return msg
 
-    def _watch_transport(self) -> None:
-        """Device transport, after a step is issued: every P2P_CHECK_EVERY-th step read the
-        error word's host mirror (written by an asynchronous copy issued at the previous check,
-        behind that step's kernels) and issue the next copy — a timed-out wait fails a later
-        step loudly without a host synchronisation per step. The host transport (CPU) reads
-        its word directly, every step."""
-        if self.comm.dry:
-            return
-        if not self.gpu:
+    def _watch(self) -> None:
+        """After a step is issued: every P2P_CHECK_EVERY-th step read the host mirrors of the
+        device error words — the device transport's, and the one-launch attention blocks' —
+        (written by asynchronous copies issued at the previous check, behind that step's kernels)
+        and issue the next copies: a wait that gave up fails a later step loudly without a host
+        synchronisation per step. The host transport (CPU) reads its word directly, every step."""
+        p2p = self._device_p2p and not self.comm.dry
+        if p2p and not self.gpu:
             err = self.comm.errors()
             if err:
                 raise TransportError(self._transport_msg(err))
+            p2p = False
+        if not self.gpu or not (p2p or self._attn_sync is not None):
             return
         self._watch_n += 1
         if self._watch_n % P2P_CHECK_EVERY:
             return
-        m = self._err_mirror
-        if m is None:
-            m = self._err_mirror = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        seen = int(m[0])
-        if seen:
-            raise TransportError(self._transport_msg(seen))
-        m.copy_(self.comm.mb.err, non_blocking=True)
+        if p2p:
+            m = self._err_mirror
+            if m is None:
+                m = self._err_mirror = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            seen = int(m[0])
+            if seen:
+                raise TransportError(self._transport_msg(seen))
+            m.copy_(self.comm.mb.err, non_blocking=True)
+        if self._attn_sync is not None:
+            m = self._attn_mirror
+            if m is None:
+                m = self._attn_mirror = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            if int(m[0]):
+                raise RuntimeError(self._attn_msg())
+            m.copy_(self._attn_sync[-1:], non_blocking=True)
+
+    def _attn_msg(self) -> str:
+        return (f"rank {self.prog.rank}: a one-launch attention block (ops.attn_block) gave up waiting for its "
+                f"q/k/v or attention tiles; the step's outputs are wrong")
+
+    def check_attn_block(self) -> None:
+        """Synchronous read of the one-launch attention blocks' error word (raises if set)."""
+        if self._attn_sync is not None and int(self._attn_sync[-1].item()) != 0:
+            raise RuntimeError(self._attn_msg())
 
     def check_mlp_fused(self) -> None:
         """The one-launch MLP block (DLS_MLP_FUSED=1, off by default) gives up a poll after its
@@ -1919,7 +1969,7 @@ class DAGExecutor:
             # step()'s fast path: the launch function, its arguments, the (static) stats
             # (the stream current at capture: the rank's own, where every later step is issued)
             self._fast = (ops.ext().graph_launch, self._graph_exec, cur.cuda_stream,
-                          StepStats(kernels=self.prog.n_kernels), self._device_p2p)
+                          StepStats(kernels=self.prog.n_kernels), self._device_p2p or self._attn_sync is not None)
         return True
 
     def _sync(self) -> None:

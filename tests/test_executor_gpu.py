@@ -244,8 +244,8 @@ def test_post_norm_under_memory_cap_on_gpu(monkeypatch, model):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("mlp_fused", [False, True])
-def test_gpt2_every_block_matches_reference(mlp_fused, monkeypatch):
+@pytest.mark.parametrize("mlp_fused,attn_block", [(False, False), (True, False), (False, True)])
+def test_gpt2_every_block_matches_reference(mlp_fused, attn_block, monkeypatch):
     """The real GPT-2-small DAG at S = 512 (the benchmarked shapes), block by block: the residual
     stream after each of the 12 blocks (the ``layer_i_output`` groups: fc2 GEMM + bias +
     residual, with the next block's folded-LN statistics handed over) against the fp32 reference
@@ -253,6 +253,7 @@ def test_gpt2_every_block_matches_reference(mlp_fused, monkeypatch):
     from distributed_llm_scheduler_amd.parallel import executor as exm
 
     monkeypatch.setattr(exm, "MLP_FUSED", mlp_fused)  # fc1 + fc2 of every block as ONE launch
+    monkeypatch.setattr(exm, "ATTN_BLOCK", attn_block)  # norm + QKV + attention + out-proj as ONE launch
     S = 512
     p = runtime.plan("gpt2", world=1, seq=S, batch=1)
     store = runtime.make_store(p)
@@ -271,6 +272,8 @@ def test_gpt2_every_block_matches_reference(mlp_fused, monkeypatch):
     ex._issue_run = issue
     ex.step()
     torch.cuda.synchronize()
+    assert (ex._attn_sync is not None) == attn_block  # the one-launch attention blocks ran
+    ex.check_attn_block()
     tok = synthetic_tokens("@tokens", S, p.cfg.vocab_size).view(1, S)
     hidden = []
     reference.gpt2_forward(p.cfg, store, tok, hidden=hidden)

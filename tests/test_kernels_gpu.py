@@ -789,3 +789,50 @@ def test_moe_xbatch_index_and_cross_request_experts(shared):
                              w2[e].cpu())
         _close(outs[gi][:cnt].cpu(), ref.float(), 3e-2)
         assert (outs[gi][cnt:].cpu().float() == 7.0).all(), "rows past the group's count were written"
+
+
+@pytest.mark.parametrize("B,S,H,nh", [(1, 512, 768, 12), (2, 256, 768, 12), (4, 128, 768, 12), (1, 1024, 768, 12),
+                                      (1, 512, 1024, 16)])
+def test_attn_block_one_launch(B, S, H, nh):
+    """The pre-norm attention block as ONE launch (attn_block.hip): folded LayerNorm-1 + QKV GEMM,
+    causal MHA, out-proj + bias + residual + the next norm's row statistics, linked by in-launch
+    ticket-ordered items and arrival counters — against the fp32 reference (GPT-2's block at
+    batch 1 x 512 and smaller shapes), three launches in a row on one counter buffer (each
+    resets its counters), no wait ever gave up."""
+    M, D = B * S, H // nh
+    assert ops.attn_block_ok(M, H, B, S, nh, nh, D)
+    x = _rand(M, H, scale=2.0, seed=400) + 0.2
+    w1, b1 = _rand(3 * H, H, scale=0.04, seed=401), _rand(3 * H, scale=0.1, seed=402)
+    wo, bo = _rand(H, H, scale=0.03, seed=403), _rand(H, scale=0.1, seed=404)
+    nw = (1 + 0.2 * _rand(H, seed=405).float()).to(torch.bfloat16)
+    nb = _rand(H, scale=0.1, seed=406)
+    res = _rand(M, H, seed=407)
+    xf = x.cpu().float()
+    st = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).to(DEV)
+    wd, cs, bd = ops.derive_norm_gemm(w1, nw, nb, b1)
+    qkv = torch.empty(M, 3 * H, device=DEV, dtype=torch.bfloat16)
+    o = torch.empty(M, H, device=DEV, dtype=torch.bfloat16)
+    out = torch.empty(M, H, device=DEV, dtype=torch.bfloat16)
+    sync = ops.attn_block_sync(M, S, B, nh, DEV)
+    for _ in range(3):
+        so = torch.zeros(M, 2, device=DEV)
+        ops.attn_block(x, wd, bd, cs, st, "layernorm", 1e-5, qkv, o, wo, bo, res, out, B, S, nh, stats_out=so,
+                       sync=sync)
+    torch.cuda.synchronize()
+    qr = ops.ref_linear(ops.ref_layernorm(x.cpu(), nw.cpu(), nb.cpu()), w1.cpu(), b1.cpu())
+    orf = ops.ref_attention(qr[:, :H], qr[:, H:2 * H], qr[:, 2 * H:], B, S, nh, nh, D, causal=True)
+    ref = ops.ref_linear(orf, wo.cpu(), bo.cpu(), residual=res.cpu()).float()
+    _close(qkv.cpu(), qr.float(), 3e-2)
+    _close(o.cpu(), orf.float(), 3e-2)
+    _close(out.cpu(), ref, 3e-2)
+    of = out.cpu().float()
+    _close(so.cpu(), torch.stack([of.sum(1), (of * of).sum(1)], 1), 1e-2)
+    assert int(sync[-1]) == 0 and int(sync[:-1].abs().sum()) == 0  # no timeout; counters reset
+
+
+def test_attn_block_shape_gate():
+    """Shapes the one-launch block does not take fall back to the three launches (executor)."""
+    assert ops.attn_block_ok(512, 768, 1, 512, 12, 12, 64)
+    assert ops.attn_block_ok(512, 1024, 1, 512, 16, 16, 64)       # GPT-2-medium
+    assert not ops.attn_block_ok(512, 4096, 1, 512, 32, 8, 128)   # Llama: GQA, head_dim 128
+    assert not ops.attn_block_ok(480, 768, 1, 480, 12, 12, 64)    # rows not a multiple of 64
