@@ -152,6 +152,13 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     for _ in range(warmup):
         ex.step()
     ctx.sync()
+    # expert-parallel capacity edges whose routing overflowed: widened on both of their ranks,
+    # then the step runs again (repeat: a corrected layer can change a later layer's routing)
+    ep_widened = 0
+    while runtime.ep_widen_on_overflow(ex, ctx.pg):
+        ep_widened += 1
+        ex.step()
+    ctx.sync()
     captured = ex.capture() if use_graph else False
     if captured and refine:
         log(f"[bench{tag}] rank {ctx.rank}: in-DAG GEMM refinement: {ex.refine_tuning()}")
@@ -171,6 +178,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     ms, per_rank = ctx.gather(mine)
     launches = ctx.gather_list(ex.launches if ex.launches is not None else -1)
     p2p_err = ctx.gather_list(ex.transport_errors())  # a timed-out device-transport wait: numbers invalid
+    ep_over = ctx.gather_list(len(ex.ep_overflow()))  # capacity overflow inside the timed steps
     st = plan.stats
     res = {
         "ms_per_step": round(ms, 5),
@@ -196,6 +204,11 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
         "issue_mode": ex.issue_mode or ("graph" if captured else "python"),
         "p2p": getattr(getattr(ex, "comm", None), "kind", None),
         "p2p_errors": [int(v) for v in p2p_err],
+        # expert-parallel capacity edges (program.plan_ep_capacity): widening rounds after warm-up,
+        # and groups that overflowed inside the timed steps (non-zero: those outputs were wrong)
+        "ep_widened_rounds": ep_widened,
+        "ep_overflow": [int(v) for v in ep_over],
+        "cross_gpu_bytes_rccl": st.get("cross_gpu_bytes_rccl"),
     }
     if profile or trace_out:
         s = ex.step(profile=True)
@@ -358,7 +371,8 @@ def main():
             # device transport: every rank's error word after the timed steps (non-zero: a wait
             # gave up, the step's numbers are wrong and ``valid`` is false)
             "p2p_errors": head["p2p_errors"],
-            "valid": not any(head["p2p_errors"]),
+            "valid": not any(head["p2p_errors"]) and not any(head["ep_overflow"]),
+            "cross_gpu_bytes_rccl": head["cross_gpu_bytes_rccl"],
             "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
             "per_rank_ms": head["per_rank_ms"],
             "hip_graph": head["hip_graph"],

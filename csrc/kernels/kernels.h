@@ -169,6 +169,26 @@ struct XbatchIndexArgs {
   int32_t* a_rows;
 };
 void launch_moe_xbatch_index(const XbatchIndexArgs& a, hipStream_t s);
+// Expert-parallel capacity edges (fixed-size RCCL messages, parallel/executor.py): the rows a
+// layer's routing sends to one expert GPU, packed (home rank) into / unpacked (expert GPU) from
+// a [cap][H] buffer in expert-sorted order — experts in the listed order, each expert's rows in
+// its sorted order. Rows past cap are not moved: the launch then sets ovf[flag] = 1 (and
+// ovf[eflag[k]] for an expert whose own count exceeds ecap[k]: its compact output rows
+// travel back in an edge of that capacity). No host sync: the counts are the device routing's.
+constexpr int kMoePackMaxDest = 8, kMoePackMaxExp = 8;
+struct MoePackDest {
+  void* buf;                        // [cap][H] compact rows
+  int cap, n_exp, flag;
+  int experts[kMoePackMaxExp];
+  int ecap[kMoePackMaxExp], eflag[kMoePackMaxExp];  // per expert: return-edge capacity / flag (-1: none)
+};
+struct MoePackArgs {
+  MoePackDest d[kMoePackMaxDest];
+  int n;
+};
+// unpack = 0: buf[c] = x[src[j]] (x: token rows); 1: x[j] = buf[c] (x: the expert-sorted rows)
+void launch_moe_pack(const void* x, int H, const int32_t* src_rows, const int32_t* offsets, const MoePackArgs& a,
+                     int32_t* ovf, int unpack, int max_rows, hipStream_t s);
 void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const float* weights, void* y, int M,
                         int topk, int H, const int32_t* range, hipStream_t s);
 // X [rows][K] sorted by expert, offsets [E+1], W [E][N][K] -> Y [rows][N]

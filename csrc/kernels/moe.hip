@@ -6,6 +6,8 @@
 //   combine : y[m] = sum_j w[m][j] * expert_out[slot_of[m*k+j]]   (fp32 sum, bf16 out)
 // Expert FFNs run as one grouped GEMM over the sorted rows (gemm.hip), so an EP edge
 // in the DAG carries exactly the token subset routed to the experts placed on a GPU.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -550,6 +552,44 @@ __global__ __launch_bounds__(256) void xbatch_index_kernel(XbatchIndexArgs a) {
   }
 }
 
+// Capacity edges (see kernels.h MoePackArgs): block (x, d) moves rows x, x + gridDim.x, ... of
+// destination d, one wave per row, 16-B vectors per lane. Every block recomputes d's segment
+// table from the device offsets (n_exp <= 8 experts: a few scalar loads).
+__global__ __launch_bounds__(256) void moe_pack_kernel(bf16* __restrict__ x, int H, const int32_t* __restrict__ src,
+                                                       const int32_t* __restrict__ off, MoePackArgs a,
+                                                       int32_t* __restrict__ ovf, int unpack) {
+  const MoePackDest& d = a.d[blockIdx.y];
+  int lo[kMoePackMaxExp], cum[kMoePackMaxExp + 1];
+  cum[0] = 0;
+#pragma unroll
+  for (int k = 0; k < kMoePackMaxExp; ++k) {
+    const int e = k < d.n_exp ? d.experts[k] : 0;
+    const int n = k < d.n_exp ? off[e + 1] - off[e] : 0;
+    lo[k] = k < d.n_exp ? off[e] : 0;
+    cum[k + 1] = cum[k] + n;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && k < d.n_exp && d.eflag[k] >= 0 && n > d.ecap[k]) ovf[d.eflag[k]] = 1;
+  }
+  const int total = cum[kMoePackMaxExp];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && total > d.cap && d.flag >= 0) ovf[d.flag] = 1;
+  const int rows = min(total, d.cap);
+  const int lane = threadIdx.x & 63;
+  bf16* buf = static_cast<bf16*>(d.buf);
+  for (int c = blockIdx.x * 4 + (threadIdx.x >> 6); c < rows; c += gridDim.x * 4) {
+    int k = 0;
+#pragma unroll
+    for (int q = 1; q < kMoePackMaxExp; ++q) k += (c >= cum[q]) ? 1 : 0;
+    const int j = lo[k] + c - cum[k];  // position in the expert-sorted order
+    bf16x8* cp = reinterpret_cast<bf16x8*>(buf + (size_t)c * H);
+    if (unpack) {
+      bf16x8* xp = reinterpret_cast<bf16x8*>(x + (size_t)j * H);
+      for (int v = lane; v < H / 8; v += 64) xp[v] = cp[v];
+    } else {
+      const bf16x8* xp = reinterpret_cast<const bf16x8*>(x + (size_t)src[j] * H);
+      for (int v = lane; v < H / 8; v += 64) cp[v] = xp[v];
+    }
+  }
+}
+
 void launch_moe_xbatch_index(const XbatchIndexArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(xbatch_index_kernel, dim3(1), dim3(256), 0, s, a);
 }
@@ -558,4 +598,11 @@ void launch_moe_combine(const void* expert_out, const int32_t* slot_of, const fl
                         int topk, int H, const int32_t* range, hipStream_t s) {
   hipLaunchKernelGGL(combine_kernel, dim3((M + 3) / 4), dim3(256), 0, s, (const bf16*)expert_out, slot_of, weights,
                      (bf16*)y, M, topk, H, range);
+}
+
+void launch_moe_pack(const void* x, int H, const int32_t* src_rows, const int32_t* offsets, const MoePackArgs& a,
+                     int32_t* ovf, int unpack, int max_rows, hipStream_t s) {
+  // blocks per destination: enough waves for the largest capacity (4 rows per block)
+  const int bx = std::max(1, std::min(64, (max_rows + 3) / 4));
+  hipLaunchKernelGGL(moe_pack_kernel, dim3(bx, a.n), dim3(256), 0, s, (bf16*)x, H, src_rows, offsets, a, ovf, unpack);
 }

@@ -518,6 +518,53 @@ at::Tensor moe_permute(const at::Tensor& x, const at::Tensor& src_rows, const c1
   return out;
 }
 
+// Expert-parallel capacity edges (kernels.h MoePackArgs): pack (unpack = false) the routed rows
+// of each destination into its [cap][H] buffer, or unpack (true) a received buffer into the
+// expert-sorted rows x. ovf: int32 flags (set to 1 where a count exceeded its capacity).
+void moe_pack(const at::Tensor& x, const at::Tensor& src_rows, const at::Tensor& offsets,
+              const std::vector<at::Tensor>& bufs, const std::vector<int64_t>& caps,
+              const std::vector<std::vector<int64_t>>& experts, const std::vector<int64_t>& flags,
+              const std::vector<std::vector<int64_t>>& ecaps, const std::vector<std::vector<int64_t>>& eflags,
+              at::Tensor& ovf, bool unpack) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0, "x must be contiguous [rows][H], H % 8 == 0");
+  TORCH_CHECK(src_rows.scalar_type() == at::kInt && offsets.scalar_type() == at::kInt && src_rows.is_contiguous() &&
+                  offsets.is_contiguous() && src_rows.is_cuda() && offsets.is_cuda(),
+              "src_rows / offsets: contiguous int32 GPU tensors");
+  TORCH_CHECK(ovf.scalar_type() == at::kInt && ovf.is_cuda() && ovf.is_contiguous(), "ovf: int32 GPU tensor");
+  const size_t n = bufs.size();
+  TORCH_CHECK(n >= 1 && n <= (size_t)kMoePackMaxDest && caps.size() == n && experts.size() == n &&
+                  flags.size() == n && ecaps.size() == n && eflags.size() == n,
+              "moe_pack: 1..", kMoePackMaxDest, " destinations, one entry each");
+  const int64_t H = x.size(1), E = offsets.numel() - 1;
+  MoePackArgs a{};
+  a.n = (int)n;
+  int max_rows = 0;
+  for (size_t d = 0; d < n; ++d) {
+    check_bf16(bufs[d], "buf");
+    TORCH_CHECK(bufs[d].is_contiguous() && bufs[d].numel() >= caps[d] * H, "buf ", d, " must hold cap x H elements");
+    TORCH_CHECK(experts[d].size() >= 1 && experts[d].size() <= (size_t)kMoePackMaxExp &&
+                    ecaps[d].size() == experts[d].size() && eflags[d].size() == experts[d].size(),
+                "moe_pack: 1..", kMoePackMaxExp, " experts per destination");
+    TORCH_CHECK(flags[d] < ovf.numel(), "flag index out of range");
+    a.d[d].buf = bufs[d].data_ptr();
+    a.d[d].cap = (int)caps[d];
+    a.d[d].n_exp = (int)experts[d].size();
+    a.d[d].flag = (int)flags[d];
+    for (size_t k = 0; k < experts[d].size(); ++k) {
+      TORCH_CHECK(experts[d][k] >= 0 && experts[d][k] < E, "expert id out of range");
+      TORCH_CHECK(eflags[d][k] < ovf.numel(), "expert flag index out of range");
+      a.d[d].experts[k] = (int)experts[d][k];
+      a.d[d].ecap[k] = (int)ecaps[d][k];
+      a.d[d].eflag[k] = (int)eflags[d][k];
+    }
+    max_rows = std::max(max_rows, (int)caps[d]);
+  }
+  if (unpack) TORCH_CHECK(x.size(0) >= src_rows.numel(), "unpack: x must hold the expert-sorted rows");
+  launch_moe_pack(x.data_ptr(), (int)H, src_rows.data_ptr<int32_t>(), offsets.data_ptr<int32_t>(), a,
+                  ovf.data_ptr<int32_t>(), unpack ? 1 : 0, max_rows, cur_stream());
+}
+
 // offs: each request's routing offsets (int32 [E+1], on the GPU); groups g: (reqs[g], experts[g]);
 // bases[q]: row of request q's expert-sorted block in the batch's token matrix
 void moe_xbatch_index(const std::vector<at::Tensor>& offs, const std::vector<int64_t>& reqs,
@@ -861,6 +908,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("moe_align", &moe_align);
   m.def("moe_route", &moe_route);
   m.def("moe_gate_route", &moe_gate_route);
+  m.def("moe_pack", &moe_pack);
   m.def("moe_permute", &moe_permute, py::arg("x"), py::arg("src_rows"), py::arg("out") = py::none());
   m.def("moe_xbatch_index", &moe_xbatch_index);
   m.def("moe_combine", &moe_combine, py::arg("expert_out"), py::arg("slot_of"), py::arg("weights"),

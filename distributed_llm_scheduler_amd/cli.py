@@ -163,6 +163,9 @@ def cmd_run(a) -> int:
         if failed is None:
             raise
     sync()
+    while failed is None and runtime.ep_widen_on_overflow(ex, dist.group.WORLD if world > 1 else None):
+        ex.step()  # expert capacity edges that overflowed: widened, the step runs again
+    sync()
     if gpu and not a.no_graph and failed is None:
         ex.capture()
     sync()

@@ -577,6 +577,40 @@ def moe_permute(x, src_rows, out=None):
     return out.copy_(y) if out is not None else y
 
 
+def moe_pack(x, src_rows, offsets, dests, ovf, unpack=False):
+    """Expert-parallel capacity edges (fixed-size messages; kernels.h MoePackArgs). ``dests``:
+    [(buf [cap][H], cap, experts, flag, ecaps, eflags)], one per expert GPU. Pack (``unpack``
+    False): buf row c <- token row ``x[src_rows[j]]`` for the c-th routed row of the listed
+    experts (expert-sorted order, experts in the listed order). Unpack: ``x`` holds the
+    expert-sorted rows and row j <- buf row c. Rows past ``cap`` are not moved and set
+    ``ovf[flag]``; an expert whose own count exceeds ``ecaps[k]`` sets ``ovf[eflags[k]]`` (its
+    compact output travels back in an edge of that many rows). No host sync on the GPU."""
+    if _gpu(x):
+        ext().moe_pack(x, src_rows, offsets, [d[0] for d in dests], [int(d[1]) for d in dests],
+                       [list(map(int, d[2])) for d in dests], [int(d[3]) for d in dests],
+                       [list(map(int, d[4])) for d in dests], [list(map(int, d[5])) for d in dests], ovf, bool(unpack))
+        return
+    off = [int(v) for v in offsets.tolist()]
+    H = x.shape[-1]
+    for buf, cap, experts, flag, ecaps, eflags in dests:
+        b2 = buf.view(-1)[:int(cap) * H].view(int(cap), H)
+        c = 0
+        for e, ecap, ef in zip(experts, ecaps, eflags):
+            lo, hi = off[e], off[e + 1]
+            if ef >= 0 and hi - lo > ecap:
+                ovf[ef] = 1
+            for j in range(lo, hi):
+                if c >= cap:
+                    break
+                if unpack:
+                    x[j] = b2[c]
+                else:
+                    b2[c] = x[int(src_rows[j])]
+                c += 1
+        if sum(off[e + 1] - off[e] for e in experts) > cap and flag >= 0:
+            ovf[flag] = 1
+
+
 XBATCH_MAX_REQ, XBATCH_MAX_GROUPS = 16, 64  # kXbatchMaxReq / kXbatchMaxGroups (kernels.h)
 
 

@@ -265,6 +265,7 @@ class DAGExecutor:
             self.comm.attach(self)  # peers pull from this rank's arenas (IPC exchange across processes)
             if EP_ROUTED:
                 self._plan_routed_edges()
+        self._plan_ep_capacity()
         if autotune and self.gpu:
             _tuning.set_model(self.model_name)
             _tuning.ensure_tuned(self.gemm_shapes(), self.device)
@@ -1193,7 +1194,18 @@ class DAGExecutor:
             route = self._moe_route(r_name, E, top_k)
             src = route[2]
             rw = self._deferred.pop(h_name, None)
-            if rw is not None:  # device transport: pull the local experts' routed rows only
+            cap = self._ep_unpack.get(h_name)
+            if cap is not None and (h_name, cap[0]) in self._ep_full:
+                cap = None
+            if cap is not None:  # capacity edge: the routed rows arrived packed — unpack them
+                H = self.tasks[h_name].op.out_shape[-1]
+                xp = out if out is not None else self._scratch("moe_xp/" + h_name.split("/")[0], (src.numel(), H))
+                peer, experts, rows, erows = cap
+                f = self._ep_groups[(h_name, peer)]
+                ops.moe_pack(xp, src, route[4], [(self._flat(self._x(h_name))[:rows], rows, experts, f,
+                                                  [erows] * len(experts), [f] * len(experts))], self._ep_ovf,
+                             unpack=True)
+            elif rw is not None:  # device transport: pull the local experts' routed rows only
                 H = self.tasks[h_name].op.out_shape[-1]
                 # one buffer per request: another request's experts may run between two of this one's
                 xp = out if out is not None else self._scratch("moe_xp/" + h_name.split("/")[0], (src.numel(), H))
@@ -1547,7 +1559,7 @@ class DAGExecutor:
             ins = self.prog.instrs[k]
             if ins.op == "recv":
                 self._wait_sends(ins)  # the recv buffer may still be read by a send to another peer
-            buf = self._act_region(ins.task) if self._device_p2p else self._views[ins.task]
+            buf = self._act_region(ins.task) if self._device_p2p else self._ep_buf(ins, self._views[ins.task])
             ops_.append((ins.op == "send", buf, ins.peer, ("act", ins.task)))
             idx.append(k)
         t0 = self._mark() if events is not None else None
@@ -1625,27 +1637,18 @@ class DAGExecutor:
         output at its post (the home's own routing), a hidden state right after its router
         logits arrived (``_pull_at``) — so its producer's ack never waits for a later consumer
         (the device analogue of RCCL's completion once both ends posted)."""
-        received = {i.task for i in self.prog.instrs if i.op == "recv"}
+        from .program import device_routed_edges
+
         self._h_route: Dict[str, Tuple[str, int, int]] = {}
-        users: Dict[str, List[Task]] = {}
-        for ins in self.prog.instrs:
-            if ins.op == "run":
-                for tid in ins.group:
-                    for d in self.tasks[tid].dependencies:
-                        users.setdefault(d, []).append(self.tasks[tid])
-        for x in received:
-            us = users.get(x, [])
-            if us and all(u.op is not None and u.op.kind == "moe_expert" and u.op.inputs[0] == x
-                          and u.id not in self._moe_batched_ids for u in us):
-                ex = sorted({u.op.attrs["expert"] for u in us})
-                self._routed_in[x] = torch.tensor(ex, dtype=torch.int32, device=self.device)
-                u = us[0]
-                self._h_route[x] = (u.op.inputs[1], u.op.attrs["n_experts"], u.op.attrs["top_k"])
-            elif us and all(u.op is not None and u.op.kind == "moe_combine" for u in us) \
-                    and self.tasks[x].op is not None and self.tasks[x].op.kind == "moe_expert":
-                self._routed_out.add(x)
-                self._exp_ids[x] = torch.tensor([self.tasks[x].op.attrs["expert"]], dtype=torch.int32,
-                                                device=self.device)
+        routed_in, routed_out = device_routed_edges(self.prog, self.tasks, self._moe_batched_ids)
+        for x, us in routed_in.items():
+            ex = sorted({u.op.attrs["expert"] for u in us})
+            self._routed_in[x] = torch.tensor(ex, dtype=torch.int32, device=self.device)
+            u = us[0]
+            self._h_route[x] = (u.op.inputs[1], u.op.attrs["n_experts"], u.op.attrs["top_k"])
+        for x in routed_out:
+            self._routed_out.add(x)
+            self._exp_ids[x] = torch.tensor([self.tasks[x].op.attrs["expert"]], dtype=torch.int32, device=self.device)
         at: Dict[str, int] = {}  # where each tensor is on this rank: its run, or its receive
         for i, ins in enumerate(self.prog.instrs):
             if ins.op == "run":
@@ -1655,6 +1658,101 @@ class DAGExecutor:
                 at.setdefault(ins.task, i)
         for h, (r, _, _) in self._h_route.items():
             self._pull_at.setdefault(max(at[h], at[r]), []).append(h)
+
+    # ------------------------------------------------- expert-parallel capacity edges (RCCL)
+    def _plan_ep_capacity(self) -> None:
+        """Expert-parallel edges as fixed-capacity messages on the RCCL / hub / gloo transports
+        (program.plan_ep_capacity sets ``Instr.rows``): the home rank packs the rows its routing
+        sends to an expert GPU right after the router runs (ops.moe_pack, inside the step's
+        kernels: no host sync), sends ``rows`` rows; the expert GPU unpacks them into the
+        expert-sorted layout its experts read; an expert's compact output returns in ``erows``
+        rows. A capacity GROUP is one (hidden state, other rank) pair — the hidden edge and its
+        experts' return edges; both of its ranks compute the same counts from the same router
+        logits, so both see an overflow (``ep_overflow``) and widen the same group."""
+        self._ep_groups: Dict[Tuple[str, int], int] = {}  # (tokens tensor, other rank) -> flag index
+        self._ep_full: set = set()                          # widened groups: whole-buffer edges
+        self._ep_msg: Dict[Tuple[str, int], Tuple[int, Tuple[str, int]]] = {}  # (task, peer) -> (rows, group)
+        self._ep_pack_at: Dict[str, List[tuple]] = {}       # router -> [(h, dst, experts, rows, erows)]
+        self._ep_unpack: Dict[str, tuple] = {}              # received h -> (src, experts, rows, erows)
+        self._ep_route: Dict[str, Tuple[str, int, int]] = {}  # h -> (router, E, top-k)
+        self._ep_bufs: Dict[Tuple[str, int], torch.Tensor] = {}
+        self._ep_ovf: Optional[torch.Tensor] = None
+        if self._device_p2p or self.comm is None:
+            return  # (the device transport pulls exactly the routed rows: _plan_routed_edges)
+        for t in self.tasks.values():
+            if t.op is not None and t.op.kind == "moe_expert":
+                self._ep_route.setdefault(t.op.inputs[0], (t.op.inputs[1], t.op.attrs["n_experts"],
+                                                           t.op.attrs["top_k"]))
+        for ins in self.prog.instrs:
+            if ins.op in ("send", "recv") and ins.rows and ins.experts:
+                g = (ins.task, ins.peer)
+                self._ep_groups.setdefault(g, len(self._ep_groups))
+                self._ep_msg[g] = (ins.rows, g)
+                if ins.op == "send":
+                    r = self._ep_route[ins.task][0]
+                    self._ep_pack_at.setdefault(r, []).append((ins.task, ins.peer, ins.experts, ins.rows, ins.erows))
+                else:
+                    self._ep_unpack[ins.task] = (ins.peer, ins.experts, ins.rows, ins.erows)
+        for ins in self.prog.instrs:  # return edges: grouped with their tokens' edge
+            if ins.op in ("send", "recv") and ins.rows and not ins.experts:
+                g = (self.tasks[ins.task].op.inputs[0], ins.peer)
+                if g not in self._ep_groups:
+                    raise RuntimeError(f"rank {self.prog.rank}: capacity edge {ins.task} without its tokens' edge")
+                self._ep_msg[(ins.task, ins.peer)] = (ins.rows, g)
+        if self._ep_groups:
+            self._ep_ovf = torch.zeros(len(self._ep_groups), dtype=torch.int32, device=self.device)
+
+    def _ep_buf(self, ins, buf):
+        """The message of a send / recv: its capacity rows unless its group was widened."""
+        m = self._ep_msg.get((ins.task, ins.peer))
+        if m is None or m[1] in self._ep_full:
+            return buf
+        rows = m[0]
+        if ins.op == "send" and ins.experts:  # packed at the router's run (_ep_pack)
+            return self._ep_bufs[(ins.task, ins.peer)][:rows]
+        return self._flat(buf)[:rows]
+
+    def _ep_pack(self, r: str) -> None:
+        """Right after the router ``r`` ran on the home rank: pack, for every expert GPU with a
+        capacity edge of this layer, the token rows routed to its experts (one launch)."""
+        dests = []
+        for h, dst, experts, rows, erows in self._ep_pack_at[r]:
+            g = (h, dst)
+            if g in self._ep_full:
+                continue
+            buf = self._ep_bufs.get(g)
+            if buf is None:  # (first, eager step: never allocated during capture)
+                H = self.tasks[h].op.out_shape[-1]
+                buf = self._ep_bufs[g] = torch.empty(rows, H, dtype=self.dtype, device=self.device)
+            f = self._ep_groups[g]
+            dests.append((h, (buf, rows, experts, f, [erows] * len(experts), [f] * len(experts))))
+        if not dests:
+            return
+        _, E, K = self._ep_route[dests[0][0]]
+        route = self._moe_route(r, E, K)
+        for h in dict.fromkeys(d[0] for d in dests):
+            ds = [d for hh, d in dests if hh == h]
+            for k in range(0, len(ds), 8):  # kMoePackMaxDest
+                ops.moe_pack(self._flat(self._x(h)), route[2], route[4], ds[k:k + 8], self._ep_ovf)
+
+    def ep_overflow(self) -> List[Tuple[str, int]]:
+        """Capacity groups whose routing exceeded a capacity since the last widening (a host read:
+        synchronises). Those steps' MoE outputs are wrong for the rows that did not fit."""
+        if self._ep_ovf is None:
+            return []
+        flags = self._ep_ovf.tolist()
+        return [g for g, i in self._ep_groups.items() if flags[i] and g not in self._ep_full]
+
+    def widen_ep(self, groups) -> None:
+        """Carry these capacity groups as whole buffers from now on (exact for any routing). The
+        captured graphs bake message sizes in: they are dropped (call ``capture`` again)."""
+        groups = [g for g in groups if g in self._ep_groups]
+        if not groups:
+            return
+        self._ep_full |= set(groups)
+        self._ep_ovf.zero_()
+        self._segments, self._graph, self._graph_exec, self._fast = {}, None, None, None
+        self._drop_runner()
 
     def _pre_run(self, ins, recv_work, events) -> None:
         """What a run must wait for: copy-stream fills and peer receives of its parameter
@@ -1708,6 +1806,10 @@ class DAGExecutor:
             events.append((ins.task, "kernel", t0, self._mark()))
         elif run is not None:
             run(ins)
+        if self._ep_pack_at and run is not None:  # a router whose rows leave through capacity edges
+            for tid in ins.group:
+                if tid in self._ep_pack_at:
+                    self._ep_pack(tid)
 
     def _psend(self, i: int, ins, stats: StepStats) -> None:
         """Send a resident parameter group to a peer that re-fills it from this rank's HBM

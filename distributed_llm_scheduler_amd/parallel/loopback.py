@@ -40,13 +40,16 @@ class LoopbackRun:
     host_us: List[float] = field(default_factory=list)
     # device transport: each rank's error word after the warm-up steps (then cleared)
     warmup_errors: List[int] = field(default_factory=list)
+    # expert-parallel capacity groups each rank widened after an overflow (then ran a step again)
+    ep_widened: List[list] = field(default_factory=list)
 
 
 def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = True, delay_us: float = 20.0,
                  poison: bool = True, store=None, timeout_s: float = 120.0,
                  before_steps: Optional[Callable] = None, cpu_runner: bool = False,
                  sync_debug: bool = False, autotune: bool = False, transport: str = "hub",
-                 single_issue: bool = False, p2p_timeout_s: Optional[float] = None) -> LoopbackRun:
+                 single_issue: bool = False, p2p_timeout_s: Optional[float] = None,
+                 ep_exact: bool = True) -> LoopbackRun:
     """Build one executor per rank of ``plan`` on ``device``, then drive every rank from its own
     thread: ``warmup`` eager steps, capture (segment hipGraphs + native runner for programs with
     p2p), ``steps`` timed steps. ``before_steps(executors)`` may patch the executors first
@@ -59,7 +62,9 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
     pull and ack flags, no host pairing — and each rank's whole step captures into ONE hipGraph;
     ``delay_us`` then delays every notify and ``poison`` fills each receive region with NaN
     when the receive is posted (``p2p_timeout_s``: the host transport's wait limit on the CPU;
-    on the GPU devp2p's DLS_P2P_TIMEOUT_S). ``single_issue`` (captured whole-step graphs only): after
+    on the GPU devp2p's DLS_P2P_TIMEOUT_S). ``ep_exact``: when an expert-parallel capacity edge
+    overflowed in the steps, every rank widens its overflowed groups and the job runs one more
+    step (``ep_widened``), so the outputs are exact. ``single_issue`` (captured whole-step graphs only): after
     warm-up, ONE host thread issues every rank's timed steps round-robin (graph launches are
     asynchronous), so ``host_us`` is the issue cost of a step without GIL contention between
     rank threads. On the CPU the same protocol runs with host waits (devp2p.HostP2PWorld)."""
@@ -71,11 +76,13 @@ def run_loopback(plan, device, steps: int = 3, warmup: int = 2, capture: bool = 
         # rank threads capture: a graph torn down by a finaliser on one rank thread while another
         # is inside a capture aborted the process (parallel/lifetime.py)
         return _run_loopback(plan, device, steps, warmup, capture, delay_us, poison, store, timeout_s,
-                             before_steps, cpu_runner, sync_debug, autotune, transport, single_issue, p2p_timeout_s)
+                             before_steps, cpu_runner, sync_debug, autotune, transport, single_issue, p2p_timeout_s,
+                             ep_exact)
 
 
 def _run_loopback(plan, device, steps, warmup, capture, delay_us, poison, store, timeout_s, before_steps,
-                  cpu_runner, sync_debug, autotune, transport, single_issue, p2p_timeout_s) -> LoopbackRun:
+                  cpu_runner, sync_debug, autotune, transport, single_issue, p2p_timeout_s,
+                  ep_exact) -> LoopbackRun:
     from . import executor as exm
     from . import runtime
 
@@ -238,9 +245,61 @@ def _run_loopback(plan, device, steps, warmup, capture, delay_us, poison, store,
     if real or errors:
         r, e = (real or errors)[0]
         raise RuntimeError(f"loopback harness: rank {r} failed: {e!r}") from e
+    widened = [[] for _ in range(world)]
+    over = [ex.ep_overflow() for ex in exs]
+    # an expert-parallel capacity edge overflowed (its routing sent more rows than it holds):
+    # every rank widens the groups IT saw overflow — both ranks of a group see the same counts —
+    # re-captures, and the whole job runs the step again. A layer's routing depends on the
+    # layers before it, so a corrected step can overflow a later layer: repeat until none does
+    # (at most once per capacity group)
+    rounds = 0
+    while ep_exact and any(over):
+        rounds += 1
+        if rounds > 1 + max(len(ex._ep_groups) for ex in exs):
+            raise RuntimeError("loopback harness: expert capacity overflow persists after widening")
+
+        def again(r, _over=over):
+            if gpu:
+                torch.cuda.set_device(device)
+            with (torch.cuda.stream(streams[r]) if gpu else _Null()):
+                exs[r].widen_ep(_over[r])
+                exs[r].step()  # eager: the widened messages
+                if capture and gpu:
+                    exs[r].capture()
+                stats[r] = exs[r].step()
+
+        _on_ranks(world, again, timeout_s, "re-running a step with widened expert edges")
+        if gpu:
+            torch.cuda.synchronize(device)
+        for r in range(world):
+            widened[r] += over[r]
+        over = [ex.ep_overflow() for ex in exs]
     hub = getattr(groups[0], "hub", None)
     issue = [ex.issue_mode or ("graph" if ex._graph is not None else None) for ex in exs]
-    return LoopbackRun(exs, stats, hub, issue, ms, host_us=host_us, warmup_errors=warm_err)
+    return LoopbackRun(exs, stats, hub, issue, ms, host_us=host_us, warmup_errors=warm_err,
+                       ep_widened=[list(w) for w in widened])
+
+
+def _on_ranks(world: int, fn, timeout_s: float, what: str) -> None:
+    """Run fn(rank) on one thread per rank (their p2p ops pair up) and re-raise a rank's error."""
+    errors = []
+
+    def wrap(r):
+        try:
+            fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errors.append((r, e))
+
+    threads = [threading.Thread(target=wrap, args=(r,), daemon=True) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout_s * 2)
+    if any(t.is_alive() for t in threads):
+        raise RuntimeError(f"loopback harness: a rank thread did not finish {what}")
+    if errors:
+        r, e = errors[0]
+        raise RuntimeError(f"loopback harness: rank {r} failed {what}: {e!r}") from e
 
 
 _RAW_STREAMS: dict = {}

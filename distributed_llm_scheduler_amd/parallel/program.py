@@ -22,6 +22,7 @@ at run time, so a rank's whole program is hipGraph-capturable.
 """
 from __future__ import annotations
 
+import math
 import os
 from collections import defaultdict
 from dataclasses import dataclass, field
@@ -54,6 +55,14 @@ class Instr:
     # run/recv: indices of earlier ``send`` instructions whose buffer this instruction's
     # output region overlaps — they must complete before it writes (see _plan_send_waits)
     wait_sends: Tuple[int, ...] = ()
+    # send/recv of an expert-parallel capacity edge (plan_ep_capacity): the message is the first
+    # ``rows`` rows of the tensor (routed token rows packed by the sender, or an expert's compact
+    # output rows) instead of the whole buffer; 0 = the whole buffer
+    rows: int = 0
+    # a routed hidden state's capacity edge: the experts on the expert GPU its rows are routed to,
+    # and the capacity of those experts' compact outputs coming back (their return edges)
+    experts: Tuple[int, ...] = ()
+    erows: int = 0
 
 
 @dataclass
@@ -351,6 +360,8 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 prog.param_offset[(len(ins) - 1, pid)] = off
         for x in ins[n0:]:
             x.gpos = len(order)
+        if EP_CAPACITY > 0:
+            plan_ep_capacity(prog, rank, tmap, placement, consumers, EP_CAPACITY)
         prog.param_peak_bytes = par.peak
         prog.param_arena_bytes = extent
         sinks = {t for t in order if not consumers.get(t)}
@@ -364,6 +375,181 @@ def build_programs(tasks: Sequence[Task], placement: Dict[str, int], order: Sequ
                 "does not need; raise the cap or use a policy that places fewer parameters on this rank")
         programs.append(prog)
     return programs
+
+
+# Expert-parallel edges on the default (RCCL) transport: a hidden state sent to an expert GPU
+# carries the token rows routed to that GPU's experts, packed by the sender into a buffer of
+# ceil(EP_CAPACITY * M * k * n / E) rows (n experts there), and an expert's compact output goes back
+# in an edge of ceil(EP_CAPACITY * M * k / E) rows — fixed-size messages (an RCCL receive must know
+# its size when it is posted; the routing lives on the device), ~EP_CAPACITY x the routed bytes
+# instead of M rows each. A layer whose routing overflows a capacity is detected on the device
+# (DAGExecutor.ep_overflow) and that edge widened to the whole buffer. DLS_EP_CAPACITY=0: whole
+# buffers always (the round-5 edges).
+EP_CAPACITY = float(os.environ.get("DLS_EP_CAPACITY", "1.25"))
+EP_ROWS_ALIGN = 8
+
+
+def ep_capacity_rows(M: int, k: int, n_exp: int, E: int, factor: float) -> int:
+    """Rows of a capacity edge to n_exp of E experts: factor x the expected routed rows M*k*n/E,
+    at most every row a routing can send there (a token counts once per expert it picks)."""
+    rows = math.ceil(factor * M * k * n_exp / E / EP_ROWS_ALIGN) * EP_ROWS_ALIGN
+    return max(EP_ROWS_ALIGN, min(M * min(k, n_exp), rows))
+
+
+def ep_routed_in(h: str, dst: int, tmap: Dict[str, Task], placement: Dict[str, int],
+                 consumers: Dict[str, List[str]]) -> Optional[List[Task]]:
+    """The expert nodes on ``dst`` that read ``h`` as their tokens, if they are h's only consumers
+    there (the edge h -> dst then carries routed rows only), else None."""
+    us = [tmap[c] for c in consumers.get(h, []) if placement.get(c) == dst]
+    if us and all(u.op is not None and u.op.kind == "moe_expert" and u.op.inputs[0] == h for u in us):
+        return us
+    return None
+
+
+def ep_routed_out(x: str, dst: int, tmap: Dict[str, Task], placement: Dict[str, int],
+                  consumers: Dict[str, List[str]]) -> bool:
+    """An expert's output whose consumers on ``dst`` are all MoE combines (compact rows)."""
+    t = tmap[x]
+    us = [tmap[c] for c in consumers.get(x, []) if placement.get(c) == dst]
+    return bool(us) and t.op is not None and t.op.kind == "moe_expert" and all(
+        u.op is not None and u.op.kind == "moe_combine" for u in us)
+
+
+def _ep_hidden_rows(h: str, src: int, dst: int, tmap, placement, consumers, factor: float):
+    """(rows, experts, router) of the capacity edge h: src -> dst, or None when that edge stays a
+    whole buffer: its consumers there are not all experts reading h as tokens, their routing is
+    not computed on src, or the capacity would not be smaller than the buffer (several experts
+    on one GPU count a token once per expert it picks)."""
+    us = ep_routed_in(h, dst, tmap, placement, consumers)
+    t = tmap[h]
+    if not us or t.op is None or not t.op.out_shape:
+        return None
+    r = us[0].op.inputs[1]
+    if placement.get(r) != src or any(u.op.inputs[1] != r for u in us):
+        return None
+    M = math.prod(t.op.out_shape[:-1])
+    a = us[0].op.attrs
+    experts = tuple(sorted({u.op.attrs["expert"] for u in us}))
+    rows = ep_capacity_rows(M, a["top_k"], len(experts), a["n_experts"], factor)
+    if rows >= M:
+        return None
+    return rows, experts, r, ep_capacity_rows(M, a["top_k"], 1, a["n_experts"], factor)
+
+
+def plan_ep_capacity(prog: Program, rank: int, tmap: Dict[str, Task], placement: Dict[str, int],
+                     consumers: Dict[str, List[str]], factor: float) -> int:
+    """Turn this rank's expert-parallel edges into capacity edges (``Instr.rows``) and move each
+    routed hidden state's send / receive right after the router logits' send / receive between
+    the same two ranks — the sender packs the rows once its routing exists, and both ends post
+    in the same order (RCCL pairs a rank pair's messages by posting order). An expert's output
+    going back is a capacity edge exactly when its tokens came through one. Returns the number
+    of capacity edges. Parameter-load indices (``param_offset``) follow the moves."""
+    ins = prog.instrs
+    moves: Dict[int, Tuple[str, str]] = {}  # instruction -> (op, router task) it is posted after
+    n = 0
+    for i, x in enumerate(ins):
+        if x.op not in ("send", "recv"):
+            continue
+        src, dst = (rank, x.peer) if x.op == "send" else (x.peer, rank)
+        hid = _ep_hidden_rows(x.task, src, dst, tmap, placement, consumers, factor)
+        if hid is not None:
+            x.rows, x.experts, r, x.erows = hid
+            moves[i] = (x.op, r)
+            n += 1
+            continue
+        t = tmap[x.task]
+        if ep_routed_out(x.task, dst, tmap, placement, consumers):
+            h = t.op.inputs[0]
+            if placement.get(h) != dst:
+                continue
+            back = _ep_hidden_rows(h, dst, src, tmap, placement, consumers, factor)  # its tokens' edge
+            if back is not None and t.op.attrs["expert"] in back[1]:
+                x.rows = back[3]
+                n += 1
+    if not moves:
+        return n
+    order = [i for i in range(len(ins)) if i not in moves]
+    for i, (op, r) in sorted(moves.items()):
+        peer = ins[i].peer
+        anchor = next((k for k, j in enumerate(order) if ins[j].op == op and ins[j].task == r and ins[j].peer == peer),
+                      None)
+        if anchor is None:
+            raise RuntimeError(f"rank {rank}: routed edge {ins[i].task} has no {op} of its router {r} to follow")
+        # after the router's message and any routed states already placed behind it
+        k = anchor + 1
+        while k < len(order) and order[k] in moves and moves[order[k]] == (op, r) and ins[order[k]].peer == peer:
+            k += 1
+        order.insert(k, i)
+        ins[i].gpos = ins[order[anchor]].gpos
+    new_index = {old: new for new, old in enumerate(order)}
+    prog.instrs = [ins[j] for j in order]
+    prog.param_offset = {(new_index[i], pid): off for (i, pid), off in prog.param_offset.items()}
+    return n
+
+
+def moe_batched_ids(prog: Program, tmap: Dict[str, Task]) -> set:
+    """Expert nodes that run as ONE grouped launch pair per MoE layer (DAGExecutor._plan_moe_batches
+    on the GPU): every expert of a layer back to back on this rank (only parameter loads between
+    them), in a program without evictions or peer parameter loads."""
+    ins = prog.instrs
+    out: set = set()
+    if any(i.op == "evict" or (i.op == "load" and i.peer >= 0) for i in ins):
+        return out
+
+    def expert_of(j):
+        x = ins[j]
+        if x.op != "run" or len(x.group) != 1:
+            return None
+        t = tmap[x.group[0]]
+        return t if t.op is not None and t.op.kind == "moe_expert" else None
+
+    i = 0
+    while i < len(ins):
+        t0 = expert_of(i)
+        if t0 is None:
+            i += 1
+            continue
+        key = tuple(t0.op.inputs[:2])
+        members, j = [i], i + 1
+        while j < len(ins):
+            t = expert_of(j)
+            if ins[j].op == "load":
+                pass
+            elif t is not None and tuple(t.op.inputs[:2]) == key:
+                members.append(j)
+            else:
+                break
+            j += 1
+        experts = sorted(tmap[ins[m].group[0]].op.attrs["expert"] for m in members)
+        if len(members) > 1 and experts == list(range(t0.op.attrs["n_experts"])):
+            out |= {ins[m].group[0] for m in members}
+        i = j
+    return out
+
+
+def device_routed_edges(prog: Program, tmap: Dict[str, Task], batched: set = frozenset()):
+    """The device transport's routed receives on this rank (DAGExecutor._plan_routed_edges and
+    validate.device_deadlock_check share this rule): {hidden state: its local expert nodes} for a
+    received hidden state whose every local consumer is an expert reading it as its tokens and
+    not part of a whole-layer batch (``batched``), and the received expert outputs whose every
+    local consumer is a MoE combine."""
+    users: Dict[str, List[Task]] = defaultdict(list)
+    for ins in prog.instrs:
+        if ins.op == "run":
+            for tid in ins.group:
+                for d in tmap[tid].dependencies:
+                    users[d].append(tmap[tid])
+    routed_in: Dict[str, List[Task]] = {}
+    routed_out: set = set()
+    for x in {i.task for i in prog.instrs if i.op == "recv"}:
+        us = users.get(x, [])
+        if us and all(u.op is not None and u.op.kind == "moe_expert" and u.op.inputs[0] == x
+                      and u.id not in batched for u in us):
+            routed_in[x] = us
+        elif us and all(u.op is not None and u.op.kind == "moe_combine" for u in us) \
+                and tmap[x].op is not None and tmap[x].op.kind == "moe_expert":
+            routed_out.add(x)
+    return routed_in, routed_out
 
 
 def _group_kind(tmap: Dict[str, Task], grp: Tuple[str, ...]) -> str:

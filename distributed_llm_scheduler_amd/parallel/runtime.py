@@ -7,6 +7,7 @@ lowering are pure functions of their arguments.
 from __future__ import annotations
 
 import json
+import math
 import os
 from collections import defaultdict
 from dataclasses import dataclass, field
@@ -443,8 +444,26 @@ def plan_stats(p: Plan) -> Dict:
         # what the same transfers move when expert-parallel edges carry routed rows only (the
         # device transport, DAGExecutor._plan_routed_edges): expected M*k/E rows per expert
         "cross_gpu_bytes_routed": _routed_cross_bytes(p, tmap),
+        # what the programs' p2p sends move per step on the RCCL transport: whole buffers, except
+        # expert-parallel capacity edges (program.plan_ep_capacity: EP_CAPACITY x the expected
+        # routed rows, fixed-size messages)
+        "cross_gpu_bytes_rccl": _rccl_send_bytes(p, tmap),
         **_steady_stats(p.scheduler),
     }
+
+
+def _rccl_send_bytes(p: Plan, tmap) -> int:
+    total = 0
+    for pr in p.programs:
+        for i in pr.instrs:
+            if i.op != "send":
+                continue
+            t = tmap[i.task]
+            if i.rows and t.op is not None and t.op.out_shape:
+                total += int(t.xfer_bytes * i.rows / math.prod(t.op.out_shape[:-1]))
+            else:
+                total += t.xfer_bytes
+    return total
 
 
 def _routed_cross_bytes(p: Plan, tmap) -> int:
@@ -479,6 +498,32 @@ def _steady_stats(s) -> Dict:
             "modelled_cold_period_ms": round(s.cold_period * 1e3, 4),
             "stages": [{"node": st["node"], "busy_ms": round(st["busy_s"] * 1e3, 4),
                         "refill_gb": round(st["refill_gb"], 6)} for st in s.stages]}
+
+
+def torch_device_type(device) -> str:
+    import torch
+
+    return torch.device(device).type
+
+
+def ep_widen_on_overflow(ex, pg=None) -> bool:
+    """After a step of an expert-parallel job (one process per rank): did any rank's capacity
+    edge overflow? (one all-reduce; a host read of this rank's flags). If so every rank widens
+    the groups IT saw overflow (both ranks of a group see the same routing counts) and the
+    caller re-runs the step — and re-captures, if it captured — then calls this again: a
+    corrected layer can change a later layer's routing, so repeat until it returns False."""
+    import torch
+    import torch.distributed as dist
+
+    mine = ex.ep_overflow()
+    flag = torch.tensor([1 if mine else 0], dtype=torch.int32,
+                        device=ex.device if (ex.gpu and pg is not None and dist.get_backend(pg) == "nccl") else "cpu")
+    if pg is not None:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=pg)
+    if not int(flag.item()):
+        return False
+    ex.widen_ep(mine)
+    return True
 
 
 def make_store(p: Plan, seed: int = 0, device_init: bool = False) -> ParamStore:
@@ -521,7 +566,9 @@ def make_executor(p: Plan, rank: int, device, store: Optional[ParamStore] = None
     if debug:
         from .validate import check_plan
 
-        errs = check_plan(p)
+        dev = torch_device_type(device) == "cuda"
+        transport = getattr(pg, "world", None) is not None and type(pg).__name__ in ("DeviceP2PGroup", "HostP2PGroup")
+        errs = check_plan(p, device=transport, gpu=dev)
         if errs:
             raise RuntimeError("invalid plan:\n  " + "\n  ".join(errs[:20]))
     # per-model GEMM choices by the canonical preset name (aliases such as "mixtral" resolve to it)

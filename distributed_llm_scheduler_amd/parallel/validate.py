@@ -213,7 +213,7 @@ def _deadlock_check(programs: Sequence[Program]) -> List[str]:
 
 
 def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], eager: bool = True,
-                          batched: bool = False) -> List[str]:
+                          batched: bool = False, gpu: bool = True, routed: bool = True) -> List[str]:
     """Deadlock freedom under the DEVICE transport's progress rules (parallel/devp2p.py), which
     differ from RCCL's: a send completes when the consumer has PULLED it (its ack), not when the
     receive was posted, and an expert-parallel receive is pulled only once the device-side routing
@@ -225,7 +225,13 @@ def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], ea
     transport did before; a layer-major expert-parallel plan deadlocks under it). ``batched``
     models one wait for ALL of a program point's flags before any of its copies — fewer graph
     nodes, but an ack then waits for flags of other producers, and the 4-rank config-5 plan
-    deadlocks under it: the executor pulls each receive after its own flag only."""
+    deadlocks under it: the executor pulls each receive after its own flag only. ``gpu`` /
+    ``routed``: the executor's conditions for routed pulls (a whole-layer expert batch on the
+    GPU pulls its tokens whole; DLS_EP_ROUTED=0 pulls everything whole at its post) — the rule
+    itself is program.device_routed_edges, shared with the executor."""
+    from .executor import MOE_BATCH
+    from .program import device_routed_edges, moe_batched_ids
+
     tmap = {t.id: t for t in tasks}
     acts: List[List[Tuple[str, tuple, int]]] = []
     for prog in programs:
@@ -242,14 +248,11 @@ def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], ea
                 at.setdefault(ins.task, i)
         pull_at: Dict[int, List[str]] = defaultdict(list)
         out_rows = set()
-        for ins in prog.instrs:
-            if ins.op != "recv":
-                continue
-            us = users.get(ins.task, [])
-            if us and all(u.op is not None and u.op.kind == "moe_expert" and u.op.inputs[0] == ins.task for u in us):
-                pull_at[max(at[ins.task], at.get(us[0].op.inputs[1], 0))].append(ins.task)
-            elif us and all(u.op is not None and u.op.kind == "moe_combine" for u in us):
-                out_rows.add(ins.task)
+        if routed:
+            bat = moe_batched_ids(prog, tmap) if (gpu and MOE_BATCH) else set()
+            routed_in, out_rows = device_routed_edges(prog, tmap, bat)
+            for x, us in routed_in.items():
+                pull_at[max(at[x], at.get(us[0].op.inputs[1], 0))].append(x)
         if not eager:  # every routed receive pulled right before its first consumer runs
             first = {x: min(at[u.id] for u in users[x]) for v in pull_at.values() for x in v}
             first.update({x: min(at[u.id] for u in users[x]) for x in out_rows})
@@ -342,9 +345,12 @@ def device_deadlock_check(tasks: Sequence[Task], programs: Sequence[Program], ea
     return [f"device transport deadlock: ranks blocked at {stuck[:4]}"] if stuck else []
 
 
-def check_plan(p, device: bool = True) -> List[str]:
-    """validate_programs on a runtime.Plan (plus the device transport's progress rules)."""
+def check_plan(p, device: bool = False, gpu: bool = True) -> List[str]:
+    """validate_programs on a runtime.Plan; ``device``: plus the device transport's progress
+    rules (for a plan that will run on that transport)."""
     errs = validate_programs(p.tasks, p.programs, p.param_bytes)
     if not errs and device:
-        errs = device_deadlock_check(p.tasks, p.programs)
+        from .executor import EP_ROUTED
+
+        errs = device_deadlock_check(p.tasks, p.programs, gpu=gpu, routed=EP_ROUTED)
     return errs

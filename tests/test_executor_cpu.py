@@ -444,12 +444,26 @@ def _ep_fixed_worker(rank, world, port, q, seq):
         ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
         for _ in range(2):
             st = ex.step()
+        widened = 0
+        while runtime.ep_widen_on_overflow(ex, dist.group.WORLD):  # capacity edges that overflowed
+            widened += 1
+            ex.step()
         runner = ex.build_runner()  # an expert-parallel program replays from the native runner
         for _ in range(2):
             st = ex.step()
-        edges = [(i.op, i.task) for i in p.programs[rank].instrs if i.op in ("send", "recv")]
+        assert not runtime.ep_widen_on_overflow(ex, dist.group.WORLD)
+        tm = {t.id: t for t in p.tasks}
+        wide = ex._ep_full
+
+        def msg_bytes(i):
+            grp = (i.task if i.experts else tm[i.task].op.inputs[0], i.peer)
+            M = tm[i.task].out_bytes // (2 * tm[i.task].op.out_shape[-1])
+            return i.rows * tm[i.task].out_bytes // M if i.rows and grp not in wide else tm[i.task].out_bytes
+
+        edges = [(i.op, i.task, msg_bytes(i)) for i in p.programs[rank].instrs if i.op in ("send", "recv")]
         res = {"rank": rank, "bytes_sent": st.bytes_sent, "bytes_recv": st.bytes_recv, "errs": [],
-               "edges": edges, "runner": runner, "issue_mode": ex.issue_mode,
+               "edges": edges, "runner": runner, "issue_mode": ex.issue_mode, "widened": widened,
+               "capacity": sum(1 for i in p.programs[rank].instrs if i.rows),
                "experts": sorted(p.placement[t.id] for t in p.tasks if t.op.kind == "moe_expert"),
                "out_bytes": {t.id: t.out_bytes for t in p.tasks}}
         if p.placement.get("output_projection") == rank:
@@ -464,9 +478,11 @@ def _ep_fixed_worker(rank, world, port, q, seq):
 def test_expert_parallel_fixed_size_edges(world):
     """Expert parallelism over 2 / 4 gloo ranks (expert e on rank e % N, the rest of the layer on
     rank 0), replayed by the native step runner: the output matches the fp32 reference, and every
-    edge moves a FIXED-size buffer known when the program is built — the normed hidden state and
-    the router logits out to each expert rank, each expert's compact output buffer back — so no
-    transfer needs routing counts on the host (each expert rank routes locally from the logits)."""
+    edge moves a FIXED-size message known when the program is built — the router logits and the
+    hidden state's routed rows packed into a capacity buffer (1.25x the expected rows; the whole
+    buffer where that is no smaller, or after an overflow widened the group) out to each expert
+    rank, each expert's compact output rows back — so no transfer needs routing counts on the
+    host (each expert rank routes locally from the logits)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -483,10 +499,11 @@ def test_expert_parallel_fixed_size_edges(world):
     assert len(set(res[0]["experts"])) == min(world, 8)
     for r in res:
         assert r["runner"] and r["issue_mode"] == "runner"
-        ob = r["out_bytes"]
-        assert r["bytes_sent"] == sum(ob[t] for op, t in r["edges"] if op == "send")
-        assert r["bytes_recv"] == sum(ob[t] for op, t in r["edges"] if op == "recv")
-        assert any("expert" in t for _, t in r["edges"]) or r["rank"] == 0
+        assert r["bytes_sent"] == sum(b for op, _, b in r["edges"] if op == "send")
+        assert r["bytes_recv"] == sum(b for op, _, b in r["edges"] if op == "recv")
+        assert any("expert" in t for _, t, _ in r["edges"]) or r["rank"] == 0
+    if world == 4:  # one expert per rank: the expert edges are capacity messages
+        assert all(r["capacity"] > 0 for r in res)
 
 
 def _runner_worker(rank, world, port, q, model, kw):
@@ -570,6 +587,8 @@ def _ep_dp_worker(rank, world, port, q, seq, max_req=None):
         store = runtime.make_store(p)
         ex = runtime.make_executor(p, rank, "cpu", store, pg=dist.group.WORLD)
         for _ in range(2):
+            ex.step()
+        while runtime.ep_widen_on_overflow(ex, dist.group.WORLD):  # capacity edges that overflowed
             ex.step()
         runner = ex.build_runner()
         for _ in range(2):

@@ -358,3 +358,88 @@ def test_loopback_gpu_device_expert_routed_rows(world, monkeypatch):
         moved[routed] = sum(ex.comm.bytes_pulled() for ex in run.executors)
         _check(p, run, store, ids, 0.03)
     assert 0 < moved[True] < 0.6 * moved[False], moved
+
+
+# ------------------------------------------- expert-parallel capacity edges (the RCCL transport)
+def test_expert_capacity_edges_planned():
+    """BASELINE config 5 (Mixtral-8x7B, 8 requests, DP attention + expert parallelism over 8 GPUs):
+    on the RCCL transport the expert edges are capacity messages — ~1.25x the routed rows instead
+    of whole [M, H] buffers (round 5: 15.0 GB per step, 4.0x the routed 3.77 GB)."""
+    p = runtime.plan("mixtral-8x7b", world=8, seq=512, placement="expert", replicas=8)
+    st = p.stats
+    assert st["cross_gpu_bytes_rccl"] <= 1.3 * st["cross_gpu_bytes_routed"], st
+    assert st["cross_gpu_bytes"] >= 3.9 * st["cross_gpu_bytes_routed"]  # what whole buffers would move
+    caps = [i for pr in p.programs for i in pr.instrs if i.rows]
+    assert caps and all(i.rows == 160 for i in caps)  # 1.25 x 512 x 2 / 8 rows per expert GPU
+
+
+@pytest.mark.parametrize("case", ["expert", "expert_dp"])
+@pytest.mark.parametrize("cpu_runner", [False, True])
+def test_loopback_cpu_expert_capacity_edges(case, cpu_runner):
+    """Capacity edges at 4 ranks (one expert per rank, M = 64 rows): every expert edge moves its
+    capacity rows (not the [M, H] buffer), the home packs and the expert rank unpacks on the
+    device-side routing, and the logits match fp32. (A tiny random router is unbalanced enough
+    that some groups overflow 1.25x: those are widened — on both of their ranks — and the step
+    re-run; the rest stay capacity edges.)"""
+    p, ids = _plan(case, 4, 64)
+    caps = {(pr.rank, i.op, i.task, i.peer): i.rows for pr in p.programs for i in pr.instrs if i.rows}
+    assert caps and all(r < 64 for r in caps.values())
+    store = runtime.make_store(p)
+    run = run_loopback(p, "cpu", steps=2, warmup=1, store=store, cpu_runner=cpu_runner)
+    tm = {t.id: t for t in p.tasks}
+    kept = 0
+    for r, st in enumerate(run.stats):
+        wide = set(run.ep_widened[r])
+        sent = 0
+        for i in p.programs[r].instrs:
+            if i.op != "send":
+                continue
+            grp = (i.task if i.experts else tm[i.task].op.inputs[0], i.peer)
+            if i.rows and grp not in wide:
+                sent += i.rows * tm[i.task].xfer_bytes // 64
+                kept += 1
+            else:
+                sent += tm[i.task].xfer_bytes
+        assert st.bytes_sent == sent, (r, st.bytes_sent, sent)
+    assert kept > 0, "every capacity edge was widened"
+    _check(p, run, store, ids, 0.03)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_loopback_cpu_expert_capacity_overflow_is_exact(world, monkeypatch):
+    """Forced overflow: capacities at 0.3x the expected routed rows. The pack / unpack launches
+    flag the overflowed groups on both of their ranks, every rank widens them, the job runs the
+    step again with whole-buffer edges there, and the logits match fp32 exactly as without
+    capacity edges."""
+    from distributed_llm_scheduler_amd.parallel import program
+
+    monkeypatch.setattr(program, "EP_CAPACITY", 0.3)
+    p, ids = _plan("expert_dp", world, 64)
+    assert any(i.rows for pr in p.programs for i in pr.instrs)
+    store = runtime.make_store(p)
+    run = run_loopback(p, "cpu", steps=1, warmup=1, store=store)
+    assert any(run.ep_widened), "0.3x capacities must overflow"
+    # a group is widened on both of its ranks
+    pairs = {(h, r, peer) for r, ws in enumerate(run.ep_widened) for h, peer in ws}
+    assert all((h, peer, r) in pairs for h, r, peer in pairs), pairs
+    _check(p, run, store, ids, 0.03)
+
+
+@gpu
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("factor", [1.25, 0.3])
+def test_loopback_gpu_expert_capacity_edges(factor, monkeypatch):
+    """Config 5's edges on one MI355X (4 ranks, hub transport = RCCL's p2p semantics, segment
+    hipGraphs + native runner, NaN-poisoned receives): capacity messages packed / unpacked by
+    the device routing; at 0.3x forced overflow the groups are widened on both ranks and the
+    step re-run — the logits match fp32 either way."""
+    from distributed_llm_scheduler_amd.parallel import program
+
+    monkeypatch.setattr(program, "EP_CAPACITY", factor)
+    p, ids = _gpu_plan("expert_dp", 4)
+    assert any(i.rows for pr in p.programs for i in pr.instrs)
+    store = runtime.make_store(p)
+    run = run_loopback(p, "cuda:0", steps=3, warmup=2, store=store, delay_us=50.0)
+    if factor < 1:
+        assert any(run.ep_widened)
+    _check(p, run, store, ids, 0.03)
