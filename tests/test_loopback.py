@@ -443,3 +443,33 @@ def test_loopback_gpu_expert_capacity_edges(factor, monkeypatch):
     if factor < 1:
         assert any(run.ep_widened)
     _check(p, run, store, ids, 0.03)
+
+
+# BASELINE configs 3-5 at FULL width through the one-GPU harness (the loopback GPU
+# coverage was mini-scale only): one request DAG of GPT-2-medium over 2 ranks under the 8 GB
+# reference-cost cap (MRU_spec and EFT: evictions, refills, p2p edges), one full-width Llama-3-8B
+# layer tensor-parallel over 2 ranks, one full-width Mixtral-8x7B layer with data-parallel
+# attention + expert parallelism over 4 ranks (capacity edges at M = 512). Logits vs fp32.
+FULL = {
+    "gpt2m_cap_mru": ("gpt2-medium", 2, dict(scheduler="MRU_spec", cap_gb=8.0, replicas=1, cost_model="reference"),
+                      ["output_projection"]),
+    "gpt2m_cap_eft": ("gpt2-medium", 2, dict(scheduler="EFT", cap_gb=8.0, replicas=1, cost_model="reference"),
+                      ["output_projection"]),
+    "llama_1l_tp2": ("llama3-8b-1l", 2, dict(placement="tensor", tp=2), ["output_projection"]),
+    "mixtral_1l_expert_dp4": ("mixtral-8x7b-1l", 4, dict(placement="expert", replicas=4), "replicas"),
+}
+
+
+@gpu
+@pytest.mark.timeout(280)
+@pytest.mark.parametrize("case", sorted(FULL))
+def test_loopback_gpu_full_width_configs(case):
+    model, world, kw, ids = FULL[case]
+    p = runtime.plan(model, world=world, seq=512, batch=1, **kw)
+    assert p.completed == p.total and _p2p_work(p) > 0
+    if ids == "replicas":
+        ids = [f"r{k}/output_projection" for k in range(world)]
+        assert any(i.rows for pr in p.programs for i in pr.instrs)  # capacity edges at full width
+    store = runtime.make_store(p)
+    run = run_loopback(p, "cuda:0", steps=2, warmup=2, store=store, delay_us=20.0, autotune=False)
+    _check(p, run, store, ids, 0.03)
