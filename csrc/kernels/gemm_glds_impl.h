@@ -973,11 +973,30 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
     // its column panel with expert g's weight; consecutive blocks share an expert (its rows
     // stay L2-resident while its weight panels stream)
     // (w_stream bit 8: groups sharing weights — panel-major, the panel's groups on one XCD)
-    int g = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    // (w_stream bit 16: row-split PAIRS — blocks b and b + 8 of each 16 sit on the same XCD and
+    // start together; the pair splits (g, tn)'s row tiles even / odd, so an expert with more routed
+    // rows than one tile streams its weight panel from HBM once, the partner's copy from the L2,
+    // instead of a second serial pass re-streaming it: profiles/r6_mixtral/rows_vs_time.txt. The
+    // odd partner of an expert that fits one tile exits at once)
+    int g = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n, t0 = 0, dt = 1;
     if (ep.w_stream & 8) {
       const int L = xcd_remap(blockIdx.x, gridDim.x), ng = gridDim.x / tiles_n;
       tn = L / ng;
       g = L % ng;
+    } else if (ep.w_stream & 16) {
+      const int pair = (blockIdx.x >> 4) * 8 + (blockIdx.x & 7);
+      if (pair >= tiles_m * tiles_n) return;  // grid rounded up to whole 16-block groups
+      g = pair / tiles_n;
+      tn = pair % tiles_n;
+      t0 = (blockIdx.x >> 3) & 1;
+      dt = 2;
+    } else if (ep.w_stream & 32) {
+      // (the odd partners as a second half of the grid: dispatched after every even block)
+      const int half = gridDim.x >> 1;
+      t0 = blockIdx.x >= half;
+      dt = 2;
+      g = (blockIdx.x - t0 * half) / tiles_n;
+      tn = (blockIdx.x - t0 * half) % tiles_n;
     }
     const int r0 = rows[g], cnt = rows[g + 1] - r0;
     const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
@@ -990,8 +1009,8 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
     const int* ag = a_rows ? a_rows + r0 : nullptr;
     const bf16* Ag = a_rows ? A : A + (size_t)r0 * lda;
 #define DLS_GROUPED_WALK(GA)                                                                                      \
-  for (int t = 0; t * C::BM < Mr; ++t) {                                                                           \
-    if (t) raw_barrier(); /* every wave is done reading the staging buffers of the previous tile */                \
+  for (int t = t0; t * C::BM < Mr; t += dt) {                                                                      \
+    if (t != t0) raw_barrier(); /* every wave is done reading the staging buffers of the previous tile */          \
     if (C::BXS > 0 && (ep.w_stream & 1))                                                                           \
       glds_tile<C, 0, kPolStream, true, GA>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K, \
                                             act, alpha, 0, K, t, tn, ln_colsum, 0, ln_eps, ep, ag);                \
@@ -1255,13 +1274,23 @@ void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned
   }();
   // (the nt path DMAs the A rows by buffer loads with 32-bit offsets: an A of 2 GB or more
   // takes the default path)
+  // row-split pairs (kernel: RANGED == 3): DLS_EXPERT_PAIRS=1 same-XCD partners, 2 partners in a
+  // second half of the grid; 0 (default) walks every row tile in one block
+  // (read per launch — a captured step replays without it — so a test can switch modes)
+  const char* pe = std::getenv("DLS_EXPERT_PAIRS");
+  const int pairs = pe && *pe ? std::atoi(pe) : 0;
+  const int pair = a.grouped_shared ? 0 : pairs;
   const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs,
-               a.grouped_shared ? 8 : ((size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0)};
+               (a.grouped_shared ? 8 : ((size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0)) |
+                   (pair == 1 ? 16 : pair == 2 ? 32 : 0)};
   const int tiles_n = (a.N + C::BN - 1) / C::BN;
-  hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(n_groups * tiles_n), dim3(C::T), 0, s, (const bf16*)a.A,
-                     a.lda, nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0,
-                     const_cast<float*>(reinterpret_cast<const float*>(a_rows)), a.M, a.N, a.K, a.act,
-                     a.alpha, 1, tiles_n, 1, a.K, nullptr, 0, 1e-5f, offsets, a.compact_rows, ep);
+  const int blocks = pair == 1 ? (n_groups * tiles_n + 7) / 8 * 16 : pair == 2 ? 2 * n_groups * tiles_n
+                                                                                : n_groups * tiles_n;
+  // (tiles_m carries the group count: the paired walk bounds its pair index by it)
+  hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(blocks), dim3(C::T), 0, s, (const bf16*)a.A, a.lda,
+                     nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0,
+                     const_cast<float*>(reinterpret_cast<const float*>(a_rows)), a.M, a.N, a.K, a.act, a.alpha,
+                     n_groups, tiles_n, 1, a.K, nullptr, 0, 1e-5f, offsets, a.compact_rows, ep);
 }
 
 }  // namespace

@@ -337,6 +337,41 @@ def test_gemm_grouped_experts(config):
         assert (outs[e][min(r1 - r0, cap):].cpu().float() == 7.0).all(), "rows past the expert's count were written"
 
 
+@pytest.mark.parametrize("pairs", ["0", "1", "2"])
+@pytest.mark.parametrize("config", [-1, 17, 31, 33, 41, 44, 46])
+def test_gemm_grouped_heavy_expert(config, pairs, monkeypatch):
+    """Experts with several row tiles (450 rows: three 160-row tiles, three 192-row tiles, eight
+    64-row tiles) next to tiny and empty ones: the row-split pairs of a grouped launch (even row
+    tiles in one block, odd in its same-XCD partner) cover every row exactly once — against
+    per-expert fp32 references, untouched rows past the last expert. DLS_EXPERT_PAIRS: 0 one
+    block walks all of (expert, column panel)'s row tiles, 1 same-XCD partner blocks, 2 partners
+    in the grid's second half."""
+    monkeypatch.setenv("DLS_EXPERT_PAIRS", pairs)
+    H, F = 256, 384
+    counts = [20, 450, 0, 200, 7, 161]
+    E, R = len(counts), sum(counts) + 16
+    off = torch.tensor([0] + list(torch.tensor(counts).cumsum(0)), dtype=torch.int32, device=DEV)
+    x = _rand(R, H, seed=190)
+    w13 = [ops.interleave_gate_up(_rand(2 * F, H, scale=0.05, seed=191 + e)) for e in range(E)]
+    w2 = [_rand(H, F, scale=0.05, seed=201 + e) for e in range(E)]
+    h = torch.full((R, F), 5.0, dtype=torch.bfloat16, device=DEV)
+    y = torch.full((R, H), 7.0, dtype=torch.bfloat16, device=DEV)
+    ext = ops.ext()
+    wp13 = torch.tensor([w.data_ptr() for w in w13], dtype=torch.int64, device=DEV)
+    wp2 = torch.tensor([w.data_ptr() for w in w2], dtype=torch.int64, device=DEV)
+    ext.gemm_grouped(x, w13, wp13, off, 4, h, [], None, config)
+    ext.gemm_grouped(h, w2, wp2, off, 0, y, [], None, config)
+    torch.cuda.synchronize()
+    o = off.tolist()
+    for e in range(E):
+        r0, r1 = o[e], o[e + 1]
+        if r1 > r0:
+            href = ops.ref_linear(x[r0:r1].cpu(), w13[e].cpu(), act="swiglu")
+            _close(h[r0:r1].cpu(), href.float(), 2e-2)
+            _close(y[r0:r1].cpu(), ops.ref_linear(h[r0:r1].cpu(), w2[e].cpu()).float(), 2e-2)
+    assert (h[o[-1]:].cpu().float() == 5.0).all() and (y[o[-1]:].cpu().float() == 7.0).all()
+
+
 @pytest.mark.parametrize("M,E,k", [(300, 8, 2), (512, 8, 2), (1500, 8, 2), (200, 64, 8), (777, 16, 1)])
 def test_moe_route_fused_equals_router_align(M, E, k):
     """The one-workgroup route kernel returns exactly what moe_router + moe_align return."""
