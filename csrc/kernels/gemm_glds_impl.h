@@ -990,10 +990,13 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
       tn = pair % tiles_n;
       t0 = (blockIdx.x >> 3) & 1;
       dt = 2;
-    } else if (ep.w_stream & 32) {
-      // (the odd partners as a second half of the grid: dispatched after every even block)
+    } else if (ep.w_stream & (32 | 64)) {
+      // the odd partners as one half of the grid: dispatched after every even block (bit 32) or
+      // before them (bit 64). A heavy expert's second row tile then runs on a CU of its own, in
+      // parallel with its first, where the serial walk doubled its blocks' time: Mixtral-8x7B
+      // 24.74 -> 23.58 ms per step (profiles/r6_ab/expert_pairs.txt)
       const int half = gridDim.x >> 1;
-      t0 = blockIdx.x >= half;
+      t0 = (blockIdx.x >= half) == ((ep.w_stream & 32) != 0);
       dt = 2;
       g = (blockIdx.x - t0 * half) / tiles_n;
       tn = (blockIdx.x - t0 * half) % tiles_n;
@@ -1274,18 +1277,18 @@ void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned
   }();
   // (the nt path DMAs the A rows by buffer loads with 32-bit offsets: an A of 2 GB or more
   // takes the default path)
-  // row-split pairs (kernel: RANGED == 3): DLS_EXPERT_PAIRS=1 same-XCD partners, 2 partners in a
-  // second half of the grid; 0 (default) walks every row tile in one block
+  // row-split pairs (kernel: RANGED == 3): DLS_EXPERT_PAIRS=0 one block walks every row tile,
+  // 1 same-XCD partners, 2 (default) partners in the grid's second half, 3 in its first half
   // (read per launch — a captured step replays without it — so a test can switch modes)
   const char* pe = std::getenv("DLS_EXPERT_PAIRS");
-  const int pairs = pe && *pe ? std::atoi(pe) : 0;
+  const int pairs = pe && *pe ? std::atoi(pe) : 2;
   const int pair = a.grouped_shared ? 0 : pairs;
   const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs,
                (a.grouped_shared ? 8 : ((size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0)) |
-                   (pair == 1 ? 16 : pair == 2 ? 32 : 0)};
+                   (pair == 1 ? 16 : pair == 2 ? 32 : pair == 3 ? 64 : 0)};
   const int tiles_n = (a.N + C::BN - 1) / C::BN;
-  const int blocks = pair == 1 ? (n_groups * tiles_n + 7) / 8 * 16 : pair == 2 ? 2 * n_groups * tiles_n
-                                                                                : n_groups * tiles_n;
+  const int blocks = pair == 1 ? (n_groups * tiles_n + 7) / 8 * 16 : pair >= 2 ? 2 * n_groups * tiles_n
+                                                                               : n_groups * tiles_n;
   // (tiles_m carries the group count: the paired walk bounds its pair index by it)
   hipLaunchKernelGGL((gemm_glds_kernel<C, 0, 3>), dim3(blocks), dim3(C::T), 0, s, (const bf16*)a.A, a.lda,
                      nullptr, a.ldw, (bf16*)a.C, a.ldc, nullptr, nullptr, 0,
