@@ -995,11 +995,11 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
       // before them (bit 64). A heavy expert's second row tile then runs on a CU of its own, in
       // parallel with its first, where the serial walk doubled its blocks' time: Mixtral-8x7B
       // 24.74 -> 23.58 ms per step (profiles/r6_ab/expert_pairs.txt)
-      const int half = gridDim.x >> 1;
-      t0 = (blockIdx.x >= half) == ((ep.w_stream & 32) != 0);
+      const int half = gridDim.x >> 1, second = blockIdx.x >= half, idx = blockIdx.x - second * half;
+      t0 = second == ((ep.w_stream & 32) != 0);
       dt = 2;
-      g = (blockIdx.x - t0 * half) / tiles_n;
-      tn = (blockIdx.x - t0 * half) % tiles_n;
+      g = idx / tiles_n;
+      tn = idx % tiles_n;
     }
     const int r0 = rows[g], cnt = rows[g + 1] - r0;
     const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
