@@ -149,8 +149,12 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     pg = runtime.p2p_group(plan, ctx.rank, ctx.device, ctx.pg, transport) if ctx.gpu else ctx.pg
     ex = runtime.make_executor(plan, ctx.rank, ctx.device, store, pg=pg, use_graph=use_graph, trace=roctx)
     log(f"[bench{tag}] rank {ctx.rank}: executor ready in {(time.time() - t0):.1f} s (device_init={dev_init})")
-    for _ in range(warmup):
-        ex.step()
+    # one eager step first (lazy initialisation, first-step weight transforms; what the capture
+    # records), then the W warmup steps run the step exactly as it is timed — the captured
+    # hipGraph when there is one — so the GPU enters the timed window in its steady state
+    # (W eager steps left it idle behind the Python issue loop: 20 timed steps after them
+    # measured 0.620-0.628 ms against 0.605 ms for 200, profiles/r6_status/short_window.txt)
+    ex.step()
     ctx.sync()
     # expert-parallel capacity edges whose routing overflowed: widened on both of their ranks,
     # then the step runs again (repeat: a corrected layer can change a later layer's routing)
@@ -162,7 +166,7 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     captured = ex.capture() if use_graph else False
     if captured and refine:
         log(f"[bench{tag}] rank {ctx.rank}: in-DAG GEMM refinement: {ex.refine_tuning()}")
-    if captured:
+    for _ in range(warmup):
         ex.step()
     ctx.sync()
     ex.reset_transport_errors()  # device transport: a cold first step may outlast a peer's wait
