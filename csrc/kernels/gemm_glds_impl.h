@@ -1001,6 +1001,18 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
       g = idx / tiles_n;
       tn = idx % tiles_n;
     }
+    if ((ep.w_stream & 128) && !(ep.w_stream & (8 | 16))) {
+      // XCD-affine walk (w_stream bit 128): blocks on XCD x (index % 8 under round-robin
+      // dispatch) take a CONTIGUOUS run of the (group, column panel) order, so an XCD works
+      // through one expert's panels at a time and that expert's rows stay in ITS L2 — the
+      // plain order spreads every expert's blocks over all eight XCDs, and each L2 then holds
+      // all eight experts' rows (Mixtral down: 8 x 3.7 MB against a 4 MB L2)
+      const int total = tiles_m * tiles_n, idx = g * tiles_n + tn;
+      const int x = idx & 7, j = idx >> 3, q = total >> 3, r = total & 7;
+      const int L = x * q + min(x, r) + j;
+      g = L / tiles_n;
+      tn = L % tiles_n;
+    }
     const int r0 = rows[g], cnt = rows[g + 1] - r0;
     const int Mr = compact_rows ? min(cnt, compact_rows) : cnt;
     const bf16* Wg = reinterpret_cast<const bf16*>(ep.grp_w[g]);
@@ -1283,9 +1295,12 @@ void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned
   const char* pe = std::getenv("DLS_EXPERT_PAIRS");
   const int pairs = pe && *pe ? std::atoi(pe) : 2;
   const int pair = a.grouped_shared ? 0 : pairs;
+  // DLS_EXPERT_XCD=1: XCD-affine block order (kernel: RANGED == 3)
+  const char* xe = std::getenv("DLS_EXPERT_XCD");
+  const bool xcd = xe && *xe == '1' && !a.grouped_shared && pair != 1;
   const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs,
                (a.grouped_shared ? 8 : ((size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0)) |
-                   (pair == 1 ? 16 : pair == 2 ? 32 : pair == 3 ? 64 : 0)};
+                   (pair == 1 ? 16 : pair == 2 ? 32 : pair == 3 ? 64 : 0) | (xcd ? 128 : 0)};
   const int tiles_n = (a.N + C::BN - 1) / C::BN;
   const int blocks = pair == 1 ? (n_groups * tiles_n + 7) / 8 * 16 : pair >= 2 ? 2 * n_groups * tiles_n
                                                                                : n_groups * tiles_n;
