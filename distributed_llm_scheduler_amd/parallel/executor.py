@@ -2036,6 +2036,7 @@ class DAGExecutor:
         if self._copy_stream is not None or (self.prog.has_comm and not self._device_p2p):
             return self.capture_segments()
         self._sync()
+        self._retire_native()
         if self._device_p2p:
             # (on this rank's own stream: a warm step spinning on a peer's flag from a pooled side
             # stream could share a hardware queue with that peer's stream — parallel/loopback.py)
@@ -2082,6 +2083,17 @@ class DAGExecutor:
         for st in (self._copy_stream, self._cap_stream):
             if st is not None:
                 st.synchronize()
+
+    def _retire_native(self) -> None:
+        """Before a (re-)capture, after a device synchronize: the graphs / runner of the previous
+        capture are replaced — hand them to the graveyard (destroyed at a quiesce point; on the
+        main thread right away) instead of keeping every capture alive until the executor dies."""
+        self._graph = self._graph_exec = None
+        self._segments = {}
+        self._drop_runner()
+        self._fast = None
+        lifetime.retire(self)
+        lifetime.release_on_main_thread()
 
     def _drop_runner(self) -> None:
         self._runner = None
@@ -2235,6 +2247,7 @@ class DAGExecutor:
                 self.step()
             return False
         self._sync()
+        self._retire_native()
         self._capture_plan = {a: b for a, b in segs}
         self._seg_pool = torch.cuda.graph_pool_handle()
         self._step_body(StepStats())  # segments captured in order as the step reaches them

@@ -49,6 +49,30 @@ def keep(owner, obj) -> object:
     return obj
 
 
+def retire(owner) -> int:
+    """The owner replaces its native objects (a re-capture, a rebuilt runner): move the ones kept
+    so far to the graveyard — destroyed at the next :func:`release`, never here. The caller must
+    not use them any more and must have synchronised with their last launches. Returns the
+    count moved."""
+    lst = owner.__dict__.get("_native_keep")
+    if not lst:
+        return 0
+    with _LOCK:
+        _GRAVE.extend(lst)
+    n = len(lst)
+    lst.clear()
+    return n
+
+
+def release_on_main_thread() -> int:
+    """:func:`release` when called on the main thread (rank threads of the single-GPU harness
+    capture inside :func:`quiesced`, where release is a no-op anyway): keeps a long-lived
+    executor that re-captures many times (in-DAG tuning) from accumulating dead graphs."""
+    if threading.current_thread() is not threading.main_thread():
+        return 0
+    return release()
+
+
 def graveyard_size() -> int:
     with _LOCK:
         return len(_GRAVE)

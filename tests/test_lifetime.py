@@ -64,6 +64,25 @@ def test_quiesced_collects_first_and_pauses_the_collector():
     assert lifetime.release() == 1 and _Res.destroyed == ["old", "new"]
 
 
+def test_retired_objects_wait_for_release():
+    """A re-capture replaces an executor's graphs: the old ones go to the graveyard (not
+    destroyed on the spot), the owner keeps only what it registers afterwards."""
+    lifetime.release()
+    _Res.destroyed.clear()
+    o = _Owner()
+    lifetime.keep(o, _Res("old1"))
+    lifetime.keep(o, _Res("old2"))
+    assert lifetime.retire(o) == 2 and _Res.destroyed == [] and lifetime.graveyard_size() == 2
+    lifetime.keep(o, _Res("new"))
+    assert len(o.__dict__["_native_keep"]) == 1
+    with lifetime.quiesced():  # (collects and releases on entry) ...
+        lifetime.keep(o, _Res("new2"))
+        assert lifetime.retire(o) == 2
+        assert lifetime.release_on_main_thread() == 0  # ... and not inside the section
+    assert sorted(_Res.destroyed) == ["old1", "old2"]
+    assert lifetime.release_on_main_thread() == 2 and sorted(_Res.destroyed) == ["new", "new2", "old1", "old2"]
+
+
 def test_executor_graphs_are_kept_by_the_executor():
     """The executor registers every hipGraph and native runner it builds (CPU: the runner)."""
     from distributed_llm_scheduler_amd.parallel import executor as exm
