@@ -237,6 +237,77 @@ def run(ctx: Ctx, steps: int, warmup: int, *, model, scheduler, cap_gb, replicas
     return res
 
 
+DEVICE_P2P_KEYS = ("ms_per_step", "per_rank_ms", "hip_graph", "launches_per_rank", "p2p_errors", "cross_gpu_bytes")
+
+
+def device_p2p_child(ctx: Ctx, args) -> None:
+    """``--device-p2p-child``: one rank of the isolated strong device-p2p sub-run (started by
+    :func:`run_device_p2p_children`); rank 0 prints the sub-result as one JSON line."""
+    merge = args.strong_mb if args.strong_merge else 1
+    if os.environ.get("DLS_TEST_CHILD_ABORT") == str(ctx.rank):
+        os.abort()  # (tests: a child that dies as a GPU fault would end it)
+    try:
+        r = run(ctx, args.extra_steps, min(args.warmup, 2), model=args.model, batch=args.batch, seq=args.seq,
+                fuse=not args.no_fuse, use_graph=not args.no_graph, scheduler="EFT", cap_gb=288.0,
+                replicas=args.strong_mb, cost_model="bytes", placement="pipeline", tag=":strong-devp2p",
+                merge_mb=merge, transport="device" if ctx.gpu else None)
+        out = {k: r[k] for k in DEVICE_P2P_KEYS}
+    except Exception as e:  # noqa: BLE001 — reported to the parent, which records it
+        log(f"[bench] rank {ctx.rank}: device-p2p child failed: {e!r}")
+        out = {"error": repr(e)[:300]}
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+    if ctx.world > 1:
+        dist.destroy_process_group()
+
+
+def run_device_p2p_children(ctx: Ctx, budget_s: float):
+    """Every rank starts one child process of this script in ``--device-p2p-child`` mode — the
+    children form a job of their own (a fresh rendezvous port from rank 0) — and waits for it
+    at most ``budget_s`` seconds. Returns rank 0's child's sub-result (None on other ranks); a
+    child that crashes, or a job that does not finish in time, becomes an ``error`` entry."""
+    import socket
+    import subprocess
+
+    if budget_s < 30:
+        raise RuntimeError(f"no time left for the isolated sub-run ({budget_s:.0f} s)")
+    port = [0]
+    if ctx.rank == 0:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port[0] = s.getsockname()[1]
+        s.close()
+    dist.broadcast_object_list(port, src=0)
+    if ctx.gpu:
+        torch.cuda.synchronize(ctx.device)
+        gc.collect()
+        torch.cuda.empty_cache()  # the parent's cached blocks: HBM the child may need
+    # (torchrun's agent-store variables would make the children's rank 0 a CLIENT of a store
+    # that does not exist on the new port)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(RANK=str(ctx.rank), WORLD_SIZE=str(ctx.world), MASTER_PORT=str(port[0]),
+               MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"))
+    argv = [a for a in sys.argv[1:] if a != "--device-p2p-child"]
+    err, out = None, ""
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), *argv, "--device-p2p-child"], env=env,
+                           stdout=subprocess.PIPE, text=True, timeout=budget_s)
+        out = r.stdout or ""
+        if r.returncode != 0:
+            err = f"child exited {r.returncode}"
+    except subprocess.TimeoutExpired:
+        err = f"child unfinished after {budget_s:.0f} s"
+    bad = ctx.gather_list(1.0 if err else 0.0)
+    ctx.sync()
+    if ctx.rank != 0:
+        return None
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    res = json.loads(lines[-1]) if lines else {}
+    if err or any(bad):
+        res.setdefault("error", err or f"child failed on rank(s) {[i for i, b in enumerate(bad) if b]}")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -275,6 +346,10 @@ def main():
                     help="run the strong sub-result's micro-batches as separate M = 512 chains (not merged)")
     ap.add_argument("--no-device-p2p-extra", dest="device_p2p_extra", action="store_false",
                     help="N > 1: skip the strong sub-result repeated over the device p2p transport")
+    ap.add_argument("--device-p2p-extra-cpu", action="store_true",
+                    help="(tests) run the isolated device-p2p sub-run's plumbing on CPU ranks too (gloo, the "
+                         "strong pipeline over the host transport)")
+    ap.add_argument("--device-p2p-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--merge-mb", type=int, default=1,
                     help="headline: merge this many request replicas into one batched request (plan merge_mb)")
     ap.add_argument("--extras-timeout", type=float, default=180.0,
@@ -307,6 +382,9 @@ def main():
         init_world(rank, world, device if gpu else None)  # RCCL bound to this GPU + one barrier
         pg = dist.group.WORLD
     ctx = Ctx(world, rank, device, gpu, pg)
+    if args.device_p2p_child:
+        device_p2p_child(ctx, args)
+        return
 
     replicas = args.replicas if args.replicas is not None else world * args.replicas_per_gpu
     if replicas < 1:
@@ -411,6 +489,7 @@ def main():
                 sys.stderr.flush()
                 os._exit(0)
 
+    t_extras = time.time()
     if not args.no_extras:
         threading.Thread(target=watchdog, daemon=True).start()
     if not args.no_extras:
@@ -469,18 +548,21 @@ def main():
         except Exception as e:  # noqa: BLE001
             log(f"[bench] strong sub-run failed: {e!r}")
             strong["error"] = repr(e)[:300]
-        if world > 1 and gpu and args.device_p2p_extra:
+        if world > 1 and (gpu or args.device_p2p_extra_cpu) and args.device_p2p_extra:
             # the same strong pipeline with its edges moved by kernels (parallel/devp2p.py): each
-            # rank's whole step ONE hipGraph; peers' arenas mapped over xGMI through IPC handles
-            sd = {"transport": "device", "micro_batches": args.strong_mb, "micro_batches_merged": merge}
+            # rank's whole step ONE hipGraph; peers' arenas mapped over xGMI through IPC handles.
+            # Never yet run across GPUs: it runs in CHILD processes (one per rank, a job of their
+            # own), so a fault there costs this sub-result, not the headline line
+            sd = {"transport": "device", "micro_batches": args.strong_mb, "micro_batches_merged": merge,
+                  "isolated": True}
             extras["strong_device_p2p"] = sd
+            budget = args.extras_timeout - (time.time() - t_extras) - 20.0
             try:
-                r = run(ctx, args.extra_steps, ew, scheduler="EFT", cap_gb=288.0, replicas=args.strong_mb,
-                        cost_model="bytes", placement="pipeline", tag=":strong-devp2p", merge_mb=merge,
-                        transport="device", **common)
-                sd.update({k: r[k] for k in ("ms_per_step", "per_rank_ms", "hip_graph", "launches_per_rank",
-                                             "p2p_errors", "cross_gpu_bytes")})
-                sd["valid"] = not any(r["p2p_errors"])
+                r = run_device_p2p_children(ctx, budget)
+                if r is not None:  # rank 0
+                    sd.update(r)
+                    if "p2p_errors" in r:
+                        sd["valid"] = not any(r["p2p_errors"])
             except Exception as e:  # noqa: BLE001
                 log(f"[bench] strong device-p2p sub-run failed: {e!r}")
                 sd["error"] = repr(e)[:300]

@@ -58,6 +58,38 @@ def test_bench_two_ranks_gloo():
     _check(lines[0], 2)
 
 
+@pytest.mark.timeout(300)
+def test_bench_isolated_device_p2p_subrun_under_torchrun():
+    """The strong device-p2p sub-result runs in child processes that form a job of their own (a
+    fault there must not cost the headline line): under torchrun (agent store variables in the
+    environment) the children rendezvous on rank 0's new port, rank 0's child result lands in
+    the ONE line, marked isolated."""
+    lines = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                  "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *ARGS,
+                  "--extra-steps", "2", "--device-p2p-extra-cpu"])
+    assert len(lines) == 1
+    _check(lines[0], 2)
+    sd = lines[0]["strong_device_p2p"]
+    assert sd["isolated"] and "error" not in sd, sd
+    assert sd["ms_per_step"] > 0 and len(sd["per_rank_ms"]) == 2 and sd["cross_gpu_bytes"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_isolated_device_p2p_subrun_crash_keeps_the_headline(monkeypatch):
+    """Rank 1's child aborts (as a GPU fault would end it): rank 0's child loses its peer (or, on a
+    transport that only hangs, is stopped at the sub-run's time budget); the job still prints its
+    ONE line, with the sub-result's error recorded."""
+    monkeypatch.setenv("DLS_TEST_CHILD_ABORT", "1")
+    lines = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                  "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *ARGS,
+                  "--extra-steps", "2", "--device-p2p-extra-cpu", "--extras-timeout", "90"])
+    assert len(lines) == 1
+    _check(lines[0], 2)
+    sd = lines[0]["strong_device_p2p"]
+    assert "error" in sd and "ms_per_step" not in sd, sd
+    assert lines[0]["strong"]["ms_per_step"] > 0  # the other sub-results stand
+
+
 def _torchrun(n, args):
     return _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                  "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n), *args])
