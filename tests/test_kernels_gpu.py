@@ -364,14 +364,24 @@ def test_gemm_grouped_heavy_expert(config, pairs, xcd, monkeypatch):
     wp2 = torch.tensor([w.data_ptr() for w in w2], dtype=torch.int64, device=DEV)
     ext.gemm_grouped(x, w13, wp13, off, 4, h, [], None, config)
     ext.gemm_grouped(h, w2, wp2, off, 0, y, [], None, config)
+    # the gate/up launch gathering its rows from a token matrix (the Mixtral step's form): sorted
+    # row r reads token a_rows[r]
+    n = sum(counts)
+    g = torch.Generator().manual_seed(5)
+    a_rows = torch.randint(0, 300, (n,), generator=g).to(torch.int32).to(DEV)
+    tok = _rand(300, H, seed=189)
+    hg = torch.full((n, F), 3.0, dtype=torch.bfloat16, device=DEV)  # (out rows = a_rows' count)
+    ext.gemm_grouped(tok, w13, wp13, off, 4, hg, [], None, config, a_rows)
     torch.cuda.synchronize()
     o = off.tolist()
+    xs = tok.cpu()[a_rows.cpu().long()]
     for e in range(E):
         r0, r1 = o[e], o[e + 1]
         if r1 > r0:
             href = ops.ref_linear(x[r0:r1].cpu(), w13[e].cpu(), act="swiglu")
             _close(h[r0:r1].cpu(), href.float(), 2e-2)
             _close(y[r0:r1].cpu(), ops.ref_linear(h[r0:r1].cpu(), w2[e].cpu()).float(), 2e-2)
+            _close(hg[r0:r1].cpu(), ops.ref_linear(xs[r0:r1], w13[e].cpu(), act="swiglu").float(), 2e-2)
     assert (h[o[-1]:].cpu().float() == 5.0).all() and (y[o[-1]:].cpu().float() == 7.0).all()
 
 
