@@ -943,6 +943,20 @@ __device__ __forceinline__ void glds_tile(bf16x8* smem, const bf16* __restrict__
 // tile walk it needs (the folded-norm statistics and the row-range loop cost registers).
 // POL (plain tiles only): streaming (nt) cache policy of the weight DMA (bit 0, split rings)
 // and of the output stores (bit 1) — GemmArgs::stream_pol
+// Grouped expert launches: a TALLER tile of the same column width that takes an expert whose
+// routed rows overflow C's tile but fit this one in ONE pass over its weight panel (instead of
+// a partner block streaming the whole panel again for a few rows). void: none. Specialised
+// below the tile configs; enabled by w_stream bit 256 (DLS_EXPERT_TALL).
+template <class C>
+struct TallTile {
+  using type = void;
+};
+template <class C>
+constexpr int tall_lds_units() {
+  if constexpr (std::is_void_v<typename TallTile<C>::type>) return 0;
+  else return TallTile<C>::type::LDS_UNITS;
+}
+
 template <class C, int LN, int RANGED, int POL = 0>
 __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __restrict__ A, int lda,
                                                          const bf16* __restrict__ W, int ldw, bf16* __restrict__ Cp,
@@ -953,7 +967,8 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
                                                          int kslice, const float* __restrict__ ln_colsum,
                                                          int ln_mode, float ln_eps, const int* __restrict__ rows,
                                                          int compact_rows, Epi ep) {
-  __shared__ bf16x8 smem[C::LDS_UNITS];
+  constexpr int kUnits = RANGED == 3 && tall_lds_units<C>() > C::LDS_UNITS ? tall_lds_units<C>() : C::LDS_UNITS;
+  __shared__ bf16x8 smem[kUnits];
   const int ntile = tiles_m * tiles_n;
   if constexpr (RANGED == 2) {
     // persistent: a resident grid walks the tiles; tile t+1's first K-tiles are issued right
@@ -1023,6 +1038,30 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
     const int* a_rows = reinterpret_cast<const int*>(part);
     const int* ag = a_rows ? a_rows + r0 : nullptr;
     const bf16* Ag = a_rows ? A : A + (size_t)r0 * lda;
+    if constexpr (!std::is_void_v<typename TallTile<C>::type>) {
+      using T2 = typename TallTile<C>::type;
+      static_assert(T2::BN == C::BN && T2::BM > C::BM && T2::T == C::T, "a taller tile of the same panel");
+      if ((ep.w_stream & 256) && Mr > C::BM && Mr <= T2::BM) {
+        if (t0 != 0) return;  // a partner block: the tall tile takes the expert's whole range
+        const bool nt = T2::BXS > 0 && (ep.w_stream & 1);
+        if (a_rows) {
+          if (nt)
+            glds_tile<T2, 0, kPolStream, true, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M,
+                                                     N, K, act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
+          else
+            glds_tile<T2, 0, 0, false, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K,
+                                             act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
+        } else {
+          if (nt)
+            glds_tile<T2, 0, kPolStream, true, false>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr,
+                                                      M, N, K, act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
+          else
+            glds_tile<T2, 0, 0, false, false>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K,
+                                              act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
+        }
+        return;
+      }
+    }
 #define DLS_GROUPED_WALK(GA)                                                                                      \
   for (int t = t0; t * C::BM < Mr; t += dt) {                                                                      \
     if (t != t0) raw_barrier(); /* every wave is done reading the staging buffers of the previous tile */          \
@@ -1278,6 +1317,15 @@ using C47 = Cfg<128, 128, 2, 2, 2, 0, 1, 1, 0, 2>;
 // (and the MoE experts' 192 x 128 tile with two K groups, 16 waves: Mixtral 28.7 / 42.6 ms
 // with it on down / gate-up against 24.3 — profiles/r4_ab/moe_gateup_cfg44.txt)
 
+// the Mixtral down tile's taller form (busiest expert per layer: 149-227 routed rows,
+// profiles/r6_mixtral/rows_vs_time.txt): 192 -> 256 rows (config 14; the grouped kernel keeps
+// 241 VGPRs, no scratch). The gate/up tile's (160 -> 224 rows, wave 112 x 64) spilled 68 VGPRs
+// in the grouped kernel: not instantiated.
+template <>
+struct TallTile<C33> {
+  using type = C14;
+};
+
 template <class C>
 void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned long long* w_ptrs,
              const unsigned long long* c_ptrs, hipStream_t s, const int* a_rows) {
@@ -1298,9 +1346,13 @@ void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned
   // DLS_EXPERT_XCD=1: XCD-affine block order (kernel: RANGED == 3)
   const char* xe = std::getenv("DLS_EXPERT_XCD");
   const bool xcd = xe && *xe == '1' && !a.grouped_shared && pair != 1;
+  // DLS_EXPERT_TALL=1: an expert past the tile's rows but within its TallTile's takes one taller
+  // pass (configs with a TallTile only)
+  const char* te = std::getenv("DLS_EXPERT_TALL");
+  const bool tall = te && *te == '1' && !a.grouped_shared;
   const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs,
                (a.grouped_shared ? 8 : ((size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0)) |
-                   (pair == 1 ? 16 : pair == 2 ? 32 : pair == 3 ? 64 : 0) | (xcd ? 128 : 0)};
+                   (pair == 1 ? 16 : pair == 2 ? 32 : pair == 3 ? 64 : 0) | (xcd ? 128 : 0) | (tall ? 256 : 0)};
   const int tiles_n = (a.N + C::BN - 1) / C::BN;
   const int blocks = pair == 1 ? (n_groups * tiles_n + 7) / 8 * 16 : pair >= 2 ? 2 * n_groups * tiles_n
                                                                                : n_groups * tiles_n;

@@ -337,19 +337,22 @@ def test_gemm_grouped_experts(config):
         assert (outs[e][min(r1 - r0, cap):].cpu().float() == 7.0).all(), "rows past the expert's count were written"
 
 
+@pytest.mark.parametrize("tall", ["0", "1"])
 @pytest.mark.parametrize("xcd", ["0", "1"])
 @pytest.mark.parametrize("pairs", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("config", [-1, 17, 31, 33, 41, 44, 46])
-def test_gemm_grouped_heavy_expert(config, pairs, xcd, monkeypatch):
+def test_gemm_grouped_heavy_expert(config, pairs, xcd, tall, monkeypatch):
     """Experts with several row tiles (450 rows: three 160-row tiles, three 192-row tiles, eight
     64-row tiles) next to tiny and empty ones: the row-split pairs of a grouped launch (even row
     tiles in one block, odd in its same-XCD partner) cover every row exactly once — against
     per-expert fp32 references, untouched rows past the last expert. DLS_EXPERT_PAIRS: 0 one
     block walks all of (expert, column panel)'s row tiles, 1 same-XCD partner blocks, 2 partners
     in the grid's second half (the default), 3 in its first half; DLS_EXPERT_XCD=1 the XCD-affine
-    block order (6 groups: not a multiple of the 8 XCDs)."""
+    block order (6 groups: not a multiple of the 8 XCDs); DLS_EXPERT_TALL=1 one taller tile for an
+    expert within it (config 33's 192 rows -> 256: the 200-row expert)."""
     monkeypatch.setenv("DLS_EXPERT_PAIRS", pairs)
     monkeypatch.setenv("DLS_EXPERT_XCD", xcd)
+    monkeypatch.setenv("DLS_EXPERT_TALL", tall)
     H, F = 256, 384
     counts = [20, 450, 0, 200, 7, 161]
     E, R = len(counts), sum(counts) + 16
