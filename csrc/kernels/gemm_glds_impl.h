@@ -1346,10 +1346,11 @@ void grouped(const GemmArgs& a, int n_groups, const int* offsets, const unsigned
   // DLS_EXPERT_XCD=1: XCD-affine block order (kernel: RANGED == 3)
   const char* xe = std::getenv("DLS_EXPERT_XCD");
   const bool xcd = xe && *xe == '1' && !a.grouped_shared && pair != 1;
-  // DLS_EXPERT_TALL=1: an expert past the tile's rows but within its TallTile's takes one taller
-  // pass (configs with a TallTile only)
+  // DLS_EXPERT_TALL (default 1): an expert past the tile's rows but within its TallTile's takes
+  // one taller pass (configs with a TallTile only): Mixtral-8x7B 24.18-24.25 -> 23.72-23.81 ms
+  // (profiles/r6_ab/expert_tall_tile.txt)
   const char* te = std::getenv("DLS_EXPERT_TALL");
-  const bool tall = te && *te == '1' && !a.grouped_shared;
+  const bool tall = !(te && *te == '0') && !a.grouped_shared;
   const Epi ep{a.rope, nullptr, nullptr, nullptr, w_ptrs, c_ptrs,
                (a.grouped_shared ? 8 : ((size_t)a.M * a.lda * 2 < (1ull << 31) ? w_stream : 0)) |
                    (pair == 1 ? 16 : pair == 2 ? 32 : pair == 3 ? 64 : 0) | (xcd ? 128 : 0) | (tall ? 256 : 0)};
