@@ -186,8 +186,12 @@ def _run_loopback(plan, device, steps, warmup, capture, delay_us, poison, store,
                     issue += time.perf_counter() - a
                 host_us[r] = issue / max(steps, 1) * 1e6
                 start.wait()
-                if sync_debug and gpu and r == 0:
-                    torch.cuda.set_sync_debug_mode(0)
+                if sync_debug and gpu:
+                    if r == 0:
+                        torch.cuda.set_sync_debug_mode(0)
+                    # (process-wide mode: no rank synchronises before rank 0 has switched it off —
+                    # rank 2's stream synchronize once raced ahead of it)
+                    start.wait()
                 if gpu:
                     streams[r].synchronize()
                 ms[r] = (time.perf_counter() - t0) / max(steps, 1) * 1e3
