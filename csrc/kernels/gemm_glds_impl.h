@@ -1039,25 +1039,34 @@ __global__ __launch_bounds__(C::T, C::OCC) void gemm_glds_kernel(const bf16* __r
     const int* ag = a_rows ? a_rows + r0 : nullptr;
     const bf16* Ag = a_rows ? A : A + (size_t)r0 * lda;
     if constexpr (!std::is_void_v<typename TallTile<C>::type>) {
+      // SPLIT = 2: the taller tile is half as wide — the block and its partner each take one half
+      // of the column panel over ALL of the expert's rows (each streams half the panel once; in
+      // the serial walk without partners the block takes both halves in turn)
       using T2 = typename TallTile<C>::type;
-      static_assert(T2::BN == C::BN && T2::BM > C::BM && T2::T == C::T, "a taller tile of the same panel");
+      constexpr int SPLIT = C::BN / T2::BN;
+      static_assert((SPLIT == 1 || SPLIT == 2) && T2::BN * SPLIT == C::BN && T2::BM > C::BM && T2::T == C::T,
+                    "a taller tile of the same panel (or of half of it)");
       if ((ep.w_stream & 256) && Mr > C::BM && Mr <= T2::BM) {
-        if (t0 != 0) return;  // a partner block: the tall tile takes the expert's whole range
         const bool nt = T2::BXS > 0 && (ep.w_stream & 1);
-        if (a_rows) {
-          if (nt)
-            glds_tile<T2, 0, kPolStream, true, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M,
-                                                     N, K, act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
-          else
-            glds_tile<T2, 0, 0, false, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K,
-                                             act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
-        } else {
-          if (nt)
-            glds_tile<T2, 0, kPolStream, true, false>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr,
-                                                      M, N, K, act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
-          else
-            glds_tile<T2, 0, 0, false, false>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N, K,
-                                              act, alpha, 0, K, 0, tn, ln_colsum, 0, ln_eps, ep, ag);
+        for (int hh = t0; hh < SPLIT; hh += dt) {  // (SPLIT 1: a partner block has nothing to do)
+          if (hh != t0) raw_barrier();
+          const int tn2 = tn * SPLIT + hh;
+          if (a_rows) {
+            if (nt)
+              glds_tile<T2, 0, kPolStream, true, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr,
+                                                       M, N, K, act, alpha, 0, K, 0, tn2, ln_colsum, 0, ln_eps, ep, ag);
+            else
+              glds_tile<T2, 0, 0, false, true>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N,
+                                               K, act, alpha, 0, K, 0, tn2, ln_colsum, 0, ln_eps, ep, ag);
+          } else {
+            if (nt)
+              glds_tile<T2, 0, kPolStream, true, false>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr,
+                                                        Mr, M, N, K, act, alpha, 0, K, 0, tn2, ln_colsum, 0, ln_eps, ep,
+                                                        ag);
+            else
+              glds_tile<T2, 0, 0, false, false>(smem, Ag, lda, Wg, ldw, Cg, ldc, bias, nullptr, 0, nullptr, Mr, M, N,
+                                                K, act, alpha, 0, K, 0, tn2, ln_colsum, 0, ln_eps, ep, ag);
+          }
         }
         return;
       }
@@ -1321,6 +1330,12 @@ using C47 = Cfg<128, 128, 2, 2, 2, 0, 1, 1, 0, 2>;
 // profiles/r6_mixtral/rows_vs_time.txt): 192 -> 256 rows (config 14; the grouped kernel keeps
 // 241 VGPRs, no scratch). The gate/up tile's (160 -> 224 rows, wave 112 x 64) spilled 68 VGPRs
 // in the grouped kernel: not instantiated.
+// gate/up (160 x 256): 224 x 256 (wave 112 x 64, split rings 2 x 28 KiB A + 3 x 32 KiB W) — the
+// grouped kernel spills 68 VGPRs with it (a 320 x 128 half-panel form spilled 132-172)
+template <>
+struct TallTile<C44> {
+  using type = Cfg<224, 256, 2, 4, 2, 0, 1>;
+};
 template <>
 struct TallTile<C33> {
   using type = C14;
