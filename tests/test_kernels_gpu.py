@@ -349,7 +349,7 @@ def test_gemm_grouped_heavy_expert(config, pairs, xcd, tall, monkeypatch):
     block walks all of (expert, column panel)'s row tiles, 1 same-XCD partner blocks, 2 partners
     in the grid's second half (the default), 3 in its first half; DLS_EXPERT_XCD=1 the XCD-affine
     block order (6 groups: not a multiple of the 8 XCDs); DLS_EXPERT_TALL=1 one taller tile for an
-    expert within it (config 33's 192 rows -> 256: the 200-row expert)."""
+    expert within it (config 33's 192 rows -> 256 and config 44's 160 -> 224: the 161- and 200-row experts)."""
     monkeypatch.setenv("DLS_EXPERT_PAIRS", pairs)
     monkeypatch.setenv("DLS_EXPERT_XCD", xcd)
     monkeypatch.setenv("DLS_EXPERT_TALL", tall)
